@@ -1,0 +1,317 @@
+"""br-archive_amd -- host-side mirror of br-archive's encoder interface on the MI355X block codec.
+
+The product is ``libbra_hip.so`` (C-ABI in ``include/bra_hip.h``; HIP kernels for gfx950 under
+``csrc/``).  This module only binds it:
+
+* the reference's encoder functions (``src/encoders/bra_{bwt,mtf,rle,huffman}.h``) with the same
+  names, argument meaning and failure behaviour (``None``/``False`` where the C function returns
+  ``NULL``/``false``), one block per call on host buffers;
+* :class:`BlockCodec`, the batched device-resident API (``bra_gpu_encode_blocks`` /
+  ``bra_gpu_decode_blocks``) on torch tensors that already live in HBM.
+
+There is no CPU implementation here: importing raises if the HIP library is missing or was not
+built, and every call runs on the GPU.  (The CPU restatement used to check results lives in the
+top-level ``oracle/`` package, which this package never imports.)
+
+Import with ``importlib.import_module("br-archive_amd")`` (the directory name carries a hyphen).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbra_hip.so")
+SYNTH_PATH = os.path.join(HERE, "libbra_synth.so")
+
+# Exported symbols of include/bra_hip.h (checked by tests/test_abi.py against the header).
+ABI_SYMBOLS = (
+    "bra_bwt_encode", "bra_bwt_encode2", "bra_bwt_decode", "bra_bwt_decode2",
+    "bra_mtf_encode", "bra_mtf_encode2", "bra_mtf_decode", "bra_mtf_decode2",
+    "bra_rle_encode", "bra_rle_decode_compute_size", "bra_rle_decode",
+    "bra_huffman_encode", "bra_huffman_decode", "bra_huffman_chunk_free",
+    "bra_gpu_ctx_create", "bra_gpu_ctx_destroy", "bra_gpu_num_blocks", "bra_gpu_payload_bound",
+    "bra_gpu_encode_blocks", "bra_gpu_decode_blocks", "bra_gpu_stage_ptr", "bra_gpu_version",
+)
+
+SYNTH_TEXT, SYNTH_RANDOM, SYNTH_SYM16, SYNTH_TILED = 0, 1, 2, 3
+HEADER_BYTES = 268  # in-memory bra_io_chunk_header_t (pi u32 + packed bra_huffman_t)
+
+
+class HuffmanMeta(C.Structure):
+    """bra_huffman_t (src/lib_bra_types.h:51-56), packed."""
+
+    _pack_ = 1
+    _fields_ = [("lengths", C.c_uint8 * 256), ("orig_size", C.c_uint32), ("encoded_size", C.c_uint32)]
+
+
+class _HuffmanChunk(C.Structure):
+    """bra_huffman_chunk_t (src/encoders/bra_huffman.h:13-17)."""
+
+    _fields_ = [("meta", HuffmanMeta), ("data", C.c_void_p)]
+
+
+assert C.sizeof(HuffmanMeta) == 264 and _HuffmanChunk.data.offset == 264
+
+
+@dataclass
+class HuffmanChunk:
+    lengths: bytes
+    orig_size: int
+    encoded_size: int
+    data: bytes
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make -C br-archive_amd` (or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    u8p, u32p, vp = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32), C.c_void_p
+    lib.bra_bwt_encode2.argtypes = [u8p, C.c_uint32, u32p, u8p]
+    lib.bra_bwt_encode2.restype = C.c_bool
+    lib.bra_bwt_decode2.argtypes = [u8p, C.c_uint32, C.c_uint32, u32p, u8p]
+    lib.bra_bwt_decode2.restype = None
+    lib.bra_mtf_encode2.argtypes = [u8p, C.c_size_t, u8p]
+    lib.bra_mtf_encode2.restype = C.c_bool
+    lib.bra_mtf_decode2.argtypes = [u8p, C.c_size_t, u8p]
+    lib.bra_mtf_decode2.restype = None
+    lib.bra_rle_encode.argtypes = [u8p, C.c_size_t, C.POINTER(vp), C.POINTER(C.c_size_t)]
+    lib.bra_rle_encode.restype = C.c_bool
+    lib.bra_rle_decode.argtypes = [u8p, C.c_size_t, C.POINTER(vp), C.POINTER(C.c_size_t)]
+    lib.bra_rle_decode.restype = C.c_bool
+    lib.bra_rle_decode_compute_size.argtypes = [u8p, C.c_size_t]
+    lib.bra_rle_decode_compute_size.restype = C.c_size_t
+    lib.bra_huffman_encode.argtypes = [u8p, C.c_uint32]
+    lib.bra_huffman_encode.restype = C.POINTER(_HuffmanChunk)
+    lib.bra_huffman_decode.argtypes = [C.POINTER(HuffmanMeta), u8p, u32p]
+    lib.bra_huffman_decode.restype = vp
+    lib.bra_huffman_chunk_free.argtypes = [C.POINTER(_HuffmanChunk)]
+    lib.bra_huffman_chunk_free.restype = None
+    lib.bra_gpu_ctx_create.argtypes = [C.c_int]
+    lib.bra_gpu_ctx_create.restype = vp
+    lib.bra_gpu_ctx_destroy.argtypes = [vp]
+    lib.bra_gpu_ctx_destroy.restype = None
+    lib.bra_gpu_num_blocks.argtypes = [C.c_uint64, C.c_uint32]
+    lib.bra_gpu_num_blocks.restype = C.c_uint32
+    lib.bra_gpu_payload_bound.argtypes = [C.c_uint64, C.c_uint32]
+    lib.bra_gpu_payload_bound.restype = C.c_uint64
+    lib.bra_gpu_encode_blocks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64, vp]
+    lib.bra_gpu_encode_blocks.restype = C.c_int
+    lib.bra_gpu_decode_blocks.argtypes = [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp]
+    lib.bra_gpu_decode_blocks.restype = C.c_int
+    lib.bra_gpu_stage_ptr.argtypes = [vp, C.c_int]
+    lib.bra_gpu_stage_ptr.restype = vp
+    lib.bra_gpu_version.argtypes = []
+    lib.bra_gpu_version.restype = C.c_char_p
+    return lib
+
+
+lib = _load()
+_libc = C.CDLL(None)
+_libc.free.argtypes = [C.c_void_p]
+
+
+def _buf(data: bytes):
+    return (C.c_uint8 * max(1, len(data))).from_buffer_copy(data if data else b"\0")
+
+
+def version() -> str:
+    return lib.bra_gpu_version().decode()
+
+
+# ------------------------------------------------------------------------------------------------
+# reference encoder interface (src/encoders/*.h), one block per call
+# ------------------------------------------------------------------------------------------------
+def bwt_encode(buf: bytes):
+    """bra_bwt_encode2: returns (last column, primary index) or None on failure."""
+    n = len(buf)
+    out = (C.c_uint8 * max(1, n))()
+    pi = C.c_uint32()
+    if not lib.bra_bwt_encode2(_buf(buf), n, C.byref(pi), out):
+        return None
+    return bytes(out)[:n], pi.value
+
+
+def bwt_decode(buf: bytes, primary_index: int) -> bytes:
+    """bra_bwt_decode2."""
+    n = len(buf)
+    out = (C.c_uint8 * max(1, n))()
+    lib.bra_bwt_decode2(_buf(buf), n, primary_index, None, out)
+    return bytes(out)[:n]
+
+
+def mtf_encode(buf: bytes):
+    """bra_mtf_encode2: MTF positions, or None on failure."""
+    out = (C.c_uint8 * max(1, len(buf)))()
+    if not lib.bra_mtf_encode2(_buf(buf), len(buf), out):
+        return None
+    return bytes(out)[: len(buf)]
+
+
+def mtf_decode(buf: bytes) -> bytes:
+    """bra_mtf_decode2."""
+    out = (C.c_uint8 * max(1, len(buf)))()
+    lib.bra_mtf_decode2(_buf(buf), len(buf), out)
+    return bytes(out)[: len(buf)]
+
+
+def rle_encode(buf: bytes):
+    """bra_rle_encode: PackBits stream, or None when the C function returns false."""
+    p, s = C.c_void_p(), C.c_size_t()
+    if not lib.bra_rle_encode(_buf(buf), len(buf), C.byref(p), C.byref(s)):
+        return None
+    out = C.string_at(p, s.value)
+    _libc.free(p)
+    return out
+
+
+def rle_decode_compute_size(buf: bytes) -> int:
+    """bra_rle_decode_compute_size: 0 on a malformed or empty stream."""
+    return lib.bra_rle_decode_compute_size(_buf(buf), len(buf))
+
+
+def rle_decode(buf: bytes):
+    """bra_rle_decode: decoded bytes, or None when the C function returns false."""
+    p, s = C.c_void_p(), C.c_size_t()
+    if not lib.bra_rle_decode(_buf(buf), len(buf), C.byref(p), C.byref(s)):
+        return None
+    out = C.string_at(p, s.value)
+    _libc.free(p)
+    return out
+
+
+def huffman_encode(buf: bytes):
+    """bra_huffman_encode: HuffmanChunk, or None (e.g. for an empty buffer)."""
+    ch = lib.bra_huffman_encode(_buf(buf), len(buf))
+    if not ch:
+        return None
+    m = ch.contents.meta
+    data = C.string_at(ch.contents.data, m.encoded_size) if m.encoded_size else b""
+    res = HuffmanChunk(bytes(m.lengths), m.orig_size, m.encoded_size, data)
+    lib.bra_huffman_chunk_free(ch)
+    return res
+
+
+def huffman_decode(lengths: bytes, orig_size: int, encoded_size: int, data: bytes):
+    """bra_huffman_decode: decoded bytes, or None when the reference would reject the stream."""
+    meta = HuffmanMeta()
+    C.memmove(meta.lengths, lengths, 256)
+    meta.orig_size, meta.encoded_size = orig_size, encoded_size
+    osz = C.c_uint32()
+    p = lib.bra_huffman_decode(C.byref(meta), _buf(data), C.byref(osz))
+    if not p:
+        return None
+    out = C.string_at(p, osz.value)
+    _libc.free(p)
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# batched device-resident codec
+# ------------------------------------------------------------------------------------------------
+class BlockCodec:
+    """Batched encode/decode of independent blocks resident in HBM (torch uint8 CUDA tensors)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.ctx = lib.bra_gpu_ctx_create(device)
+        if not self.ctx:
+            raise RuntimeError("bra_gpu_ctx_create failed (no usable MI355X?)")
+
+    def close(self):
+        if self.ctx:
+            lib.bra_gpu_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def num_blocks(total: int, block_size: int) -> int:
+        return lib.bra_gpu_num_blocks(total, block_size)
+
+    @staticmethod
+    def payload_bound(total: int, block_size: int) -> int:
+        return lib.bra_gpu_payload_bound(total, block_size)
+
+    def encode(self, data, block_size: int, headers=None, offsets=None, payload=None, stream=None):
+        """Encode a uint8 CUDA tensor; returns (headers[nb,268] u8, offsets[nb+1] i64, payload u8)."""
+        import torch
+
+        total = data.numel()
+        nb = self.num_blocks(total, block_size)
+        dev = data.device
+        if headers is None:
+            headers = torch.empty((nb, HEADER_BYTES), dtype=torch.uint8, device=dev)
+        if offsets is None:
+            offsets = torch.empty((nb + 1,), dtype=torch.int64, device=dev)
+        if payload is None:
+            payload = torch.empty((int(total * 1.25) + 64 * nb + 4096,), dtype=torch.uint8, device=dev)
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_encode_blocks(self.ctx, data.data_ptr(), total, block_size, headers.data_ptr(), offsets.data_ptr(),
+                                       payload.data_ptr(), payload.numel(), s)
+        if rc == -2:
+            need = int(offsets[nb].item())
+            payload = torch.empty((need + 4096,), dtype=torch.uint8, device=dev)
+            rc = lib.bra_gpu_encode_blocks(self.ctx, data.data_ptr(), total, block_size, headers.data_ptr(), offsets.data_ptr(),
+                                           payload.data_ptr(), payload.numel(), s)
+        if rc != 0:
+            raise RuntimeError(f"bra_gpu_encode_blocks failed ({rc})")
+        return headers, offsets, payload
+
+    def decode(self, headers, offsets, payload, total: int, block_size: int, out=None, stream=None):
+        import torch
+
+        if out is None:
+            out = torch.empty((total,), dtype=torch.uint8, device=headers.device)
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_decode_blocks(self.ctx, headers.data_ptr(), offsets.data_ptr(), payload.data_ptr(), total, block_size,
+                                       out.data_ptr(), s)
+        if rc != 0:
+            raise RuntimeError(f"bra_gpu_decode_blocks failed ({rc})")
+        return out
+
+    def stage_ptr(self, stage: int) -> int:
+        return lib.bra_gpu_stage_ptr(self.ctx, stage) or 0
+
+
+def parse_header(h: bytes):
+    """(primary_index, lengths, orig_size, encoded_size) of a 268-byte in-memory chunk header."""
+    pi = int.from_bytes(h[0:4], "little")
+    return pi, bytes(h[4:260]), int.from_bytes(h[260:264], "little"), int.from_bytes(h[264:268], "little")
+
+
+# ------------------------------------------------------------------------------------------------
+# synthetic inputs (csrc/bra_synth.c)
+# ------------------------------------------------------------------------------------------------
+_synth = None
+
+
+def synth_lib():
+    global _synth
+    if _synth is None:
+        if not os.path.exists(SYNTH_PATH):
+            raise ImportError(f"{SYNTH_PATH} not built")
+        _synth = C.CDLL(SYNTH_PATH)
+        _synth.bra_synth_block.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_uint64]
+        _synth.bra_synth_fill.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64]
+    return _synth
+
+
+def synth_block(kind: int, index: int, n: int) -> bytes:
+    b = (C.c_uint8 * max(1, n))()
+    synth_lib().bra_synth_block(kind, index, b, n)
+    return bytes(b)[:n]
+
+
+def synth_fill(kind: int, total: int, block_size: int, first_block: int = 0):
+    """numpy uint8 array of `total` bytes: consecutive synthetic blocks."""
+    import numpy as np
+
+    a = np.empty(total, dtype=np.uint8)
+    synth_lib().bra_synth_fill(kind, first_block, a.ctypes.data, total, block_size)
+    return a

@@ -1,0 +1,252 @@
+// bra_hip_common.h -- shared host/device helpers for the gfx950 block-codec kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define BRA_HIP_CHECK(expr)                                                                              \
+    do                                                                                                   \
+    {                                                                                                    \
+        hipError_t _e = (expr);                                                                          \
+        if (_e != hipSuccess)                                                                            \
+        {                                                                                                \
+            bra_hip_report("HIP error %s at %s:%d: %s", hipGetErrorString(_e), __FILE__, __LINE__, #expr); \
+            return false;                                                                                \
+        }                                                                                                \
+    } while (0)
+
+// Error sink: forwards to the reference's bra_log_error when lib_bra is linked in, else stderr.
+void bra_hip_report(const char* fmt, ...);
+
+namespace bra {
+
+constexpr int WAVE = 64;
+
+// ---------------------------------------------------------------------------------------------
+// Batch geometry: a batch is `nblocks` independent blocks laid out back to back in HBM.
+// ---------------------------------------------------------------------------------------------
+struct BlockDesc
+{
+    uint64_t off;  // byte offset of the block in the batch (== slot offset of its rotations)
+    uint32_t len;  // block length n (1 <= n < 2^24)
+    uint32_t pad;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Wave-level helpers (wave64).  Elements are distributed 4 per lane: element e = 4*lane + r.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
+{
+    uint32_t lo = (uint32_t) v, hi = (uint32_t) (v >> 32);
+    lo          = __shfl_xor(lo, m, WAVE);
+    hi          = __shfl_xor(hi, m, WAVE);
+    return ((uint64_t) hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d)
+{
+    uint32_t lo = (uint32_t) v, hi = (uint32_t) (v >> 32);
+    lo          = __shfl_up(lo, d, WAVE);
+    hi          = __shfl_up(hi, d, WAVE);
+    return ((uint64_t) hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int d)
+{
+    uint32_t lo = (uint32_t) v, hi = (uint32_t) (v >> 32);
+    lo          = __shfl_down(lo, d, WAVE);
+    hi          = __shfl_down(hi, d, WAVE);
+    return ((uint64_t) hi << 32) | lo;
+}
+
+// (key, val) lexicographic "greater than".
+__device__ __forceinline__ bool kv_gt(uint64_t ka, uint32_t va, uint64_t kb, uint32_t vb)
+{
+    return ka > kb || (ka == kb && va > vb);
+}
+
+// Bitonic sort of P (4..256, power of two) elements held 4 per lane, ascending by (key, val).
+// Lanes >= P/4 hold padding and take part only in their own (ignored) sub-network.
+__device__ __forceinline__ void wave_bitonic_sort4(uint64_t (&k)[4], uint32_t (&v)[4], int P)
+{
+    const int lane = lane_id();
+    for (int size = 2; size <= P; size <<= 1)
+    {
+        for (int j = size >> 1; j > 0; j >>= 1)
+        {
+            if (j >= 4)
+            {
+                const int lm = j >> 2;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const int      e    = lane * 4 + r;
+                    const uint64_t ok   = shfl_xor64(k[r], lm);
+                    const uint32_t ov   = __shfl_xor(v[r], lm, WAVE);
+                    const bool     up   = (e & size) == 0;
+                    const bool     low  = (e & j) == 0;
+                    const bool     gt   = kv_gt(k[r], v[r], ok, ov);
+                    // lower element keeps min when ascending, max when descending
+                    const bool     take = (low == up) ? gt : !gt;
+                    if (take && !(k[r] == ok && v[r] == ov))
+                    {
+                        k[r] = ok;
+                        v[r] = ov;
+                    }
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const int p = r ^ j;
+                    if (p > r)
+                    {
+                        const int  e  = lane * 4 + r;
+                        const bool up = (e & size) == 0;
+                        const bool gt = kv_gt(k[r], v[r], k[p], v[p]);
+                        if (gt == up)
+                        {
+                            uint64_t tk = k[r];
+                            k[r]        = k[p];
+                            k[p]        = tk;
+                            uint32_t tv = v[r];
+                            v[r]        = v[p];
+                            v[p]        = tv;
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Inclusive max-scan over 256 elements (4 per lane) in element order.
+__device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
+{
+    x[1]         = max(x[1], x[0]);
+    x[2]         = max(x[2], x[1]);
+    x[3]         = max(x[3], x[2]);
+    uint32_t agg = x[3];
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        uint32_t o = __shfl_up(agg, d, WAVE);
+        if (lane_id() >= d)
+            agg = max(agg, o);
+    }
+    uint32_t ex = __shfl_up(agg, 1, WAVE);
+    if (lane_id() == 0)
+        ex = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        x[r] = max(x[r], ex);
+}
+
+// Inclusive min-scan over 256 elements (4 per lane) in REVERSE element order.
+__device__ __forceinline__ void wave_min_rscan4(uint32_t (&x)[4])
+{
+    x[2]         = min(x[2], x[3]);
+    x[1]         = min(x[1], x[2]);
+    x[0]         = min(x[0], x[1]);
+    uint32_t agg = x[0];
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        uint32_t o = __shfl_down(agg, d, WAVE);
+        if (lane_id() + d < WAVE)
+            agg = min(agg, o);
+    }
+    uint32_t ex = __shfl_down(agg, 1, WAVE);
+    if (lane_id() == WAVE - 1)
+        ex = 0xFFFFFFFFu;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        x[r] = min(x[r], ex);
+}
+
+// Block-wide exclusive sum over 256 threads (one value per thread).  `tmp` >= 8 words of LDS.
+__device__ __forceinline__ uint32_t block256_exclusive_sum(uint32_t v, uint32_t* tmp, uint32_t* total = nullptr)
+{
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t  x    = v;
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        uint32_t o = __shfl_up(x, d, WAVE);
+        if (lane >= d)
+            x += o;
+    }
+    if (lane == WAVE - 1)
+        tmp[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int i = 0; i < 4; ++i)
+    {
+        if (i < w)
+            pre += tmp[i];
+        tot += tmp[i];
+    }
+    __syncthreads();
+    if (total)
+        *total = tot;
+    return pre + x - v;
+}
+
+__device__ __forceinline__ uint64_t block256_exclusive_sum64(uint64_t v, uint64_t* tmp, uint64_t* total = nullptr)
+{
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint64_t  x    = v;
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        uint64_t o = shfl_up64(x, d);
+        if (lane >= d)
+            x += o;
+    }
+    if (lane == WAVE - 1)
+        tmp[w] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int i = 0; i < 4; ++i)
+    {
+        if (i < w)
+            pre += tmp[i];
+        tot += tmp[i];
+    }
+    __syncthreads();
+    if (total)
+        *total = tot;
+    return pre + x - v;
+}
+
+// 8 cyclic bytes of a block starting at `start` (< n), big-endian (first byte most significant).
+// Non-wrapping reads use two naturally aligned 8-byte loads: each aligned word holds at least one
+// in-range byte, so the read never leaves the pages of the buffer.
+__device__ __forceinline__ uint64_t load_key8(const uint8_t* __restrict__ blk, uint32_t n, uint32_t start)
+{
+    if (start + 8u <= n)
+    {
+        const uintptr_t a  = (uintptr_t) (blk + start);
+        const uint64_t* p  = (const uint64_t*) (a & ~(uintptr_t) 7);
+        const unsigned  sh = (unsigned) (a & 7) * 8u;
+        uint64_t        w  = p[0] >> sh;
+        if (sh)
+            w |= p[1] << (64u - sh);
+        return __builtin_bswap64(w);
+    }
+    uint64_t k = 0;
+    uint32_t q = start;
+    for (int i = 0; i < 8; ++i)
+    {
+        k = (k << 8) | blk[q];
+        q = (q + 1 == n) ? 0 : q + 1;
+    }
+    return k;
+}
+
+__host__ __device__ __forceinline__ uint32_t div_up(uint64_t a, uint32_t b) { return (uint32_t) ((a + b - 1) / b); }
+
+}  // namespace bra

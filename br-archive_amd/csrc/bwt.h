@@ -1,0 +1,16 @@
+// bwt.h -- device-side stage entry points of the block codec (host-callable, device pointers).
+#pragma once
+
+#include "bra_hip_common.h"
+
+namespace bra {
+
+struct BwtWorkspace;
+BwtWorkspace* bwt_workspace_create();
+void          bwt_workspace_destroy(BwtWorkspace* w);
+
+// BWT of every block: d_L[off..off+len) = last column, d_pi[b] = primary index (block-local).
+bool bwt_encode_device(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
+                       uint8_t* d_L, uint32_t* d_pi, hipStream_t s);
+
+}  // namespace bra

@@ -1,0 +1,712 @@
+// capi.hip -- the C-ABI of libbra_hip.so (include/bra_hip.h): the reference's 14 encoder entry
+// points (single block, host buffers) and the batched device-resident codec.
+#include "../../include/bra_hip.h"
+
+#include "bwt.h"
+#include "huffman.h"
+#include "ibwt.h"
+#include "mtf.h"
+#include "rle.h"
+
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+extern "C" void bra_log_error(const char* fmt, ...) __attribute__((weak));
+
+void bra_hip_report(const char* fmt, ...)
+{
+    char    buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (bra_log_error)
+        bra_log_error("%s", buf);
+    else
+        fprintf(stderr, "[bra_hip] %s\n", buf);
+}
+
+static_assert(sizeof(bra_io_chunk_header_t) == 268, "in-memory chunk header layout (lib_bra_types.h:63-68)");
+static_assert(sizeof(bra_huffman_t) == 264, "bra_huffman_t layout");
+static_assert(offsetof(bra_huffman_chunk_t, data) == 264, "bra_huffman_chunk_t layout");
+
+using namespace bra;
+
+namespace {
+
+__global__ void k_headers(const uint32_t* __restrict__ pi, const HuffMetaRec* __restrict__ meta, uint32_t nb,
+                          bra_io_chunk_header_t* __restrict__ hdr)
+{
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x)
+    {
+        uint8_t*       dst = reinterpret_cast<uint8_t*>(hdr + b);
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(meta + b);
+        for (uint32_t i = threadIdx.x; i < 268; i += blockDim.x)
+            dst[i] = (i < 4) ? (uint8_t) (pi[b] >> (8 * i)) : src[i - 4];
+    }
+}
+
+__global__ void k_split_headers(const bra_io_chunk_header_t* __restrict__ hdr, uint32_t nb, uint32_t* __restrict__ pi,
+                                HuffMetaRec* __restrict__ meta)
+{
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x)
+    {
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(hdr + b);
+        uint8_t*       dst = reinterpret_cast<uint8_t*>(meta + b);
+        for (uint32_t i = threadIdx.x; i < 264; i += blockDim.x)
+            dst[i] = src[i + 4];
+        if (threadIdx.x == 0)
+            pi[b] = hdr[b].primary_index;
+    }
+}
+
+template <typename T>
+bool grow(T*& p, uint64_t& cap, uint64_t need)
+{
+    if (need <= cap)
+        return true;
+    (void) hipFree(p);
+    p   = nullptr;
+    cap = need + need / 8 + 256;
+    BRA_HIP_CHECK(hipMalloc(&p, cap * sizeof(T)));
+    return true;
+}
+
+}  // namespace
+
+struct bra_gpu_ctx_s
+{
+    int            device = 0;
+    hipStream_t    stream = nullptr;
+    BwtWorkspace*  bwt    = nullptr;
+    MtfWorkspace   mtf;
+    RleWorkspace   rle;
+    HuffWorkspace  huf;
+    IbwtWorkspace  ib;
+    Tiling         hist_tiling;
+    // batch buffers
+    uint8_t*       d_L = nullptr;
+    uint8_t*       d_mtf = nullptr;
+    uint8_t*       d_rle = nullptr;
+    uint8_t*       d_tmp = nullptr;
+    uint64_t       cap_L = 0, cap_mtf = 0, cap_rle = 0, cap_tmp = 0;
+    BlockDesc*     d_blocks = nullptr;
+    uint32_t*      d_pi = nullptr;
+    uint32_t*      d_rle_size = nullptr;
+    uint32_t*      d_hist = nullptr;
+    uint32_t*      d_status = nullptr;
+    uint64_t*      d_rle_base = nullptr;
+    uint64_t*      d_rle_cap = nullptr;
+    uint64_t*      d_aux = nullptr;  // block offsets for decode, record bases
+    HuffMetaRec*   d_meta = nullptr;
+    uint64_t       cap_b = 0, cap_pi = 0, cap_rs = 0, cap_hist = 0, cap_st = 0, cap_rb = 0, cap_rc = 0, cap_aux = 0, cap_meta = 0;
+    uint64_t       cap_recs = 0;
+    uint64_t*      d_recs = nullptr;
+    // single-call staging
+    uint8_t*       d_io = nullptr;
+    uint64_t       cap_io = 0;
+    uint64_t*      d_off = nullptr;
+    uint64_t       cap_off = 0;
+    uint8_t*       d_pay = nullptr;
+    uint64_t       cap_pay = 0;
+    bra_io_chunk_header_t* d_hdr = nullptr;
+    uint64_t       cap_hdr = 0;
+    uint32_t       last_nblocks = 0;
+};
+
+static bool ctx_init(bra_gpu_ctx_s* c, int device)
+{
+    c->device = device;
+    BRA_HIP_CHECK(hipSetDevice(device));
+    BRA_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->bwt = bwt_workspace_create();
+    return c->bwt != nullptr;
+}
+
+static void ctx_free(bra_gpu_ctx_s* c)
+{
+    (void) hipSetDevice(c->device);
+    bwt_workspace_destroy(c->bwt);
+    c->mtf.release();
+    c->rle.release();
+    c->huf.release();
+    c->ib.release();
+    c->hist_tiling.release();
+    void* ptrs[] = {c->d_L,       c->d_mtf,   c->d_rle,  c->d_tmp,  c->d_blocks, c->d_pi,  c->d_rle_size, c->d_hist, c->d_status, c->d_rle_base,
+                    c->d_rle_cap, c->d_aux,   c->d_meta, c->d_recs, c->d_io,     c->d_off, c->d_pay,      c->d_hdr};
+    for (void* p : ptrs)
+        (void) hipFree(p);
+    if (c->stream)
+        (void) hipStreamDestroy(c->stream);
+}
+
+static std::vector<BlockDesc> geometry(uint64_t total, uint32_t block_size)
+{
+    std::vector<BlockDesc> v;
+    for (uint64_t off = 0; off < total; off += block_size)
+        v.push_back(BlockDesc{off, (uint32_t) std::min<uint64_t>(block_size, total - off), 0});
+    return v;
+}
+
+static bool ensure_block_arrays(bra_gpu_ctx_s* c, uint32_t nb)
+{
+    return grow(c->d_blocks, c->cap_b, nb) && grow(c->d_pi, c->cap_pi, nb) && grow(c->d_rle_size, c->cap_rs, nb) &&
+           grow(c->d_hist, c->cap_hist, (uint64_t) nb * 256) && grow(c->d_status, c->cap_st, nb) && grow(c->d_rle_base, c->cap_rb, nb + 1) &&
+           grow(c->d_rle_cap, c->cap_rc, nb + 1) && grow(c->d_aux, c->cap_aux, 2ull * nb + 2) && grow(c->d_meta, c->cap_meta, nb);
+}
+
+// The whole encode chain for a batch already in HBM.
+static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<BlockDesc>& hb, bra_io_chunk_header_t* d_headers,
+                       uint64_t* d_payload_off, uint8_t* d_payload, uint64_t payload_cap, hipStream_t s, uint64_t* needed)
+{
+    const uint32_t nb = (uint32_t) hb.size();
+    if (nb == 0)
+        return -1;
+    const uint64_t N = hb.back().off + hb.back().len;
+    std::vector<uint64_t> rle_base(nb + 1);
+    std::vector<BlockDesc> rle_blocks(nb);
+    uint64_t R = 0;
+    for (uint32_t b = 0; b < nb; ++b)
+    {
+        rle_base[b]   = R;
+        rle_blocks[b] = BlockDesc{R, (uint32_t) rle_capacity(hb[b].len), 0};
+        R += rle_capacity(hb[b].len);
+    }
+    rle_base[nb] = R;
+    if (!ensure_block_arrays(c, nb) || !grow(c->d_L, c->cap_L, N + 16) || !grow(c->d_mtf, c->cap_mtf, N + 16) || !grow(c->d_rle, c->cap_rle, R + 16))
+        return -1;
+    if (hipMemcpyAsync(c->d_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(c->d_rle_base, rle_base.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -1;
+    if (!bwt_encode_device(c->bwt, d_in, c->d_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
+        return -1;
+    if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s))
+        return -1;
+    if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
+        return -1;
+    uint64_t total = 0;
+    if (!huff_encode_device(c->huf, c->d_rle, rle_blocks.data(), nb, c->d_hist, c->d_rle_size, c->d_meta, d_payload_off, d_payload, payload_cap,
+                            &total, s))
+    {
+        if (needed)
+            *needed = total;
+        return total + 8 > payload_cap ? -2 : -1;
+    }
+    hipLaunchKernelGGL(k_headers, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, c->d_pi, c->d_meta, nb, d_headers);
+    if (hipGetLastError() != hipSuccess)
+        return -1;
+    c->last_nblocks = nb;
+    if (needed)
+        *needed = total;
+    return 0;
+}
+
+// The whole decode chain.  d_out receives the blocks of geometry hb.
+static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
+                       const std::vector<BlockDesc>& hb, uint8_t* d_out, hipStream_t s)
+{
+    const uint32_t nb = (uint32_t) hb.size();
+    if (nb == 0)
+        return -1;
+    const uint64_t N = hb.back().off + hb.back().len;
+    if (!ensure_block_arrays(c, nb))
+        return -1;
+    std::vector<bra_io_chunk_header_t> hh(nb);
+    if (hipMemcpyAsync(hh.data(), d_headers, nb * sizeof(bra_io_chunk_header_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    // RLE streams back to back; record arrays; MTF input at the block offsets
+    std::vector<uint64_t> rbase(nb), rcap(nb), recb(nb), outb(nb), outcap(nb);
+    std::vector<uint32_t> rsz(nb);
+    uint64_t R = 0, RC = 0;
+    for (uint32_t b = 0; b < nb; ++b)
+    {
+        const uint32_t os = hh[b].huffman.orig_size;
+        if (hh[b].primary_index >= hb[b].len)
+        {
+            bra_hip_report("invalid primary index (%u) for chunk size %u", hh[b].primary_index, hb[b].len);
+            return -1;
+        }
+        rbase[b]  = R;
+        rsz[b]    = os;
+        recb[b]   = RC;
+        outb[b]   = hb[b].off;
+        outcap[b] = hb[b].len;
+        R += (uint64_t) os + 16;
+        RC += os / 2 + 2;
+    }
+    if (!grow(c->d_rle, c->cap_rle, R + 16) || !grow(c->d_recs, c->cap_recs, RC + 16) || !grow(c->d_L, c->cap_L, N + 16) ||
+        !grow(c->d_mtf, c->cap_mtf, N + 16) || !grow(c->d_tmp, c->cap_tmp, N + 16))
+        return -1;
+    uint64_t* d_rbase  = c->d_rle_base;
+    uint64_t* d_outcap = c->d_rle_cap;
+    uint64_t* d_recb   = c->d_aux;
+    uint64_t* d_outb   = c->d_aux + nb + 1;
+    if (hipMemcpyAsync(c->d_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_rbase, rbase.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_outcap, outcap.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_recb, recb.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_outb, outb.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(c->d_rle_size, rsz.data(), nb * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_split_headers, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, d_headers, nb, c->d_pi, c->d_meta);
+    if (!huff_decode_device(c->huf, c->d_meta, nb, d_payload, d_payload_off, c->d_rle, d_rbase, c->d_status, s))
+        return -1;
+    uint32_t* d_dec_size = c->d_hist;           // nb words
+    uint32_t* d_nrec     = c->d_hist + nb;      // nb words
+    if (!rle_decode_device(c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, c->d_recs, d_recb, d_nrec, s))
+        return -1;
+    std::vector<uint32_t> st(nb), dsz(nb);
+    if (hipMemcpyAsync(st.data(), c->d_status, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(dsz.data(), d_dec_size, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    for (uint32_t b = 0; b < nb; ++b)
+    {
+        if (st[b])
+        {
+            bra_hip_report("huffman decode error in block %u", b);
+            return -1;
+        }
+        if (dsz[b] != hb[b].len)
+        {
+            bra_hip_report("RLE decode of block %u gave %u bytes, expected %u", b, dsz[b], hb[b].len);
+            return -1;
+        }
+    }
+    if (!mtf_decode_device(c->mtf, c->d_mtf, c->d_L, c->d_tmp, hb.data(), nb, s))
+        return -1;
+    if (!ibwt_device(c->ib, c->d_L, c->d_pi, c->d_blocks, hb.data(), nb, d_out, s))
+        return -1;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
+}
+
+// =================================================================================================
+// Part 2: batch API
+// =================================================================================================
+extern "C" {
+
+bra_gpu_ctx_t* bra_gpu_ctx_create(int device)
+{
+    auto* c = new bra_gpu_ctx_s();
+    if (!ctx_init(c, device))
+    {
+        ctx_free(c);
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void bra_gpu_ctx_destroy(bra_gpu_ctx_t* c)
+{
+    if (!c)
+        return;
+    ctx_free(c);
+    delete c;
+}
+
+uint32_t bra_gpu_num_blocks(uint64_t total, uint32_t block_size) { return block_size ? (uint32_t) ((total + block_size - 1) / block_size) : 0; }
+
+uint64_t bra_gpu_payload_bound(uint64_t total, uint32_t block_size)
+{
+    uint64_t r = 0;
+    for (const BlockDesc& b : geometry(total, block_size))
+        r += rle_capacity(b.len) * 4;  // codes of <= 32 bits
+    return r + 64;
+}
+
+int bra_gpu_encode_blocks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t total, uint32_t block_size, bra_io_chunk_header_t* d_headers,
+                          uint64_t* d_payload_off, uint8_t* d_payload, uint64_t payload_cap, void* stream)
+{
+    if (!c || !d_in || !total || !block_size || block_size >= (1u << 24) || !d_headers || !d_payload_off || !d_payload)
+        return -1;
+    if (hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    return encode_impl(c, d_in, geometry(total, block_size), d_headers, d_payload_off, d_payload, payload_cap, s, nullptr);
+}
+
+int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
+                          uint64_t total, uint32_t block_size, uint8_t* d_out, void* stream)
+{
+    if (!c || !d_headers || !d_payload_off || !d_payload || !total || !block_size || block_size >= (1u << 24) || !d_out)
+        return -1;
+    if (hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    return decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
+}
+
+const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)
+{
+    if (!c)
+        return nullptr;
+    switch (stage)
+    {
+    case 0: return c->d_L;
+    case 1: return c->d_mtf;
+    case 2: return c->d_rle;
+    case 3: return c->d_rle_base;
+    case 4: return c->d_rle_size;
+    default: return nullptr;
+    }
+}
+
+const char* bra_gpu_version(void) { return "bra_hip 0.1.0 (gfx950)"; }
+
+}  // extern "C"
+
+// =================================================================================================
+// Part 1: the reference encoder ABI on a lazily created process-wide context
+// =================================================================================================
+namespace {
+
+std::mutex     g_mu;
+bra_gpu_ctx_s* g_ctx = nullptr;
+
+bra_gpu_ctx_s* global_ctx()
+{
+    if (!g_ctx)
+    {
+        auto* c = new bra_gpu_ctx_s();
+        if (!ctx_init(c, 0))
+        {
+            bra_hip_report("no usable HIP device for the block codec");
+            ctx_free(c);
+            delete c;
+            return nullptr;
+        }
+        g_ctx = c;
+    }
+    (void) hipSetDevice(g_ctx->device);
+    return g_ctx;
+}
+
+bool upload(bra_gpu_ctx_s* c, const uint8_t* buf, uint64_t n)
+{
+    if (!grow(c->d_io, c->cap_io, n + 64))
+        return false;
+    BRA_HIP_CHECK(hipMemcpyAsync(c->d_io, buf, n, hipMemcpyHostToDevice, c->stream));
+    return true;
+}
+
+bool download(bra_gpu_ctx_s* c, void* dst, const void* src, uint64_t n)
+{
+    if (n)
+        BRA_HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+    BRA_HIP_CHECK(hipStreamSynchronize(c->stream));
+    return true;
+}
+
+std::vector<BlockDesc> one_block(uint64_t n) { return {BlockDesc{0, (uint32_t) n, 0}}; }
+
+}  // namespace
+
+extern "C" {
+
+bool bra_bwt_encode2(const uint8_t* buf, const bra_bwt_index_t buf_size, bra_bwt_index_t* primary_index, uint8_t* out_buf)
+{
+    if (!buf || !buf_size || !primary_index || !out_buf)
+        return false;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !upload(c, buf, buf_size))
+        return false;
+    auto hb = one_block(buf_size);
+    if (!ensure_block_arrays(c, 1) || !grow(c->d_L, c->cap_L, (uint64_t) buf_size + 16))
+        return false;
+    if (hipMemcpyAsync(c->d_blocks, hb.data(), sizeof(BlockDesc), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return false;
+    if (!bwt_encode_device(c->bwt, c->d_io, c->d_blocks, hb.data(), 1, c->d_L, c->d_pi, c->stream))
+        return false;
+    return download(c, primary_index, c->d_pi, 4) && download(c, out_buf, c->d_L, buf_size);
+}
+
+uint8_t* bra_bwt_encode(const uint8_t* buf, const bra_bwt_index_t buf_size, bra_bwt_index_t* primary_index)
+{
+    uint8_t* out = (uint8_t*) malloc(buf_size);
+    if (!out)
+        return nullptr;
+    if (!bra_bwt_encode2(buf, buf_size, primary_index, out))
+    {
+        free(out);
+        return nullptr;
+    }
+    return out;
+}
+
+void bra_bwt_decode2(const uint8_t* buf, const bra_bwt_index_t buf_size, const bra_bwt_index_t primary_index, bra_bwt_index_t* transform,
+                     uint8_t* out_buf)
+{
+    if (!buf || !buf_size || !out_buf || primary_index >= buf_size)
+        return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !upload(c, buf, buf_size))
+        return;
+    auto hb = one_block(buf_size);
+    if (!ensure_block_arrays(c, 1) || !grow(c->d_L, c->cap_L, (uint64_t) buf_size + 16))
+        return;
+    if (hipMemcpyAsync(c->d_blocks, hb.data(), sizeof(BlockDesc), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->d_pi, &primary_index, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return;
+    if (!ibwt_device(c->ib, c->d_io, c->d_pi, c->d_blocks, hb.data(), 1, c->d_L, c->stream))
+        return;
+    if (transform)
+        (void) download(c, transform, c->ib.T, (uint64_t) buf_size * 4);  // the LF transform, as the reference leaves it
+    (void) download(c, out_buf, c->d_L, buf_size);
+}
+
+uint8_t* bra_bwt_decode(const uint8_t* buf, const bra_bwt_index_t buf_size, const bra_bwt_index_t primary_index)
+{
+    if (!buf || !buf_size || primary_index >= buf_size)
+        return nullptr;
+    uint8_t* out = (uint8_t*) malloc(buf_size);
+    if (!out)
+        return nullptr;
+    bra_bwt_decode2(buf, buf_size, primary_index, nullptr, out);
+    return out;
+}
+
+bool bra_mtf_encode2(const uint8_t* buf, const size_t buf_size, uint8_t* out_buf)
+{
+    if (!buf || !buf_size || !out_buf || buf_size >= (1ull << 31))
+        return false;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !upload(c, buf, buf_size) || !grow(c->d_mtf, c->cap_mtf, (uint64_t) buf_size + 16))
+        return false;
+    // blocks larger than 2^24 are fine for MTF: the segment scan is exact at any length
+    std::vector<BlockDesc> hb{BlockDesc{0, (uint32_t) buf_size, 0}};
+    if (!mtf_encode_device(c->mtf, c->d_io, c->d_mtf, hb.data(), 1, c->stream))
+        return false;
+    return download(c, out_buf, c->d_mtf, buf_size);
+}
+
+uint8_t* bra_mtf_encode(const uint8_t* buf, const size_t buf_size)
+{
+    uint8_t* out = (uint8_t*) malloc(buf_size ? buf_size : 1);
+    if (!out)
+        return nullptr;
+    if (!bra_mtf_encode2(buf, buf_size, out))
+    {
+        free(out);
+        return nullptr;
+    }
+    return out;
+}
+
+void bra_mtf_decode2(const uint8_t* buf, const size_t buf_size, uint8_t* out_buf)
+{
+    if (!buf || !buf_size || !out_buf || buf_size >= (1ull << 31))
+        return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !upload(c, buf, buf_size) || !grow(c->d_mtf, c->cap_mtf, (uint64_t) buf_size + 16) ||
+        !grow(c->d_tmp, c->cap_tmp, (uint64_t) buf_size + 16))
+        return;
+    std::vector<BlockDesc> hb{BlockDesc{0, (uint32_t) buf_size, 0}};
+    if (!mtf_decode_device(c->mtf, c->d_io, c->d_mtf, c->d_tmp, hb.data(), 1, c->stream))
+        return;
+    (void) download(c, out_buf, c->d_mtf, buf_size);
+}
+
+uint8_t* bra_mtf_decode(const uint8_t* buf, const size_t buf_size)
+{
+    if (!buf || !buf_size)
+        return nullptr;
+    uint8_t* out = (uint8_t*) malloc(buf_size);
+    if (!out)
+        return nullptr;
+    bra_mtf_decode2(buf, buf_size, out);
+    return out;
+}
+
+bool bra_rle_encode(const uint8_t* buf, const size_t buf_size, uint8_t** out_buf, size_t* out_buf_size)
+{
+    if (out_buf)
+        *out_buf = nullptr;
+    if (out_buf_size)
+        *out_buf_size = 0;
+    if (!buf || !out_buf || !out_buf_size || buf_size == 0 || buf_size >= (1ull << 31))
+        return false;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !upload(c, buf, buf_size) || !ensure_block_arrays(c, 1))
+        return false;
+    const uint64_t cap = rle_capacity((uint32_t) buf_size);
+    if (!grow(c->d_rle, c->cap_rle, cap + 16))
+        return false;
+    const uint64_t zero = 0;
+    if (hipMemcpyAsync(c->d_rle_base, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return false;
+    std::vector<BlockDesc> hb{BlockDesc{0, (uint32_t) buf_size, 0}};
+    if (!rle_encode_device(c->rle, c->d_io, hb.data(), 1, c->d_rle_base, c->d_rle, c->d_rle_size, c->d_hist, c->stream))
+        return false;
+    uint32_t rs = 0;
+    if (!download(c, &rs, c->d_rle_size, 4) || rs == 0)
+        return false;
+    uint8_t* b = (uint8_t*) malloc(rs);
+    if (!b)
+        return false;
+    if (!download(c, b, c->d_rle, rs))
+    {
+        free(b);
+        return false;
+    }
+    *out_buf      = b;
+    *out_buf_size = rs;
+    return true;
+}
+
+static bool rle_decode_one(bra_gpu_ctx_s* c, const uint8_t* buf, size_t buf_size, uint32_t* dec_size, bool expand)
+{
+    if (!upload(c, buf, buf_size) || !ensure_block_arrays(c, 1))
+        return false;
+    const uint64_t out_cap = expand ? (uint64_t) buf_size * 64 + 64 : 0;  // a 2-byte run block expands to <= 128 bytes
+    if (!grow(c->d_tmp, c->cap_tmp, std::max<uint64_t>(out_cap, 16)) || !grow(c->d_recs, c->cap_recs, buf_size / 2 + 16))
+        return false;
+    const uint64_t zero = 0, cap = out_cap;
+    const uint32_t sz   = (uint32_t) buf_size;
+    if (hipMemcpyAsync(c->d_rle_base, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->d_rle_cap, &cap, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->d_aux, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->d_rle_size, &sz, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return false;
+    if (!rle_decode_device(c->d_io, c->d_rle_base, c->d_rle_size, 1, c->d_tmp, c->d_aux, c->d_rle_cap, c->d_status, c->d_recs, c->d_aux,
+                           c->d_pi, c->stream))
+        return false;
+    return download(c, dec_size, c->d_status, 4);
+}
+
+size_t bra_rle_decode_compute_size(const uint8_t* buf, const size_t buf_size)
+{
+    if (!buf || buf_size == 0 || buf_size >= (1ull << 31))
+        return 0;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    uint32_t                    s = 0;
+    if (!c || !rle_decode_one(c, buf, buf_size, &s, false))
+        return 0;
+    return s;
+}
+
+bool bra_rle_decode(const uint8_t* buf, const size_t buf_size, uint8_t** out_buf, size_t* out_buf_size)
+{
+    if (out_buf)
+        *out_buf = nullptr;
+    if (out_buf_size)
+        *out_buf_size = 0;
+    if (!buf || !out_buf || !out_buf_size || buf_size == 0 || buf_size >= (1ull << 31))
+        return false;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    uint32_t                    s = 0;
+    if (!c || !rle_decode_one(c, buf, buf_size, &s, true) || s == 0)
+        return false;
+    uint8_t* b = (uint8_t*) malloc(s);
+    if (!b)
+        return false;
+    if (!download(c, b, c->d_tmp, s))
+    {
+        free(b);
+        return false;
+    }
+    *out_buf      = b;
+    *out_buf_size = s;
+    return true;
+}
+
+bra_huffman_chunk_t* bra_huffman_encode(const uint8_t* buf, const uint32_t buf_size)
+{
+    if (!buf || buf_size == 0)
+    {
+        bra_hip_report("unable to huffman encode");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !upload(c, buf, buf_size) || !ensure_block_arrays(c, 1) || !grow(c->d_off, c->cap_off, 4))
+        return nullptr;
+    std::vector<BlockDesc> hb{BlockDesc{0, buf_size, 0}};
+    if (!histogram_device(c->hist_tiling, c->d_io, hb.data(), 1, c->d_hist, c->stream))
+        return nullptr;
+    if (hipMemcpyAsync(c->d_rle_size, &buf_size, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return nullptr;
+    uint64_t cap = (uint64_t) buf_size * 4 + 64, total = 0;
+    for (int attempt = 0; attempt < 2; ++attempt)
+    {
+        if (!grow(c->d_pay, c->cap_pay, cap))
+            return nullptr;
+        if (huff_encode_device(c->huf, c->d_io, hb.data(), 1, c->d_hist, c->d_rle_size, c->d_meta, c->d_off, c->d_pay, c->cap_pay, &total,
+                               c->stream))
+            break;
+        if (total + 8 <= c->cap_pay || attempt == 1)
+            return nullptr;
+        cap = total + 64;
+    }
+    auto* out = (bra_huffman_chunk_t*) malloc(sizeof(bra_huffman_chunk_t));
+    if (!out)
+        return nullptr;
+    out->data = nullptr;
+    if (!download(c, &out->meta, c->d_meta, sizeof(bra_huffman_t)))
+    {
+        free(out);
+        return nullptr;
+    }
+    out->data = (uint8_t*) malloc(out->meta.encoded_size ? out->meta.encoded_size : 1);
+    if (!out->data || !download(c, out->data, c->d_pay, out->meta.encoded_size))
+    {
+        free(out->data);
+        free(out);
+        return nullptr;
+    }
+    return out;
+}
+
+uint8_t* bra_huffman_decode(const bra_huffman_t* meta, const uint8_t* data, uint32_t* out_size)
+{
+    if (out_size)
+        *out_size = 0;
+    if (!meta || !data || !out_size)
+        return nullptr;
+    std::lock_guard<std::mutex> lk(g_mu);
+    bra_gpu_ctx_s*              c = global_ctx();
+    if (!c || !ensure_block_arrays(c, 1) || !grow(c->d_off, c->cap_off, 4))
+        return nullptr;
+    if (!upload(c, data, meta->encoded_size) || !grow(c->d_tmp, c->cap_tmp, (uint64_t) meta->orig_size + 16))
+        return nullptr;
+    const uint64_t zero = 0;
+    if (hipMemcpyAsync(c->d_meta, meta, sizeof(bra_huffman_t), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->d_off, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->d_rle_base, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return nullptr;
+    if (!huff_decode_device(c->huf, c->d_meta, 1, c->d_io, c->d_off, c->d_tmp, c->d_rle_base, c->d_status, c->stream))
+        return nullptr;
+    uint32_t st = 1;
+    if (!download(c, &st, c->d_status, 4) || st)
+    {
+        bra_hip_report("huffman decode error: invalid code sequence");
+        return nullptr;
+    }
+    uint8_t* out = (uint8_t*) malloc(meta->orig_size ? meta->orig_size : 1);
+    if (!out || !download(c, out, c->d_tmp, meta->orig_size))
+    {
+        free(out);
+        return nullptr;
+    }
+    *out_size = meta->orig_size;
+    return out;
+}
+
+void bra_huffman_chunk_free(bra_huffman_chunk_t* chunk)
+{
+    if (!chunk)
+        return;
+    free(chunk->data);
+    free(chunk);
+}
+
+}  // extern "C"

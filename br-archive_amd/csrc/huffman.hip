@@ -1,0 +1,796 @@
+// huffman.hip -- canonical Huffman coding for a batch of independent blocks.
+//
+// Replaces bra_huffman_encode / bra_huffman_decode (reference src/encoders/bra_huffman.c:352-432,
+// :434-498).  Encode:
+//   k_huff_build     one wave per block: code lengths from the reference's frequency-sorted list
+//                    (bra_minHeap_insert :90-118 restated as: position 0 if the head's frequency is
+//                    larger, else max(1, lower_bound(f)); leaves inserted in symbol order :140-153;
+//                    merge = pop l, pop r, insert l+r :158-175), leaf depth by pointer jumping,
+//                    canonical codes in uint32 with wrap (:227-261), bit count and encoded size
+//                    (:389-395).  Single-leaf trees get length 1 (:201-207).
+//   k_huff_offsets   exclusive scan of the encoded sizes -> byte offset of each block's payload
+//   k_huff_tilebits  bits of each 4096-symbol tile of a block's RLE output
+//   k_huff_tilescan  per block: bit offset of every tile
+//   k_huff_zero      zero the words at tile boundaries (they are OR-ed by two tiles)
+//   k_huff_pack      codes written MSB-first (:405-428) into an LDS word image of the tile, stored
+//                    with plain stores inside the tile and atomicOr on the two boundary words.
+// Decode: per block the reference's decode tree (:263-348: canonical codes inserted bit by bit,
+// a leaf that gains children stops being a leaf) is rebuilt on the device, turned into an 11-bit
+// primary lookup table, and walked (:455-482) with the reference's stop rule and error cases.
+#include "huffman.h"
+
+namespace bra {
+
+namespace {
+
+constexpr int TPB = 256;
+
+// ------------------------------------------------------------------------------------------------
+// code lengths + canonical codes (one wave per block)
+// ------------------------------------------------------------------------------------------------
+struct BuildLds
+{
+    uint32_t list_f[1024];   // frequencies of the list entries, list occupies [head, head+len)
+    uint16_t list_id[1024];
+    uint32_t node_f[512];
+    uint16_t parent[512];
+    uint32_t cnt[260];
+    uint32_t next[260];
+    uint8_t  len_s[256];
+};
+
+__global__ void __launch_bounds__(64) k_huff_build(const uint32_t* __restrict__ hist, const uint32_t* __restrict__ rle_size,
+                                                   uint32_t nblocks, HuffMetaRec* __restrict__ meta, uint32_t* __restrict__ codes)
+{
+    __shared__ BuildLds S;
+    const int           lane = lane_id();
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const uint32_t* H = hist + (size_t) b * 256;
+        uint32_t        h[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            h[r] = H[lane * 4 + r];
+        // leaves: ids in symbol order
+        uint32_t nz = (h[0] != 0) + (h[1] != 0) + (h[2] != 0) + (h[3] != 0);
+        uint32_t ex = nz;
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            uint32_t o = __shfl_up(ex, d, 64);
+            if (lane >= d)
+                ex += o;
+        }
+        const uint32_t leaves = __shfl(ex, 63, 64);
+        ex -= nz;
+        {
+            uint32_t id = ex;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (h[r])
+                {
+                    S.node_f[id] = h[r];
+                    S.parent[id] = 0xFFFF;
+                    ++id;
+                }
+        }
+        __syncthreads();
+        uint32_t head = 0, len = 0;
+        auto insert = [&](uint32_t id, uint32_t f) {
+            // position = 0 if empty or head.f > f, else max(1, #entries with freq < f)
+            uint32_t lt = 0;
+            for (uint32_t j = lane; j < len; j += 64)
+                lt += S.list_f[head + j] < f;
+            for (int d = 32; d > 0; d >>= 1)
+                lt += __shfl_xor(lt, d, 64);
+            uint32_t p;
+            if (len == 0 || S.list_f[head] > f)
+                p = 0;
+            else
+                p = lt > 1 ? lt : 1;
+            // shift [p, len) right by one (read everything first, then write)
+            uint32_t vf[4], vi[4];
+            const uint32_t m = len - p;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const uint32_t j = p + lane + 64 * r;
+                if (j < len)
+                {
+                    vf[r] = S.list_f[head + j];
+                    vi[r] = S.list_id[head + j];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const uint32_t j = p + lane + 64 * r;
+                if (j < len)
+                {
+                    S.list_f[head + j + 1]  = vf[r];
+                    S.list_id[head + j + 1] = (uint16_t) vi[r];
+                }
+            }
+            if (lane == 0)
+            {
+                S.list_f[head + p]  = f;
+                S.list_id[head + p] = (uint16_t) id;
+            }
+            __syncthreads();
+            ++len;
+            (void) m;
+        };
+        for (uint32_t id = 0; id < leaves; ++id)
+            insert(id, S.node_f[id]);
+        uint32_t nodes = leaves;
+        while (len > 1)
+        {
+            const uint32_t l = S.list_id[head], r = S.list_id[head + 1];
+            const uint32_t f = S.list_f[head] + S.list_f[head + 1];
+            head += 2;
+            len -= 2;
+            const uint32_t id = nodes++;
+            if (lane == 0)
+            {
+                S.node_f[id] = f;
+                S.parent[id] = 0xFFFF;
+                S.parent[l]  = (uint16_t) id;
+                S.parent[r]  = (uint16_t) id;
+            }
+            __syncthreads();
+            insert(id, f);
+        }
+        // depth of every node by pointer jumping (root has parent 0xFFFF, depth 0)
+        uint32_t anc[8], dep[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+        {
+            const uint32_t v = lane + 64 * r;
+            if (v < nodes)
+            {
+                anc[r] = S.parent[v];
+                dep[r] = anc[r] == 0xFFFF ? 0 : 1;
+            }
+        }
+        __syncthreads();
+        for (int it = 0; it < 9; ++it)
+        {
+            // node_f reused as depth scratch, parent as ancestor scratch
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+            {
+                const uint32_t v = lane + 64 * r;
+                if (v < nodes)
+                {
+                    S.node_f[v] = dep[r];
+                    S.parent[v] = (uint16_t) anc[r];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+            {
+                const uint32_t v = lane + 64 * r;
+                if (v < nodes && anc[r] != 0xFFFF)
+                {
+                    dep[r] += S.node_f[anc[r]];
+                    anc[r] = S.parent[anc[r]];
+                }
+            }
+            __syncthreads();
+        }
+        // lengths per symbol
+        if (lane < 65)
+            for (int i = lane; i < 260; i += 64)
+                S.cnt[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+        {
+            const uint32_t v = lane + 64 * r;
+            if (v < nodes)
+                S.node_f[v] = dep[r];
+        }
+        __syncthreads();
+        {
+            uint32_t id = ex;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                uint32_t L = 0;
+                if (h[r])
+                {
+                    const uint32_t d = S.node_f[id++];
+                    L                = (leaves == 1) ? 1 : (d & 0xFF);
+                }
+                S.len_s[lane * 4 + r] = (uint8_t) L;
+                if (L)
+                    atomicAdd(&S.cnt[L], 1u);
+            }
+        }
+        __syncthreads();
+        uint64_t bits = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            bits += (uint64_t) h[r] * S.len_s[lane * 4 + r];
+        for (int d = 32; d > 0; d >>= 1)
+            bits += shfl_xor64(bits, d);
+        if (lane == 0)
+        {
+            uint32_t code = 0;
+            for (int l = 1; l <= 256; ++l)
+            {
+                code <<= 1;
+                S.next[l] = code;
+                code += S.cnt[l];
+            }
+            for (int s = 0; s < 256; ++s)
+            {
+                const uint32_t L = S.len_s[s];
+                codes[(size_t) b * 256 + s] = L ? S.next[L]++ : 0;
+            }
+            HuffMetaRec& M  = meta[b];
+            M.orig_size     = rle_size[b];
+            const uint32_t bc = (uint32_t) bits;  // bra_huffman.c:390-392 accumulates in uint32
+            M.encoded_size  = (bc + 7u) / 8u;
+        }
+        for (int i = lane; i < 256; i += 64)
+            meta[b].lengths[i] = S.len_s[i];
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(TPB) k_huff_offsets(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, uint64_t* __restrict__ off)
+{
+    __shared__ uint64_t tmp[8];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0)
+        carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nblocks; base += TPB)
+    {
+        const uint32_t b = base + threadIdx.x;
+        const uint64_t v = b < nblocks ? meta[b].encoded_size : 0;
+        uint64_t       total;
+        const uint64_t ex = block256_exclusive_sum64(v, tmp, &total);
+        if (b < nblocks)
+            off[b] = carry + ex;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        off[nblocks] = carry;
+}
+
+// tiles over the RLE-output CAPACITY of each block; a tile beyond the block's RLE size is empty
+__global__ void __launch_bounds__(TPB) k_huff_tilebits(const uint8_t* __restrict__ rle, const Piece* __restrict__ tiles, uint32_t ntiles,
+                                                       const HuffMetaRec* __restrict__ meta, uint32_t* __restrict__ tbits)
+{
+    __shared__ uint8_t  L[256];
+    __shared__ uint32_t tmp[8];
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        const Piece    P    = tiles[t];
+        const uint32_t rs   = meta[P.block].orig_size;
+        L[threadIdx.x]      = meta[P.block].lengths[threadIdx.x];
+        __syncthreads();
+        const uint32_t cnt = P.start < rs ? min(P.len, rs - P.start) : 0;
+        uint32_t       acc = 0;
+        for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
+            acc += L[rle[P.off + i]];
+        uint32_t total;
+        block256_exclusive_sum(acc, tmp, &total);
+        if (threadIdx.x == 0)
+            tbits[t] = total;
+        __syncthreads();
+    }
+}
+
+__global__ void k_huff_tilescan(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
+                                const uint64_t* __restrict__ payload_off, uint32_t* __restrict__ tbits, uint64_t* __restrict__ tbit0)
+{
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    {
+        uint64_t run = payload_off[b] * 8;
+        for (uint32_t i = 0; i < count[b]; ++i)
+        {
+            const uint32_t t = first[b] + i;
+            tbit0[t]         = run;
+            run += tbits[t];
+        }
+    }
+}
+
+__global__ void k_huff_zero(const uint32_t* __restrict__ tbits, const uint64_t* __restrict__ tbit0, uint32_t ntiles,
+                            uint32_t* __restrict__ out_words)
+{
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x)
+    {
+        if (!tbits[t])
+            continue;
+        const uint64_t b0 = tbit0[t], b1 = b0 + tbits[t] - 1;
+        out_words[b0 >> 5] = 0;
+        out_words[b1 >> 5] = 0;
+    }
+}
+
+__device__ __forceinline__ void or_bits(uint32_t* w, uint64_t pos, uint32_t v, uint32_t nb, bool global)
+{
+    // place the nb-bit value v at stream bit pos (MSB-first within 32-bit words)
+    const uint32_t word = (uint32_t) (pos >> 5), off = (uint32_t) (pos & 31);
+    if (off + nb <= 32)
+    {
+        const uint32_t x = v << (32 - off - nb);
+        if (x)
+            global ? atomicOr(&w[word], __builtin_bswap32(x)) : atomicOr(&w[word], x);
+    }
+    else
+    {
+        const uint32_t spill = off + nb - 32;
+        const uint32_t x0    = v >> spill;
+        const uint32_t x1    = v << (32 - spill);
+        if (x0)
+            global ? atomicOr(&w[word], __builtin_bswap32(x0)) : atomicOr(&w[word], x0);
+        if (x1)
+            global ? atomicOr(&w[word + 1], __builtin_bswap32(x1)) : atomicOr(&w[word + 1], x1);
+    }
+}
+
+constexpr uint32_t PACK_WORDS = RLE_TILE + 2;  // 32 bits/symbol max on the LDS path
+
+__global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ rle, const Piece* __restrict__ tiles, uint32_t ntiles,
+                                                   const HuffMetaRec* __restrict__ meta, const uint32_t* __restrict__ codes,
+                                                   const uint32_t* __restrict__ tbits, const uint64_t* __restrict__ tbit0,
+                                                   uint32_t* __restrict__ out_words)
+{
+    __shared__ uint8_t  L[256];
+    __shared__ uint32_t C[256];
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t img[PACK_WORDS];
+    constexpr int       PT = RLE_TILE / TPB;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        const uint32_t nbits = tbits[t];
+        if (nbits == 0)
+            continue;  // uniform
+        const Piece    P  = tiles[t];
+        const uint32_t rs = meta[P.block].orig_size;
+        L[threadIdx.x]    = meta[P.block].lengths[threadIdx.x];
+        C[threadIdx.x]    = codes[(size_t) P.block * 256 + threadIdx.x];
+        const uint32_t cnt = min(P.len, rs - P.start);
+        const uint64_t g0  = tbit0[t];
+        const uint32_t sh  = (uint32_t) (g0 & 31);
+        const uint32_t nw  = (sh + nbits + 31) >> 5;
+        const bool     lds = nw <= PACK_WORDS;
+        if (lds)
+            for (uint32_t i = threadIdx.x; i < nw; i += TPB)
+                img[i] = 0;
+        __syncthreads();
+        // this thread's contiguous symbols
+        const uint32_t i0 = threadIdx.x * PT;
+        uint8_t        sym[PT];
+        uint32_t       mybits = 0;
+#pragma unroll
+        for (int k = 0; k < PT; ++k)
+        {
+            sym[k] = (i0 + k < cnt) ? rle[P.off + i0 + k] : 0;
+            mybits += (i0 + k < cnt) ? L[sym[k]] : 0;
+        }
+        if (!lds)
+        {
+            // global path (codes > 32 bits make the tile image too large for LDS): the words strictly
+            // inside the tile are owned by it; zero them before OR-ing (boundary words: k_huff_zero)
+            uint32_t* gw = out_words + (g0 >> 5);
+            for (uint32_t i = 1 + threadIdx.x; i + 1 < nw; i += TPB)
+                gw[i] = 0;
+        }
+        const uint32_t ex  = block256_exclusive_sum(mybits, tmp);  // (contains __syncthreads)
+        uint64_t       pos = lds ? (uint64_t) sh + ex : g0 + ex;
+        uint32_t*      dst = lds ? img : out_words;
+#pragma unroll
+        for (int k = 0; k < PT; ++k)
+        {
+            if (i0 + k >= cnt)
+                break;
+            uint32_t       nb = L[sym[k]];
+            const uint32_t c  = C[sym[k]];
+            if (nb > 32)
+            {
+                pos += nb - 32;  // leading zero bits of a wrapped long code
+                nb = 32;
+            }
+            or_bits(dst, pos, c, nb, !lds);
+            pos += nb;
+        }
+        __syncthreads();
+        if (lds)
+        {
+            uint32_t* gw = out_words + (g0 >> 5);
+            for (uint32_t i = threadIdx.x; i < nw; i += TPB)
+            {
+                const uint32_t v = __builtin_bswap32(img[i]);
+                if (i == 0 || i == nw - 1)
+                {
+                    if (v)
+                        atomicOr(&gw[i], v);
+                }
+                else
+                    gw[i] = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t TREE_CAP = 256 * 256 + 4;  // nodes per block (a code inserts <= len nodes)
+constexpr int      PEEK     = 11;
+
+// Reference tree from lengths (bra_huffman.c:263-348), one thread per block.  child[2*v+bit],
+// -1 = none.  status[b] = 1 on a failed insertion (the reference returns NULL).
+__global__ void k_huff_tree(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, int32_t* __restrict__ child, uint8_t* __restrict__ sym,
+                            uint32_t* __restrict__ status)
+{
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    {
+        const HuffMetaRec& M  = meta[b];
+        int32_t*           ch = child + (size_t) b * TREE_CAP * 2;
+        uint8_t*           sy = sym + (size_t) b * TREE_CAP;
+        uint32_t           count[257] = {0};
+        for (int s = 0; s < 256; ++s)
+            if (M.lengths[s])
+                count[M.lengths[s]]++;
+        uint32_t next[257];
+        uint32_t code = 0;
+        for (int l = 1; l <= 256; ++l)
+        {
+            code <<= 1;
+            next[l] = code;
+            code += count[l];
+        }
+        uint32_t nodes = 1;
+        ch[0] = ch[1] = -1;
+        sy[0]         = 0;
+        uint32_t st   = 0;
+        for (int s = 0; s < 256 && !st; ++s)
+        {
+            const uint32_t l = M.lengths[s];
+            if (!l)
+                continue;
+            const uint32_t c   = next[l]++;
+            uint32_t       cur = 0;
+            for (uint32_t j = 0; j < l; ++j)
+            {
+                const uint32_t bi  = l - 1 - j;
+                const int      bit = bi < 32 ? (int) ((c >> bi) & 1u) : 0;
+                if (j == l - 1)
+                {
+                    if (ch[2 * cur + bit] != -1)
+                    {
+                        st = 1;
+                        break;
+                    }
+                    ch[2 * cur + bit] = (int32_t) nodes;
+                    ch[2 * nodes] = ch[2 * nodes + 1] = -1;
+                    sy[nodes++]                       = (uint8_t) s;
+                }
+                else
+                {
+                    if (ch[2 * cur + bit] == -1)
+                    {
+                        ch[2 * cur + bit] = (int32_t) nodes;
+                        ch[2 * nodes] = ch[2 * nodes + 1] = -1;
+                        sy[nodes++]                       = 0;
+                    }
+                    cur = (uint32_t) ch[2 * cur + bit];
+                }
+            }
+        }
+        status[b] = st;
+    }
+}
+
+// 11-bit primary table per block: entry = kind(2) | used(4) | value(24)
+//   kind 0: leaf `value` reached after `used` bits; kind 1: continue at node `value` after 11 bits;
+//   kind 2: dead edge (decode error) after `used` bits.
+__global__ void k_huff_table(const int32_t* __restrict__ child, const uint8_t* __restrict__ sym, uint32_t nblocks, uint32_t* __restrict__ table)
+{
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const int32_t* ch = child + (size_t) b * TREE_CAP * 2;
+        for (uint32_t v = threadIdx.x; v < (1u << PEEK); v += blockDim.x)
+        {
+            uint32_t cur = 0, e = 0;
+            int      j   = 0;
+            for (; j < PEEK; ++j)
+            {
+                const int bit = (v >> (PEEK - 1 - j)) & 1;
+                const int nx  = ch[2 * cur + bit];
+                if (nx < 0)
+                {
+                    e = (2u << 28) | ((uint32_t) (j + 1) << 24);
+                    break;
+                }
+                cur = (uint32_t) nx;
+                if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
+                {
+                    e = (0u << 28) | ((uint32_t) (j + 1) << 24) | sym[(size_t) b * TREE_CAP + cur];
+                    break;
+                }
+            }
+            if (j == PEEK)
+                e = (1u << 28) | ((uint32_t) PEEK << 24) | cur;
+            table[(size_t) b * (1u << PEEK) + v] = e;
+        }
+    }
+}
+
+// One thread per block walks the stream; out_status[b] = 0 ok, else error.
+__global__ void k_huff_decode(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
+                              const uint64_t* __restrict__ payload_off, const int32_t* __restrict__ child, const uint8_t* __restrict__ sym,
+                              const uint32_t* __restrict__ table, const uint32_t* __restrict__ tree_status, uint8_t* __restrict__ out,
+                              const uint64_t* __restrict__ out_base, uint32_t* __restrict__ out_status)
+{
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    {
+        if (tree_status[b])
+        {
+            out_status[b] = 1;
+            continue;
+        }
+        const HuffMetaRec& M     = meta[b];
+        const uint8_t*     src   = payload + payload_off[b];
+        const uint64_t     nbits = (uint64_t) M.encoded_size * 8;
+        const int32_t*     ch    = child + (size_t) b * TREE_CAP * 2;
+        const uint8_t*     sy    = sym + (size_t) b * TREE_CAP;
+        const uint32_t*    tb    = table + (size_t) b * (1u << PEEK);
+        uint8_t*           dst   = out + out_base[b];
+        uint64_t           pos   = 0;
+        uint32_t           k     = 0;
+        uint32_t           err   = 0;
+        // bit reader: 64-bit window starting at byte (pos >> 3)
+        auto peek = [&](uint64_t p, int n) -> uint32_t {
+            uint64_t w   = 0;
+            uint64_t byt = p >> 3;
+            for (int i = 0; i < 8; ++i)
+                w = (w << 8) | (byt + i < M.encoded_size ? src[byt + i] : 0);
+            return (uint32_t) ((w << (p & 7)) >> (64 - n));
+        };
+        while (k < M.orig_size)
+        {
+            if (pos >= nbits)
+            {
+                err = 1;  // ran out of data (decoded_idx != orig_size)
+                break;
+            }
+            const uint32_t e    = tb[peek(pos, PEEK)];
+            const uint32_t kind = e >> 28, used = (e >> 24) & 15;
+            if (pos + used > nbits)
+            {
+                // the walk would read past the data: re-walk bit by bit to find where it stops
+                uint32_t cur = 0;
+                bool     leaf = false;
+                while (pos < nbits)
+                {
+                    const int nx = ch[2 * cur + (int) peek(pos, 1)];
+                    ++pos;
+                    if (nx < 0)
+                    {
+                        err = 1;
+                        break;
+                    }
+                    cur = (uint32_t) nx;
+                    if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
+                    {
+                        dst[k++] = sy[cur];
+                        leaf     = true;
+                        break;
+                    }
+                }
+                if (err || !leaf)
+                {
+                    err = 1;
+                    break;
+                }
+                continue;
+            }
+            if (kind == 0)
+            {
+                dst[k++] = (uint8_t) (e & 0xFFFFFF);
+                pos += used;
+            }
+            else if (kind == 2)
+            {
+                err = 1;
+                break;
+            }
+            else
+            {
+                uint32_t cur = e & 0xFFFFFF;
+                pos += PEEK;
+                bool leaf = false;
+                while (pos < nbits)
+                {
+                    const int nx = ch[2 * cur + (int) peek(pos, 1)];
+                    ++pos;
+                    if (nx < 0)
+                        break;
+                    cur = (uint32_t) nx;
+                    if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
+                    {
+                        dst[k++] = sy[cur];
+                        leaf     = true;
+                        break;
+                    }
+                }
+                if (!leaf)
+                {
+                    err = 1;
+                    break;
+                }
+            }
+        }
+        if (!err)
+        {
+            // the reference leaves the bit loop of the current byte and keeps walking the
+            // remaining whole bytes: a completed symbol there would overrun its buffer (error),
+            // a dead edge is an error, an unfinished walk is ignored.
+            uint64_t p2  = (pos + 7) & ~7ull;
+            uint32_t cur = 0;
+            while (p2 < nbits)
+            {
+                const int nx = ch[2 * cur + (int) peek(p2, 1)];
+                ++p2;
+                if (nx < 0)
+                {
+                    err = 1;
+                    break;
+                }
+                cur = (uint32_t) nx;
+                if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
+                {
+                    err = 1;
+                    break;
+                }
+            }
+        }
+        out_status[b] = err;
+    }
+}
+
+}  // namespace
+
+bool HuffWorkspace::reserve(uint32_t nblocks, uint32_t ntiles)
+{
+    if (nblocks > cap_b)
+    {
+        (void) hipFree(codes);
+        (void) hipFree(tree_child);
+        (void) hipFree(tree_sym);
+        (void) hipFree(table);
+        (void) hipFree(status);
+        cap_b = nblocks + 8;
+        BRA_HIP_CHECK(hipMalloc(&codes, (size_t) cap_b * 256 * 4));
+        tree_child = nullptr;  // decode buffers allocated lazily
+        tree_sym   = nullptr;
+        table      = nullptr;
+        BRA_HIP_CHECK(hipMalloc(&status, (size_t) cap_b * 4));
+        cap_tree = 0;
+    }
+    if (ntiles > cap_t)
+    {
+        (void) hipFree(tbits);
+        (void) hipFree(tbit0);
+        cap_t = ntiles + ntiles / 4 + 64;
+        BRA_HIP_CHECK(hipMalloc(&tbits, (size_t) cap_t * 4));
+        BRA_HIP_CHECK(hipMalloc(&tbit0, (size_t) cap_t * 8));
+    }
+    return true;
+}
+
+bool HuffWorkspace::reserve_tree(uint32_t nblocks)
+{
+    if (nblocks <= cap_tree)
+        return true;
+    (void) hipFree(tree_child);
+    (void) hipFree(tree_sym);
+    (void) hipFree(table);
+    cap_tree = nblocks;
+    BRA_HIP_CHECK(hipMalloc(&tree_child, (size_t) cap_tree * TREE_CAP * 8));
+    BRA_HIP_CHECK(hipMalloc(&tree_sym, (size_t) cap_tree * TREE_CAP));
+    BRA_HIP_CHECK(hipMalloc(&table, (size_t) cap_tree * (1u << PEEK) * 4));
+    return true;
+}
+
+void HuffWorkspace::release()
+{
+    tiling.release();
+    (void) hipFree(codes);
+    (void) hipFree(tbits);
+    (void) hipFree(tbit0);
+    (void) hipFree(tree_child);
+    (void) hipFree(tree_sym);
+    (void) hipFree(table);
+    (void) hipFree(status);
+    *this = HuffWorkspace{};
+}
+
+bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc* h_rle_cap_blocks, uint32_t nblocks,
+                        const uint32_t* d_hist, const uint32_t* d_rle_size, HuffMetaRec* d_meta, uint64_t* d_payload_off,
+                        uint8_t* d_payload, uint64_t payload_cap, uint64_t* h_total, hipStream_t s)
+{
+    if (!w.tiling.build(h_rle_cap_blocks, nblocks, RLE_TILE, s))
+        return false;
+    const uint32_t nt = w.tiling.n;
+    if (!w.reserve(nblocks, nt))
+        return false;
+    hipLaunchKernelGGL(k_huff_build, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_hist, d_rle_size, nblocks, d_meta, w.codes);
+    hipLaunchKernelGGL(k_huff_offsets, dim3(1), dim3(TPB), 0, s, d_meta, nblocks, d_payload_off);
+    const uint32_t grid = std::min<uint32_t>(nt, 8192);
+    hipLaunchKernelGGL(k_huff_tilebits, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.tbits);
+    hipLaunchKernelGGL(k_huff_tilescan, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
+                       d_payload_off, w.tbits, w.tbit0);
+    BRA_HIP_CHECK(hipMemcpyAsync(h_total, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s));
+    BRA_HIP_CHECK(hipStreamSynchronize(s));
+    if (*h_total + 8 > payload_cap)
+    {
+        bra_hip_report("huffman: payload capacity %llu too small for %llu bytes", (unsigned long long) payload_cap,
+                       (unsigned long long) *h_total);
+        return false;
+    }
+    uint32_t* words = reinterpret_cast<uint32_t*>(d_payload);
+    hipLaunchKernelGGL(k_huff_zero, dim3(std::min<uint32_t>(div_up(nt, 256), 4096)), dim3(256), 0, s, w.tbits, w.tbit0, nt, words);
+    hipLaunchKernelGGL(k_huff_pack, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.codes, w.tbits, w.tbit0, words);
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, uint32_t nblocks, const uint8_t* d_payload, const uint64_t* d_payload_off,
+                        uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s)
+{
+    if (!w.reserve(nblocks, 1) || !w.reserve_tree(nblocks))
+        return false;
+    hipLaunchKernelGGL(k_huff_tree, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, w.tree_child, w.tree_sym, w.status);
+    hipLaunchKernelGGL(k_huff_table, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, w.tree_child, w.tree_sym, nblocks, w.table);
+    hipLaunchKernelGGL(k_huff_decode, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child,
+                       w.tree_sym, w.table, w.status, d_out, d_out_base, d_status);
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+namespace {
+__global__ void __launch_bounds__(256) k_hist256(const uint8_t* __restrict__ in, const Piece* __restrict__ tiles, uint32_t ntiles,
+                                                 uint32_t* __restrict__ hist)
+{
+    __shared__ uint32_t h[256];
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        h[threadIdx.x] = 0;
+        __syncthreads();
+        const Piece P = tiles[t];
+        for (uint32_t i = threadIdx.x; i < P.len; i += 256)
+            atomicAdd(&h[in[P.off + i]], 1u);
+        __syncthreads();
+        if (h[threadIdx.x])
+            atomicAdd(&hist[(size_t) P.block * 256 + threadIdx.x], h[threadIdx.x]);
+        __syncthreads();
+    }
+}
+}  // namespace
+
+bool histogram_device(Tiling& tiling, const uint8_t* d_in, const BlockDesc* h_blocks, uint32_t nblocks, uint32_t* d_hist, hipStream_t s)
+{
+    if (!tiling.build(h_blocks, nblocks, RLE_TILE, s))
+        return false;
+    BRA_HIP_CHECK(hipMemsetAsync(d_hist, 0, (size_t) nblocks * 256 * 4, s));
+    if (tiling.n)
+        hipLaunchKernelGGL(k_hist256, dim3(std::min<uint32_t>(tiling.n, 8192)), dim3(256), 0, s, d_in, tiling.d_pieces, tiling.n, d_hist);
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+}  // namespace bra

@@ -1,0 +1,114 @@
+// mtf.h -- move-to-front stage (device pointers) + the block tiling helper shared by the stages.
+#pragma once
+
+#include "bra_hip_common.h"
+
+#include <algorithm>
+#include <vector>
+
+namespace bra {
+
+// A fixed-size piece of one block (the last piece of a block may be short).
+struct Piece
+{
+    uint64_t off;    // absolute offset of the piece in the batch buffer
+    uint32_t start;  // offset inside its block
+    uint32_t len;
+    uint32_t block;
+    uint32_t pad;
+};
+
+// Cut every block into pieces of `piece` bytes; device copies of the piece list and of the
+// per-block (first piece, piece count).  Rebuilt only when the geometry changes.
+struct Tiling
+{
+    uint32_t               n        = 0;
+    Piece*                 d_pieces = nullptr;
+    uint32_t*              d_first  = nullptr;
+    uint32_t*              d_count  = nullptr;
+    std::vector<Piece>     h_pieces;
+    std::vector<uint32_t>  h_first, h_count;
+    std::vector<BlockDesc> key;
+    uint32_t               key_piece = 0;
+    size_t                 cap_p = 0, cap_b = 0;
+
+    bool build(const BlockDesc* blocks, uint32_t nblocks, uint32_t piece, hipStream_t s)
+    {
+        if (piece == key_piece && key.size() == nblocks &&
+            std::equal(key.begin(), key.end(), blocks, [](const BlockDesc& a, const BlockDesc& b) { return a.off == b.off && a.len == b.len; }))
+            return true;
+        h_pieces.clear();
+        h_first.assign(nblocks, 0);
+        h_count.assign(nblocks, 0);
+        for (uint32_t b = 0; b < nblocks; ++b)
+        {
+            h_first[b] = (uint32_t) h_pieces.size();
+            for (uint32_t st = 0; st < blocks[b].len; st += piece)
+                h_pieces.push_back(Piece{blocks[b].off + st, st, std::min(piece, blocks[b].len - st), b, 0});
+            h_count[b] = (uint32_t) h_pieces.size() - h_first[b];
+        }
+        n = (uint32_t) h_pieces.size();
+        if (n > cap_p)
+        {
+            (void) hipFree(d_pieces);
+            cap_p = n + n / 4 + 16;
+            BRA_HIP_CHECK(hipMalloc(&d_pieces, cap_p * sizeof(Piece)));
+        }
+        if (nblocks > cap_b)
+        {
+            (void) hipFree(d_first);
+            (void) hipFree(d_count);
+            cap_b = nblocks + 16;
+            BRA_HIP_CHECK(hipMalloc(&d_first, cap_b * 4));
+            BRA_HIP_CHECK(hipMalloc(&d_count, cap_b * 4));
+        }
+        BRA_HIP_CHECK(hipMemcpyAsync(d_pieces, h_pieces.data(), n * sizeof(Piece), hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipMemcpyAsync(d_first, h_first.data(), nblocks * 4, hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipMemcpyAsync(d_count, h_count.data(), nblocks * 4, hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));  // host vectors are the source of the async copies
+        key.assign(blocks, blocks + nblocks);
+        key_piece = piece;
+        return true;
+    }
+
+    void release()
+    {
+        (void) hipFree(d_pieces);
+        (void) hipFree(d_first);
+        (void) hipFree(d_count);
+        *this = Tiling{};
+    }
+};
+
+constexpr uint32_t MTF_SEG = 2048;  // symbols per thread-segment
+
+struct MtfWorkspace
+{
+    Tiling tiling;
+    void*  state     = nullptr;
+    size_t cap_state = 0;
+
+    bool reserve(size_t bytes)
+    {
+        if (bytes <= cap_state)
+            return true;
+        (void) hipFree(state);
+        cap_state = bytes + bytes / 4 + 4096;
+        BRA_HIP_CHECK(hipMalloc(&state, cap_state));
+        return true;
+    }
+    void release()
+    {
+        tiling.release();
+        (void) hipFree(state);
+        state     = nullptr;
+        cap_state = 0;
+    }
+};
+
+bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s);
+// d_tmp: scratch of the batch size (labels)
+bool mtf_decode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, uint8_t* d_tmp, const BlockDesc* h_blocks, uint32_t nblocks,
+                       hipStream_t s);
+
+}  // namespace bra

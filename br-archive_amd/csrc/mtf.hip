@@ -1,0 +1,312 @@
+// mtf.hip -- move-to-front encode/decode for a batch of independent blocks.
+//
+// Replaces bra_mtf_encode2 / bra_mtf_decode2 (reference src/encoders/bra_mtf.c:67-82, :98-115;
+// table init :9-13, encode step :16-32 = output position then move to front, decode step :35-46).
+//
+// Encode is made segment-parallel with the recency formulation: the MTF table at any point lists
+// symbols by decreasing last-occurrence time, never-seen symbols last in ascending order (the
+// initial identity table is the recency order of a virtual prefix 255, 254, ..., 0).  So
+//   k_mtf_lastocc   last occurrence of every symbol inside each segment (LDS atomicMax),
+//   k_mtf_scan      exclusive max-scan over the segments of a block -> start-of-segment times,
+//   k_mtf_encode    each thread rebuilds its segment's start table (a wave sorts 256 times per
+//                   table) and runs the sequential MTF on a private LDS table.
+// Decode uses relabelling: a decode step moves table POSITION p to the front whatever the table
+// holds, so decoding a segment from the identity table gives labels u_i and an end permutation
+// P_k; the true start tables satisfy S_{k+1}[j] = S_k[P_k[j]] and the output is S_k[u_i].
+#include "mtf.h"
+
+namespace bra {
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ uint32_t haszero8(uint32_t x) { return (x - 0x01010101u) & ~x & 0x80808080u; }
+
+// ------------------------------------------------------------------------------------------------
+// encode
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__ in, const Piece* __restrict__ segs, uint32_t nseg,
+                                                     int32_t* __restrict__ state)
+{
+    __shared__ int32_t lo[256];
+    for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x)
+    {
+        lo[threadIdx.x] = -1;
+        __syncthreads();
+        const Piece    P = segs[s];
+        const uint8_t* p = in + P.off;
+        for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
+            atomicMax(&lo[p[i]], (int32_t) i);
+        __syncthreads();
+        state[(size_t) s * 256 + threadIdx.x] = lo[threadIdx.x] >= 0 ? (int32_t) P.start + lo[threadIdx.x] : -1;
+        __syncthreads();
+    }
+}
+
+// One workgroup per block; thread c scans symbol c over the block's segments (exclusive max).
+__global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
+                                                  uint32_t nblocks, int32_t* __restrict__ state)
+{
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const uint32_t s0  = first_seg[b];
+        const uint32_t ns  = nseg_blk[b];
+        int32_t        run = -1;
+        const uint32_t c   = threadIdx.x;
+        uint32_t       k   = 0;
+        for (; k + 8 <= ns; k += 8)
+        {
+            int32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                v[u] = state[(size_t) (s0 + k + u) * 256 + c];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+            {
+                state[(size_t) (s0 + k + u) * 256 + c] = run;
+                run                                    = max(run, v[u]);
+            }
+        }
+        for (; k < ns; ++k)
+        {
+            const int32_t v                       = state[(size_t) (s0 + k) * 256 + c];
+            state[(size_t) (s0 + k) * 256 + c] = run;
+            run                                   = max(run, v);
+        }
+    }
+}
+
+// LDS table of thread t, dword w (4 table entries, little-endian) lives at tbl[w * TPB + t].
+__device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st, uint32_t* tbl, uint32_t owner)
+{
+    // K(c) = last-occurrence time + 256 for seen symbols, 255 - c for unseen: the table is the
+    // symbols by decreasing K.  Sort ascending by (2^40 - K) << 8 | c.
+    const int lane = lane_id();
+    uint64_t  k[4];
+    uint32_t  v[4];
+    const int4 tv = reinterpret_cast<const int4*>(st)[lane];
+    const int32_t tt[4] = {tv.x, tv.y, tv.z, tv.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = lane * 4 + r;
+        const uint64_t K = tt[r] >= 0 ? (uint64_t) tt[r] + 256u : (uint64_t) (255u - c);
+        k[r]             = (((1ull << 40) - K) << 8) | c;
+        v[r]             = c;
+    }
+    wave_bitonic_sort4(k, v, 256);
+    tbl[lane * TPB + owner] = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
+}
+
+__global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
+                                                    uint32_t nseg, const int32_t* __restrict__ state)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];  // 64 * TPB dwords
+    const uint32_t t    = threadIdx.x;
+    const int      lane = lane_id();
+    const uint32_t wave = t >> 6;
+    for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
+    {
+        // tables for the 64 segments of this wave
+        for (int q = 0; q < 64; ++q)
+        {
+            const uint32_t owner = wave * 64 + q;
+            const uint32_t s     = g0 + owner;
+            if (s >= nseg)
+                break;
+            if (segs[s].start == 0)
+                tbl[lane * TPB + owner] = (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u;
+            else
+                build_table_wave(state + (size_t) s * 256, tbl, owner);
+        }
+        __syncthreads();
+        const uint32_t s = g0 + t;
+        if (s < nseg)
+        {
+            const Piece    P   = segs[s];
+            const uint8_t* src = in + P.off;
+            uint8_t*       dst = out + P.off;
+            for (uint32_t i = 0; i < P.len; ++i)
+            {
+                const uint32_t c  = src[i];
+                const uint32_t cc = c * 0x01010101u;
+                uint32_t       w = 0, z = 0;
+                uint32_t       cur = 0;
+                for (; w < 64; ++w)  // always found: the table is a permutation of 0..255
+                {
+                    cur = tbl[w * TPB + t];
+                    z   = haszero8(cur ^ cc);
+                    if (z)
+                        break;
+                }
+                if (w == 64)
+                    break;
+                const uint32_t b = (uint32_t) __builtin_ctz(z) >> 3;
+                dst[i]           = (uint8_t) (w * 4 + b);
+                // move to front: entries [0, p) shift up by one, entry 0 = c
+                {
+                    const uint32_t below   = w ? tbl[(w - 1) * TPB + t] : c << 24;
+                    const uint32_t shifted = (cur << 8) | (below >> 24);
+                    const uint32_t keep    = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
+                    tbl[w * TPB + t]       = (cur & keep) | (shifted & ~keep);
+                    uint32_t hi            = below;
+                    for (int x = (int) w - 1; x >= 0; --x)
+                    {
+                        const uint32_t lo  = x ? tbl[(x - 1) * TPB + t] : c << 24;
+                        tbl[x * TPB + t]   = (hi << 8) | (lo >> 24);
+                        hi                 = lo;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decode
+// ------------------------------------------------------------------------------------------------
+// Pass 1: decode each segment from the identity table; labels -> out, end table -> perm.
+__global__ void __launch_bounds__(TPB) k_mtf_dec_local(const uint8_t* __restrict__ in, uint8_t* __restrict__ lab,
+                                                       const Piece* __restrict__ segs, uint32_t nseg, uint32_t* __restrict__ perm)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
+    {
+        const uint32_t s = g0 + t;
+        if (s < nseg)
+        {
+            for (int w = 0; w < 64; ++w)
+                tbl[w * TPB + t] = (uint32_t) (w * 4) * 0x01010101u + 0x03020100u;
+            const Piece    P   = segs[s];
+            const uint8_t* src = in + P.off;
+            uint8_t*       dst = lab + P.off;
+            for (uint32_t i = 0; i < P.len; ++i)
+            {
+                const uint32_t p   = src[i];
+                const uint32_t w   = p >> 2, b = p & 3;
+                const uint32_t cur = tbl[w * TPB + t];
+                const uint32_t c   = (cur >> (8 * b)) & 0xFF;
+                dst[i]             = (uint8_t) c;
+                const uint32_t below   = w ? tbl[(w - 1) * TPB + t] : c << 24;
+                const uint32_t shifted = (cur << 8) | (below >> 24);
+                const uint32_t keep    = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
+                tbl[w * TPB + t]       = (cur & keep) | (shifted & ~keep);
+                uint32_t hi            = below;
+                for (int x = (int) w - 1; x >= 0; --x)
+                {
+                    const uint32_t lo = x ? tbl[(x - 1) * TPB + t] : c << 24;
+                    tbl[x * TPB + t]  = (hi << 8) | (lo >> 24);
+                    hi                = lo;
+                }
+            }
+            for (int w = 0; w < 64; ++w)
+                perm[(size_t) s * 64 + w] = tbl[w * TPB + t];
+        }
+    }
+}
+
+// Pass 2: one wave per block composes start tables S_{k+1}[j] = S_k[P_k[j]] (in place in perm:
+// perm[k] becomes S_k).
+__global__ void __launch_bounds__(64) k_mtf_dec_compose(const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
+                                                        uint32_t nblocks, uint32_t* __restrict__ perm)
+{
+    const int lane = lane_id();
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const uint32_t s0 = first_seg[b], ns = nseg_blk[b];
+        uint32_t       S  = (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u;  // identity
+        uint32_t       Pn = perm[(size_t) s0 * 64 + lane];
+        for (uint32_t k = 0; k < ns; ++k)
+        {
+            const uint32_t Pk = Pn;
+            if (k + 1 < ns)
+                Pn = perm[(size_t) (s0 + k + 1) * 64 + lane];
+            perm[(size_t) (s0 + k) * 64 + lane] = S;
+            uint32_t nS = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const uint32_t j   = (Pk >> (8 * r)) & 0xFF;
+                const uint32_t src = __shfl(S, (int) (j >> 2), 64);
+                nS |= ((src >> (8 * (j & 3))) & 0xFF) << (8 * r);
+            }
+            S = nS;
+        }
+    }
+}
+
+// Pass 3: out = S_k[label]
+__global__ void __launch_bounds__(TPB) k_mtf_dec_relabel(const uint8_t* __restrict__ lab, uint8_t* __restrict__ out,
+                                                         const Piece* __restrict__ segs, uint32_t nseg, const uint32_t* __restrict__ perm)
+{
+    __shared__ uint8_t S[256];
+    for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x)
+    {
+        if (threadIdx.x < 64)
+            reinterpret_cast<uint32_t*>(S)[threadIdx.x] = perm[(size_t) s * 64 + threadIdx.x];
+        __syncthreads();
+        const Piece P = segs[s];
+        for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
+            out[P.off + i] = S[lab[P.off + i]];
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s)
+{
+    if (!w.tiling.build(h_blocks, nblocks, MTF_SEG, s))
+        return false;
+    const uint32_t nseg = w.tiling.n;
+    if (!w.reserve((size_t) nseg * 256 * 4))
+        return false;
+    int32_t* st = reinterpret_cast<int32_t*>(w.state);
+    hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(nseg, 8192)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
+    hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
+                       nblocks, st);
+    const size_t lds = 64 * TPB * 4;
+    static bool  attr = false;
+    if (!attr)
+    {
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
+                       w.tiling.d_pieces, nseg, st);
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+bool mtf_decode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, uint8_t* d_tmp, const BlockDesc* h_blocks, uint32_t nblocks,
+                       hipStream_t s)
+{
+    if (!w.tiling.build(h_blocks, nblocks, MTF_SEG, s))
+        return false;
+    const uint32_t nseg = w.tiling.n;
+    if (!w.reserve((size_t) nseg * 256))
+        return false;
+    uint32_t*    perm = reinterpret_cast<uint32_t*>(w.state);
+    const size_t lds  = 64 * TPB * 4;
+    static bool  attr = false;
+    if (!attr)
+    {
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_mtf_dec_local, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_tmp,
+                       w.tiling.d_pieces, nseg, perm);
+    hipLaunchKernelGGL(k_mtf_dec_compose, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count,
+                       nblocks, perm);
+    hipLaunchKernelGGL(k_mtf_dec_relabel, dim3(std::min<uint32_t>(nseg, 16384)), dim3(TPB), 0, s, d_tmp, d_out, w.tiling.d_pieces, nseg,
+                       perm);
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+}  // namespace bra

@@ -1,0 +1,38 @@
+// rle.h -- PackBits RLE stage (device pointers).
+#pragma once
+
+#include "mtf.h"  // Tiling, Piece
+
+namespace bra {
+
+constexpr uint32_t RLE_TILE = 4096;
+
+// Worst-case RLE output of an n-byte block (all literals): n + ceil(n/128).
+__host__ __device__ inline uint64_t rle_capacity(uint32_t n) { return (uint64_t) n + (n + 127) / 128 + 16; }
+
+struct RleWorkspace
+{
+    Tiling   tiling;
+    void*    runs = nullptr;
+    void*    link = nullptr;
+    void*    gaps = nullptr;
+    void*    offs = nullptr;
+    uint32_t cap  = 0;
+    bool     reserve(uint32_t ntiles);
+    void     release();
+};
+
+// Encode every block of d_in (geometry h_blocks) into d_out at d_rle_base[b]; per-block output
+// sizes to d_rle_size, byte histograms of the output to d_hist[b * 256 + c].
+bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_blocks, uint32_t nblocks, const uint64_t* d_rle_base,
+                       uint8_t* d_out, uint32_t* d_rle_size, uint32_t* d_hist, hipStream_t s);
+
+// Decode: block b's stream is at d_in + d_in_base[b] (d_in_size[b] bytes); output goes to
+// d_out + d_out_base[b] (capacity d_out_cap[b]).  d_out_size[b] = decoded size, 0 on a malformed
+// stream (bra_rle_decode_compute_size semantics).  d_recs: 8 bytes per record, block b's records
+// from index d_rec_base[b] (a block needs <= in_size/2 + 1 records); d_nrec: nblocks words.
+bool rle_decode_device(const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
+                       const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, void* d_recs, const uint64_t* d_rec_base,
+                       uint32_t* d_nrec, hipStream_t s);
+
+}  // namespace bra

@@ -1,0 +1,200 @@
+"""Parity of the HIP path (through the C-ABI of libbra_hip.so) with the reference.
+
+Checker: oracle/ (the CPU restatement, itself pinned to the reference's golden vectors in
+tests/test_oracle.py) and tests/golden/golden.npz (outputs of the reference encoders).
+Bar: bit-exact for every stage (BWT last column + primary index, MTF, RLE, Huffman lengths /
+sizes / payload) and for the decoded bytes.
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HDR = 268
+
+
+@pytest.fixture(scope="module")
+def bra():
+    return importlib.import_module("br-archive_amd")
+
+
+@pytest.fixture(scope="module")
+def codec(bra):
+    c = bra.BlockCodec(0)
+    yield c
+    c.close()
+
+
+# ---- reference known answers (test/test_bra_encoders.cpp) through the single-block C-ABI ----------
+def test_kat_bwt(bra):
+    assert bra.bwt_encode(b"BANANA") == (b"NNBAAA", 3)
+    fox = b"The quick brown fox jumps over the lazy dog."
+    assert bra.bwt_encode(fox) == (b"kynxeserg.l i hhv otTu c uwd rfm ebp qjoooza", 9)
+    assert bra.bwt_decode(b"NNBAAA", 3) == b"BANANA"
+    assert bra.bwt_decode(b"kynxeserg.l i hhv otTu c uwd rfm ebp qjoooza", 9) == fox
+
+
+def test_kat_mtf(bra):
+    assert bra.mtf_encode(b"BANANA") == bytes([66, 66, 78, 1, 1, 1])
+    assert bra.mtf_decode(bytes([0x4E, 0, 0x43, 0x43, 0, 0])) == b"NNBAAA"
+
+
+def test_kat_rle(bra):
+    assert bra.rle_encode(b"A" * 10) == bytes([(-9) & 0xFF, 65])
+    assert bra.rle_encode(b"AAAAABBBCD") == bytes([(-4) & 0xFF, 65, (-2) & 0xFF, 66, 1, 67, 68])
+    assert len(bra.rle_encode(b"ABCDEFGH")) == 9
+    for s in (b"A" * 10, b"AAAAABBBCD", b"ABCDEFGH"):
+        assert bra.rle_decode(bra.rle_encode(s)) == s
+    assert bra.rle_encode(b"") is None
+    assert bra.rle_decode_compute_size(bytes([5, 1, 2])) == 0
+    assert bra.rle_decode_compute_size(bytes([0x80])) == 0
+    assert bra.rle_decode(bytes([0xFE])) is None
+
+
+def test_kat_huffman(bra):
+    h = bra.huffman_encode(b"BANANA")
+    assert (h.orig_size, h.encoded_size) == (6, 2)
+    assert (h.lengths[0], h.lengths[65], h.lengths[66], h.lengths[78]) == (0, 1, 2, 2)
+    assert h.data == bytes([155, 0])
+    assert bra.huffman_decode(h.lengths, h.orig_size, h.encoded_size, h.data) == b"BANANA"
+    h = bra.huffman_encode(b"AAAAA")
+    assert (h.orig_size, h.encoded_size, h.lengths[65], h.data) == (5, 1, 1, b"\0")
+    assert bra.huffman_encode(b"") is None
+    lens = bra.huffman_encode(b"abcde").lengths
+    assert [lens[c] for c in b"abcde"] == [2, 2, 3, 3, 2]
+
+
+# ---- every golden vector, stage by stage, through the single-block C-ABI --------------------------
+def test_golden_stages(bra, golden):
+    for name, g in golden.items():
+        inp = g["input"]
+        L, pi = bra.bwt_encode(inp)
+        assert (pi, L) == (g["pi"], g["bwt"]), name
+        assert bra.mtf_encode(L) == g["mtf"], name
+        assert bra.rle_encode(g["mtf"]) == g["rle"], name
+        h = bra.huffman_encode(g["rle"])
+        assert h.lengths == g["lengths"], name
+        assert (h.orig_size, h.encoded_size) == (g["orig_size"], g["encoded_size"]), name
+        assert h.data == g["payload"], name
+        # inverse chain
+        assert bra.huffman_decode(g["lengths"], g["orig_size"], g["encoded_size"], g["payload"]) == g["rle"], name
+        assert bra.rle_decode(g["rle"]) == g["mtf"], name
+        assert bra.mtf_decode(g["mtf"]) == g["bwt"], name
+        assert bra.bwt_decode(g["bwt"], g["pi"]) == inp, name
+
+
+# ---- batched device path vs the oracle ----------------------------------------------------------
+def _encode_check(bra, codec, orc, data: np.ndarray, block_size: int, check_blocks=None, roundtrip=True):
+    import torch
+
+    d = torch.from_numpy(data).cuda()
+    total = data.size
+    nb = codec.num_blocks(total, block_size)
+    hdr, off, pay = codec.encode(d, block_size)
+    torch.cuda.synchronize()
+    hdr_h = hdr.cpu().numpy()
+    off_h = off.cpu().numpy()
+    pay_h = pay.cpu().numpy()
+    blocks = range(nb) if check_blocks is None else check_blocks
+    for b in blocks:
+        lo, hi = b * block_size, min(total, (b + 1) * block_size)
+        blk = data[lo:hi].tobytes()
+        ch = orc.encode_block(blk)
+        pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
+        assert pi == ch.primary_index, ("pi", b)
+        assert lens == ch.lengths, ("lengths", b)
+        assert (osz, esz) == (ch.orig_size, ch.encoded_size), ("sizes", b)
+        assert int(off_h[b + 1] - off_h[b]) == esz, ("offset", b)
+        assert pay_h[off_h[b]: off_h[b] + esz].tobytes() == ch.payload, ("payload", b)
+    if roundtrip:
+        out = codec.decode(hdr, off, pay, total, block_size)
+        torch.cuda.synchronize()
+        assert torch.equal(out, d), "round trip"
+    return hdr_h, off_h
+
+
+def _stage_check(bra, codec, orc, data: np.ndarray, block_size: int, b: int):
+    """Diagnostic: compare the intermediate stages of block b of the last encode."""
+    import ctypes as C
+
+    lo, hi = b * block_size, min(data.size, (b + 1) * block_size)
+    blk = data[lo:hi].tobytes()
+    ch = orc.encode_block(blk)
+    import torch
+
+    n = hi - lo
+    L = torch.empty(n, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    buf = (C.c_uint8 * n)()
+    hip.hipMemcpy(buf, codec.stage_ptr(0) + lo, n, 2)
+    assert bytes(buf) == ch.bwt, ("bwt stage", b)
+    hip.hipMemcpy(buf, codec.stage_ptr(1) + lo, n, 2)
+    assert bytes(buf) == ch.mtf, ("mtf stage", b)
+    del L
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_batch_64k_blocks(bra, codec, orc, kind):
+    data = bra.synth_fill(kind, 48 * 65536 + 777, 65536, first_block=100 * kind)
+    try:
+        _encode_check(bra, codec, orc, data, 65536)
+    except AssertionError:
+        for b in range(3):
+            _stage_check(bra, codec, orc, data, 65536, b)
+        raise
+
+
+def test_batch_tiny_and_ragged(bra, codec, orc):
+    rng = np.random.default_rng(7)
+    for bs in (1, 2, 3, 5, 8, 64, 255, 256, 257, 1000):
+        data = rng.integers(0, 3, size=bs * 7 + (bs // 2), dtype=np.uint8)
+        _encode_check(bra, codec, orc, data, bs)
+
+
+def test_batch_periodic_and_runs(bra, codec, orc):
+    parts = [
+        np.zeros(4096, np.uint8),
+        np.frombuffer(b"ab" * 2048, np.uint8),
+        np.frombuffer(b"ba" * 2048, np.uint8),
+        np.frombuffer((b"xyz" * 2000)[:4096], np.uint8),
+        np.frombuffer((b"abcabca" * 600)[:4096], np.uint8),
+        np.full(4096, 255, np.uint8),
+        np.repeat(np.arange(16, dtype=np.uint8), 256),
+        np.repeat(np.arange(32, dtype=np.uint8), 128),
+    ]
+    data = np.concatenate(parts)
+    _encode_check(bra, codec, orc, data, 4096)
+
+
+def test_config1_tiled_block(bra, codec, golden):
+    import torch
+
+    g = golden["cfg1_tiled_65536"]
+    data = np.frombuffer(g["input"], np.uint8).copy()
+    d = torch.from_numpy(data).cuda()
+    hdr, off, pay = codec.encode(d, 65536)
+    pi, lens, osz, esz = bra.parse_header(hdr[0].cpu().numpy().tobytes())
+    assert (pi, lens, osz, esz) == (g["pi"], g["lengths"], g["orig_size"], g["encoded_size"])
+    assert pay[: esz].cpu().numpy().tobytes() == g["payload"]
+    assert torch.equal(codec.decode(hdr, off, pay, 65536, 65536), d)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_full_size_256mib(bra, codec, orc, kind):
+    """BASELINE configs 2/3 at full size: round trip + oracle on sampled blocks."""
+    total, bs = 256 << 20, 1 << 20
+    data = bra.synth_fill(kind, total, bs)
+    _encode_check(bra, codec, orc, data, bs, check_blocks=[0, 1, 77, 128, 254, 255])
+
+
+def test_8mib_blocks_sym16(bra, codec, orc):
+    """BASELINE config 5 block shape (8 MiB, 16-symbol geometric), scaled to 4 blocks."""
+    total, bs = 4 * (8 << 20), 8 << 20
+    data = bra.synth_fill(2, total, bs)
+    _encode_check(bra, codec, orc, data, bs, check_blocks=[0, 3])
