@@ -64,6 +64,13 @@ class HuffmanChunk:
 
 
 def _load() -> C.CDLL:
+    # One HIP runtime per process: torch ships its own libamdhip64 (same SONAME).  Loading torch
+    # first makes libbra_hip.so bind to that copy instead of opening a second runtime that could
+    # no longer see the GPUs.  Without torch the library uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `make -C br-archive_amd` (or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)
