@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""bench.py -- br-archive block codec on MI355X: encode GB/s of input bytes (BASELINE.json metric).
+
+One step = one pass of the hot path (BWT -> MTF -> PackBits RLE -> canonical Huffman, the chunk
+encoder of lib_bra_io_file_chunks.c:217-245) over one batch of synthetic blocks that is already
+resident in HBM: BASELINE configs[1], 256 x 1 MiB "enwik-style" text blocks per GPU.  With N > 1
+GPUs (torchrun, one process per GPU, RCCL) every rank encodes its own 256 MiB (weak scaling) and the
+compressed chunks are gathered to rank 0 over xGMI inside the step (SURVEY 8.1 row e).
+
+Printed (rank 0, one JSON line): the metric, `roofline` for the dominant kernel (algorithmic bytes
+per launch / average launch time measured with HIP events on the codec's stream during the timed
+steps), and `cpu_baseline`: the reference's own src/encoders (oracle/_ref/libbraref.so, compiled
+from the reference sources) timed on this host on a bounded sample of the same blocks.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "encode GB/s (input bytes) on 256 MiB synthetic blocks, 1/2/4/8 GPU; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+KINDS = {"text": 0, "random": 1, "sym16": 2, "tiled": 3}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kind", default="text", choices=sorted(KINDS))
+    ap.add_argument("--block-size", type=int, default=1 << 20)
+    ap.add_argument("--bytes-per-gpu", type=int, default=256 << 20)
+    ap.add_argument("--cpu-blocks", type=int, default=32, help="blocks in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--profile-all", action="store_true", help="time every kernel during the timed steps")
+    return ap.parse_args()
+
+
+def cpu_baseline(data_np, bs, nblocks, threads, gpu_chunks):
+    """Reference encoders on host cores: one block per task, `threads` workers (ctypes drops the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import Oracle, Reference, have_ref
+
+    impl, kind = (Reference(), "reference") if have_ref() else (Oracle(), "port")
+    nblocks = min(nblocks, data_np.size // bs)
+    blocks = [data_np[i * bs:(i + 1) * bs].tobytes() for i in range(nblocks)]
+    threads = max(1, min(threads, nblocks))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        chunks = list(ex.map(impl.encode_block, blocks))
+    dt = time.perf_counter() - t0
+    same = all(
+        (c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) == g for c, g in zip(chunks, gpu_chunks[:nblocks])
+    )
+    return {
+        "value": round(nblocks * bs / dt / 1e9, 6),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"{nblocks} x {bs} B blocks of the benchmark input, one block per task on {threads} threads "
+                  f"({os.cpu_count()} host CPUs visible), {dt:.2f} s wall",
+        "bit_exact_vs_gpu": bool(same),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+    bra = importlib.import_module("br-archive_amd")
+
+    bs = args.block_size
+    total = args.bytes_per_gpu
+    nb = bra.BlockCodec.num_blocks(total, bs)
+    data_np = bra.synth_fill(KINDS[args.kind], total, bs, first_block=rank * nb)
+    d = torch.from_numpy(data_np).cuda()
+    codec = bra.BlockCodec(local)
+    hdr = torch.empty((nb, bra.HEADER_BYTES), dtype=torch.uint8, device=d.device)
+    off = torch.empty((nb + 1,), dtype=torch.int64, device=d.device)
+    pay = torch.empty((int(total * 1.25) + 64 * nb + 65536,), dtype=torch.uint8, device=d.device)
+
+    # RCCL gather of the compressed chunks to rank 0 (sizes first, then one send/recv per peer)
+    gather_bufs = {}
+
+    def gather_to_root():
+        sz = off[nb:nb + 1].clone()
+        sizes = [torch.empty_like(sz) for _ in range(world)]
+        dist.all_gather(sizes, sz)
+        sizes = [int(s.item()) for s in sizes]
+        ops = []
+        if rank == 0:
+            for r in range(1, world):
+                if r not in gather_bufs or gather_bufs[r][1].numel() < sizes[r]:
+                    gather_bufs[r] = (torch.empty_like(hdr), torch.empty((int(sizes[r] * 1.1) + 4096,), dtype=torch.uint8,
+                                                                            device=d.device))
+                ops.append(dist.P2POp(dist.irecv, gather_bufs[r][0], r))
+                ops.append(dist.P2POp(dist.irecv, gather_bufs[r][1][: sizes[r]], r))
+        else:
+            ops.append(dist.P2POp(dist.isend, hdr, 0))
+            ops.append(dist.P2POp(dist.isend, pay[: sizes[rank]], 0))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+    def step():
+        codec.encode(d, bs, hdr, off, pay)
+        if world > 1:
+            gather_to_root()
+
+    # ---- find the dominant kernel (one untimed, fully profiled pass) ----
+    kernel_slots = [s for s in codec.SLOTS if not s.startswith("stage.")]
+    codec.prof_enable(codec.slot_mask(*codec.SLOTS))
+    step()
+    torch.cuda.synchronize()
+    prof0 = codec.prof_read()
+    dominant = max(kernel_slots, key=lambda s: prof0[s][0])
+    stage_slots = [s for s in codec.SLOTS if s.startswith("stage.")]
+    timed_slots = codec.SLOTS if args.profile_all else (dominant, *stage_slots)
+    codec.prof_enable(codec.slot_mask(*timed_slots))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    codec.prof_reset()
+
+    # ---- timed region ----
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=d.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    prof = codec.prof_read()
+
+    value = world * total * args.steps / elapsed / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+    dms, dcnt, dbytes = prof[dominant]
+    avg_ms = dms / max(1, dcnt)
+    bytes_per_launch = dbytes / max(1, dcnt)
+    achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
+
+    # ---- outside the timed region: ratio, round trip, reference check ----
+    off_h = off.cpu().numpy()
+    payload_bytes = int(off_h[nb])
+    hdr_h = hdr.cpu().numpy()
+    rle_bytes = int(sum(int.from_bytes(hdr_h[b, 260:264].tobytes(), "little") for b in range(nb)))
+    pipeline_alg = 14 * total + 3 * rle_bytes + payload_bytes + 267 * nb  # SURVEY 8.1 row d
+    stage_ms = {s.split(".")[1]: round(prof[s][0] / max(1, prof[s][1]), 3) for s in stage_slots}
+    encode_dev_ms = sum(stage_ms.values())
+    check = None
+    if not args.no_check:
+        out = codec.decode(hdr, off, pay, total, bs)
+        torch.cuda.synchronize()
+        check = bool(torch.equal(out, d))
+        del out
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{nb} x {bs} B {args.kind} blocks per GPU (BASELINE configs[1]: 256 x 1 MiB enwik-style text), "
+                        "encode BWT+MTF+RLE+Huffman, inputs resident in HBM",
+            "block_size": bs,
+            "bytes_per_gpu": total,
+            "parallelism": f"dp{world}: blocks sharded per GPU" + (", RCCL gather of compressed chunks to rank 0" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dominant,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "avg_launch_ms": round(avg_ms, 4),
+            "launches": dcnt,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+        },
+        "pipeline": {
+            "stage_ms": stage_ms,
+            "encode_device_ms": round(encode_dev_ms, 3),
+            "algorithmic_bytes": pipeline_alg,
+            "hbm_frac": round(pipeline_alg / (ms_per_step / 1e3) / (HBM_PEAK_GBS * 1e9), 4),
+            "ratio": round((payload_bytes + 267 * nb) / total, 4),
+            "rle_bytes": rle_bytes,
+            "payload_bytes": payload_bytes,
+            "roundtrip_bit_exact": check,
+        },
+        "cpu_baseline": None,
+    }
+    if args.profile_all:
+        line["kernels"] = {k: {"ms": round(v[0] / max(1, v[1]), 4), "launches": v[1], "GBps": round(v[2] / max(v[0], 1e-9) / 1e6, 1)}
+                           for k, v in prof.items() if v[1]}
+    # traffic from a committed PMC profile of the same kernel, if one exists (profiles/pmc_summary.json)
+    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(pmc):
+        try:
+            pm = json.load(open(pmc))
+            k = pm.get("kernels", {}).get(dominant)
+            if k and k.get("workload") == line["config"]["workload"]:
+                line["roofline"]["traffic"] = k.get("hbm_bytes_per_launch")
+        except Exception:
+            pass
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        gpu_chunks = []
+        pay_h = pay[: payload_bytes].cpu().numpy()
+        for b in range(min(args.cpu_blocks, nb)):
+            pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
+            gpu_chunks.append((pi, lens, osz, esz, pay_h[off_h[b]:off_h[b] + esz].tobytes()))
+        line["cpu_baseline"] = cpu_baseline(data_np, bs, args.cpu_blocks, args.cpu_threads, gpu_chunks)
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    codec.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

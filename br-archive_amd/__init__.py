@@ -33,6 +33,7 @@ ABI_SYMBOLS = (
     "bra_huffman_encode", "bra_huffman_decode", "bra_huffman_chunk_free",
     "bra_gpu_ctx_create", "bra_gpu_ctx_destroy", "bra_gpu_num_blocks", "bra_gpu_payload_bound",
     "bra_gpu_encode_blocks", "bra_gpu_decode_blocks", "bra_gpu_stage_ptr", "bra_gpu_version",
+    "bra_gpu_prof_enable", "bra_gpu_prof_reset", "bra_gpu_prof_read",
 )
 
 SYNTH_TEXT, SYNTH_RANDOM, SYNTH_SYM16, SYNTH_TILED = 0, 1, 2, 3
@@ -109,6 +110,13 @@ def _load() -> C.CDLL:
     lib.bra_gpu_decode_blocks.restype = C.c_int
     lib.bra_gpu_stage_ptr.argtypes = [vp, C.c_int]
     lib.bra_gpu_stage_ptr.restype = vp
+    lib.bra_gpu_prof_enable.argtypes = [vp, C.c_uint64]
+    lib.bra_gpu_prof_enable.restype = None
+    lib.bra_gpu_prof_reset.argtypes = [vp]
+    lib.bra_gpu_prof_reset.restype = None
+    lib.bra_gpu_prof_read.argtypes = [vp, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_uint32),
+                                      C.POINTER(C.c_double)]
+    lib.bra_gpu_prof_read.restype = C.c_int
     lib.bra_gpu_version.argtypes = []
     lib.bra_gpu_version.restype = C.c_char_p
     return lib
@@ -281,6 +289,36 @@ class BlockCodec:
         if rc != 0:
             raise RuntimeError(f"bra_gpu_decode_blocks failed ({rc})")
         return out
+
+    def prof_enable(self, mask: int):
+        """Time the selected kernel slots with HIP events (bit i = slot i, see csrc/prof.h)."""
+        lib.bra_gpu_prof_enable(self.ctx, mask)
+
+    def prof_reset(self):
+        lib.bra_gpu_prof_reset(self.ctx)
+
+    def prof_read(self) -> dict:
+        """{slot name: (total device ms, launches, algorithmic bytes)} since the last reset."""
+        out = {}
+        n = lib.bra_gpu_prof_read(self.ctx, -1, None, None, None, None)
+        for i in range(n):
+            name, ms, cnt, by = C.c_char_p(), C.c_double(), C.c_uint32(), C.c_double()
+            lib.bra_gpu_prof_read(self.ctx, i, C.byref(name), C.byref(ms), C.byref(cnt), C.byref(by))
+            out[name.value.decode()] = (ms.value, cnt.value, by.value)
+        return out
+
+    SLOTS = ("stage.bwt", "stage.mtf", "stage.rle", "stage.huffman",
+             "bwt.l0_hist", "bwt.l0_scatter", "bwt.build_tiles", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.fallback",
+             "mtf.lastocc", "mtf.scan", "mtf.encode",
+             "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
+             "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack")
+
+    @classmethod
+    def slot_mask(cls, *names) -> int:
+        m = 0
+        for n in names:
+            m |= 1 << cls.SLOTS.index(n)
+        return m
 
     def stage_ptr(self, stage: int) -> int:
         return lib.bra_gpu_stage_ptr(self.ctx, stage) or 0

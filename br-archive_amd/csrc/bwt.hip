@@ -21,6 +21,7 @@
 //                pathological, highly repetitive blocks get here), using the same MSD/wave
 //                machinery on 32-bit rank keys.
 #include "bwt.h"
+#include "prof.h"
 
 #include <algorithm>
 #include <cstring>
@@ -71,7 +72,9 @@ struct Counters
     uint32_t overflow;    // a work list overflowed (fatal)
     uint32_t g_members;   // members of appended fallback groups
     uint32_t hmin;        // min depth of appended fallback groups
-    uint32_t pad;
+    uint32_t n_elems;     // elements in this level's big buckets (k_build_tiles)
+    uint32_t n_moved;     // elements the level's scatter moves (k_scan)
+    uint32_t pad[3];
 };
 
 // -------------------------------------------------------------------------------------------------
@@ -210,7 +213,11 @@ __global__ void __launch_bounds__(TPB) k_scan(ScanArgs a)
         const uint32_t nd     = B.d + 1;
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
         if (dg == 0)
+        {
             a.nomove[bi] = nomove ? 1 : 0;
+            if (!nomove)
+                atomicAdd(&a.ctr->n_moved, B.len);
+        }
         // big sub-buckets
         if (tot > JOB_MAX)
         {
@@ -435,14 +442,16 @@ __global__ void __launch_bounds__(TPB) k_build_tiles(Bucket* __restrict__ bucket
                                                      uint32_t cap_tiles, Counters* __restrict__ ctr)
 {
     __shared__ uint32_t tmp[8];
-    __shared__ uint32_t carry;
+    __shared__ uint32_t carry, elems;
     if (threadIdx.x == 0)
-        carry = 0;
+        carry = elems = 0;
     __syncthreads();
     for (uint32_t base = 0; base < nb; base += TPB)
     {
         const uint32_t i  = base + threadIdx.x;
         const uint32_t nt = (i < nb) ? div_up(buckets[i].len, TILE) : 0;
+        if (i < nb)
+            atomicAdd(&elems, buckets[i].len);
         uint32_t       total;
         const uint32_t ex = block256_exclusive_sum(nt, tmp, &total);
         const uint32_t t0 = carry + ex;
@@ -461,6 +470,7 @@ __global__ void __launch_bounds__(TPB) k_build_tiles(Bucket* __restrict__ bucket
     if (threadIdx.x == 0)
     {
         ctr->n_tiles = carry;
+        ctr->n_elems = elems;
         if (carry > cap_tiles)
             ctr->overflow = 1;
     }
@@ -912,20 +922,39 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
     const size_t lds = tile_stage_bytes();
     while (nbig > 0)
     {
-        hipLaunchKernelGGL(k_build_tiles, dim3(1), dim3(TPB), 0, s, w.big[cur], nbig, w.tile_bucket, w.cap_tiles, w.ctr);
-        // zero n_big for the next level (keep jobs/groups counters)
+        {
+            BRA_PROF(P_BWT_TILES, s);
+            hipLaunchKernelGGL(k_build_tiles, dim3(1), dim3(TPB), 0, s, w.big[cur], nbig, w.tile_bucket, w.cap_tiles, w.ctr);
+        }
+        // zero n_big / n_moved for the next level (keep jobs/groups counters)
         BRA_HIP_CHECK(hipMemsetAsync(&w.ctr->n_big, 0, 4, s));
+        BRA_HIP_CHECK(hipMemsetAsync(&w.ctr->n_moved, 0, 4, s));
         const int grid = w.grid;
-        hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket, w.ctr, w.key[0],
-                           w.key[1], w.pay[0], w.pay[1], w.tile_hist);
+        {
+            BRA_PROF(P_BWT_HIST, s);
+            hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket, w.ctr, w.key[0],
+                               w.key[1], w.pay[0], w.pay[1], w.tile_hist);
+        }
         ScanArgs a{w.big[cur], nbig,    w.tile_hist, w.tile_off, w.nomove,  w.big[cur ^ 1], w.cap_big, w.jobs, w.cap_jobs,
                    groups_out, w.cap_groups, w.ctr,  MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES};
-        hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(nbig, 65535u)), dim3(TPB), 0, s, a);
-        hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket, w.ctr, w.tile_off,
-                           w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
+        {
+            BRA_PROF(P_BWT_SCAN, s);
+            hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(nbig, 65535u)), dim3(TPB), 0, s, a);
+        }
+        {
+            BRA_PROF(P_BWT_SCATTER, s);
+            hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket, w.ctr, w.tile_off,
+                               w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
+        }
         BRA_HIP_CHECK(hipGetLastError());
         if (!read_ctr(w, s))
             return false;
+        // algorithmic bytes: keys read by the histogram, tile histograms, KV moved by the scatter
+        const double nt = w.h_ctr->n_tiles, ne = w.h_ctr->n_elems, nm = w.h_ctr->n_moved;
+        prof_bytes(P_BWT_TILES, 32.0 * nbig + 4.0 * nt);
+        prof_bytes(P_BWT_HIST, 8.0 * ne + 1024.0 * nt);
+        prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * nbig);
+        prof_bytes(P_BWT_SCATTER, 24.0 * nm + 1024.0 * nt);
         nbig = w.h_ctr->n_big;
         cur ^= 1;
     }
@@ -980,15 +1009,27 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return false;
     BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, nblocks, s));
     const int grid = w.grid;
-    hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist);
+    {
+        BRA_PROF(P_BWT_L0HIST, s);
+        hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist);
+    }
     ScanArgs a0{w.big[1], nblocks,  w.tile_hist, w.tile_off, w.nomove, w.big[0], w.cap_big, w.jobs, w.cap_jobs,
                 w.groups[0], w.cap_groups, w.ctr, DCAP_BIG};
-    hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(TPB), 0, s, a0);
-    hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), tile_stage_bytes() + TILE + 16, s, d_in, d_blocks,
-                       w.l0tiles, nt0, w.tile_off, w.key[0], w.pay[0]);
+    {
+        BRA_PROF(P_BWT_SCAN, s);
+        hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(TPB), 0, s, a0);
+    }
+    {
+        BRA_PROF(P_BWT_L0SCATTER, s);
+        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), tile_stage_bytes() + TILE + 16, s, d_in, d_blocks,
+                           w.l0tiles, nt0, w.tile_off, w.key[0], w.pay[0]);
+    }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
         return false;
+    prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
+    prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
+    prof_bytes(P_BWT_L0SCATTER, 13.0 * N + 1024.0 * nt0);
     // Level 0 never keeps data in place ("nomove" only matters for level >= 1): all sub-buckets are in buf 0.
     uint32_t njobs = 0;
     if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, 0, d_L, d_pi, w.groups[0], 0, s, njobs))
@@ -998,10 +1039,14 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     JobArgs ja{w.jobs,  njobs,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
                w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0};
     if (njobs)
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(std::min<uint32_t>(div_up(njobs, 4), 8192u)), dim3(256), 0, s, ja);
+        {
+            BRA_PROF(P_BWT_JOBS, s);
+            hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(std::min<uint32_t>(div_up(njobs, 4), 8192u)), dim3(256), 0, s, ja);
+        }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
         return false;
+    prof_bytes(P_BWT_JOBS, 17.0 * N);  // read key+payload, write SA entry + L byte
 
     // ---- fallback: prefix doubling on the groups still tied ----
     uint32_t ng = w.h_ctr->n_groups;
@@ -1040,15 +1085,27 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
             // big buckets: levels over 4 key bytes; subgroups of equal key > JOB_MAX become groups directly
             while (nb > 0)
             {
-                hipLaunchKernelGGL(k_build_tiles, dim3(1), dim3(TPB), 0, s, w.big[cur], nb, w.tile_bucket, w.cap_tiles, w.ctr);
+                {
+                    BRA_PROF(P_BWT_TILES, s);
+                    hipLaunchKernelGGL(k_build_tiles, dim3(1), dim3(TPB), 0, s, w.big[cur], nb, w.tile_bucket, w.cap_tiles, w.ctr);
+                }
                 BRA_HIP_CHECK(hipMemsetAsync(&w.ctr->n_big, 0, 4, s));
-                hipLaunchKernelGGL(k_hist<MODE_RANK>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket, w.ctr,
-                                   w.key[0], w.key[1], w.pay[0], w.pay[1], w.tile_hist);
+                {
+                    BRA_PROF(P_BWT_HIST, s);
+                    hipLaunchKernelGGL(k_hist<MODE_RANK>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket, w.ctr,
+                                       w.key[0], w.key[1], w.pay[0], w.pay[1], w.tile_hist);
+                }
                 ScanArgs a{w.big[cur], nb,    w.tile_hist, w.tile_off, w.nomove, w.big[cur ^ 1], w.cap_big, w.jobs, w.cap_jobs,
                            gnext,      w.cap_groups, w.ctr, RANK_KEYBYTES};
-                hipLaunchKernelGGL(k_scan<MODE_RANK>, dim3(std::min<uint32_t>(nb, 65535u)), dim3(TPB), 0, s, a);
-                hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), tile_stage_bytes(), s, w.big[cur], w.nomove, w.tile_bucket, w.ctr,
-                                   w.tile_off, w.key[0], w.key[1], w.pay[0], w.pay[1], (uint32_t) MODE_RANK);
+                {
+                    BRA_PROF(P_BWT_SCAN, s);
+                    hipLaunchKernelGGL(k_scan<MODE_RANK>, dim3(std::min<uint32_t>(nb, 65535u)), dim3(TPB), 0, s, a);
+                }
+                {
+                    BRA_PROF(P_BWT_SCATTER, s);
+                    hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), tile_stage_bytes(), s, w.big[cur], w.nomove, w.tile_bucket, w.ctr,
+                                       w.tile_off, w.key[0], w.key[1], w.pay[0], w.pay[1], (uint32_t) MODE_RANK);
+                }
                 if (!read_ctr(w, s))
                     return false;
                 nb = w.h_ctr->n_big;
@@ -1064,7 +1121,10 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
             hipLaunchKernelGGL(k_rank_flush, dim3(std::min<uint32_t>(ng_big, 4096u)), dim3(256), 0, s, gnext, ng_big, d_blocks, w.pay[0],
                                w.pay[1], w.fsa, d_L, w.isa, d_pi);
         if (nj)
-            hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr);
+            {
+                BRA_PROF(P_BWT_JOBS, s);
+                hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr);
+            }
         BRA_HIP_CHECK(hipGetLastError());
         if (!read_ctr(w, s))
             return false;

@@ -7,6 +7,7 @@
 #include "ibwt.h"
 #include "mtf.h"
 #include "rle.h"
+#include "prof.h"
 
 #include <cstdarg>
 #include <cstring>
@@ -33,6 +34,73 @@ static_assert(sizeof(bra_huffman_t) == 264, "bra_huffman_t layout");
 static_assert(offsetof(bra_huffman_chunk_t, data) == 264, "bra_huffman_chunk_t layout");
 
 using namespace bra;
+
+// ---- event profiler (prof.h) ----
+namespace bra {
+Prof* g_prof = nullptr;
+
+const char* prof_name(int slot)
+{
+    static const char* names[P_NSLOT] = {
+        "stage.bwt", "stage.mtf", "stage.rle", "stage.huffman",
+        "bwt.l0_hist", "bwt.l0_scatter", "bwt.build_tiles", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.fallback",
+        "mtf.lastocc", "mtf.scan", "mtf.encode",
+        "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
+        "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack"};
+    return (slot >= 0 && slot < P_NSLOT) ? names[slot] : "";
+}
+
+hipEvent_t Prof::get()
+{
+    if (!pool.empty())
+    {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void) hipEventCreate(&e);
+    return e;
+}
+
+void Prof::collect()
+{
+    for (int i = 0; i < P_NSLOT; ++i)
+    {
+        for (auto& pr : pending[i])
+        {
+            float ms_ = 0.f;
+            (void) hipEventSynchronize(pr.second);
+            if (hipEventElapsedTime(&ms_, pr.first, pr.second) == hipSuccess)
+            {
+                ms[i] += ms_;
+                launches[i] += 1;
+            }
+            pool.push_back(pr.first);
+            pool.push_back(pr.second);
+        }
+        pending[i].clear();
+    }
+}
+
+void Prof::reset()
+{
+    collect();
+    for (int i = 0; i < P_NSLOT; ++i)
+    {
+        ms[i]       = 0;
+        launches[i] = 0;
+        bytes[i]    = 0;
+    }
+}
+
+Prof::~Prof()
+{
+    collect();
+    for (hipEvent_t e : pool)
+        (void) hipEventDestroy(e);
+}
+}  // namespace bra
 
 namespace {
 
@@ -114,6 +182,7 @@ struct bra_gpu_ctx_s
     bra_io_chunk_header_t* d_hdr = nullptr;
     uint64_t       cap_hdr = 0;
     uint32_t       last_nblocks = 0;
+    Prof           prof;
 };
 
 static bool ctx_init(bra_gpu_ctx_s* c, int device)
@@ -180,15 +249,29 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     if (hipMemcpyAsync(c->d_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(c->d_rle_base, rle_base.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
         return -1;
-    if (!bwt_encode_device(c->bwt, d_in, c->d_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
-        return -1;
-    if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s))
-        return -1;
-    if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
-        return -1;
+    {
+        BRA_PROF(P_STAGE_BWT, s);
+        if (!bwt_encode_device(c->bwt, d_in, c->d_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
+            return -1;
+    }
+    {
+        BRA_PROF(P_STAGE_MTF, s);
+        if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s))
+            return -1;
+    }
+    {
+        BRA_PROF(P_STAGE_RLE, s);
+        if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
+            return -1;
+    }
     uint64_t total = 0;
-    if (!huff_encode_device(c->huf, c->d_rle, rle_blocks.data(), nb, c->d_hist, c->d_rle_size, c->d_meta, d_payload_off, d_payload, payload_cap,
-                            &total, s))
+    bool     hok   = false;
+    {
+        BRA_PROF(P_STAGE_HUF, s);
+        hok = huff_encode_device(c->huf, c->d_rle, rle_blocks.data(), nb, c->d_hist, c->d_rle_size, c->d_meta, d_payload_off, d_payload,
+                                 payload_cap, &total, s);
+    }
+    if (!hok)
     {
         if (needed)
             *needed = total;
@@ -197,6 +280,24 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     hipLaunchKernelGGL(k_headers, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, c->d_pi, c->d_meta, nb, d_headers);
     if (hipGetLastError() != hipSuccess)
         return -1;
+    if (g_prof && g_prof->mask)
+    {
+        // sizes of the RLE outputs for the byte accounting of rle.write / huf.* (profiling only)
+        std::vector<uint32_t> rs(nb);
+        if (hipMemcpyAsync(rs.data(), c->d_rle_size, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return -1;
+        double Rt = 0;
+        for (uint32_t v : rs)
+            Rt += v;
+        const double ntiles = (double) c->huf.tiling.n;
+        prof_bytes(P_RLE_WRITE, (double) N + Rt + 48.0 * c->rle.tiling.n);
+        prof_bytes(P_HUF_BUILD, 1024.0 * nb + 264.0 * nb);
+        prof_bytes(P_HUF_TILEBITS, Rt + 4.0 * ntiles);
+        prof_bytes(P_HUF_TILESCAN, 12.0 * ntiles);
+        prof_bytes(P_HUF_ZERO, 20.0 * ntiles);
+        prof_bytes(P_HUF_PACK, Rt + (double) total + 12.0 * ntiles);
+        prof_bytes(P_HUF_OFFSETS, 16.0 * nb);
+    }
     c->last_nblocks = nb;
     if (needed)
         *needed = total;
@@ -325,7 +426,10 @@ int bra_gpu_encode_blocks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t total,
     if (hipSetDevice(c->device) != hipSuccess)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
-    return encode_impl(c, d_in, geometry(total, block_size), d_headers, d_payload_off, d_payload, payload_cap, s, nullptr);
+    g_prof       = c->prof.mask ? &c->prof : nullptr;
+    const int rc = encode_impl(c, d_in, geometry(total, block_size), d_headers, d_payload_off, d_payload, payload_cap, s, nullptr);
+    g_prof       = nullptr;
+    return rc;
 }
 
 int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
@@ -355,6 +459,37 @@ const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)
 }
 
 const char* bra_gpu_version(void) { return "bra_hip 0.1.0 (gfx950)"; }
+
+void bra_gpu_prof_enable(bra_gpu_ctx_t* c, uint64_t mask)
+{
+    if (c)
+        c->prof.mask = mask;
+}
+
+void bra_gpu_prof_reset(bra_gpu_ctx_t* c)
+{
+    if (c)
+        c->prof.reset();
+}
+
+int bra_gpu_prof_read(bra_gpu_ctx_t* c, int slot, const char** name, double* total_ms, uint32_t* launches, double* bytes)
+{
+    if (!c)
+        return 0;
+    c->prof.collect();
+    if (slot >= 0 && slot < P_NSLOT)
+    {
+        if (name)
+            *name = prof_name(slot);
+        if (total_ms)
+            *total_ms = c->prof.ms[slot];
+        if (launches)
+            *launches = c->prof.launches[slot];
+        if (bytes)
+            *bytes = c->prof.bytes[slot];
+    }
+    return P_NSLOT;
+}
 
 }  // extern "C"
 

@@ -18,6 +18,7 @@
 // a leaf that gains children stops being a leaf) is rebuilt on the device, turned into an 11-bit
 // primary lookup table, and walked (:455-482) with the reference's stop rule and error cases.
 #include "huffman.h"
+#include "prof.h"
 
 namespace bra {
 
@@ -728,12 +729,24 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
     const uint32_t nt = w.tiling.n;
     if (!w.reserve(nblocks, nt))
         return false;
-    hipLaunchKernelGGL(k_huff_build, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_hist, d_rle_size, nblocks, d_meta, w.codes);
-    hipLaunchKernelGGL(k_huff_offsets, dim3(1), dim3(TPB), 0, s, d_meta, nblocks, d_payload_off);
+    {
+        BRA_PROF(P_HUF_BUILD, s);
+        hipLaunchKernelGGL(k_huff_build, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_hist, d_rle_size, nblocks, d_meta, w.codes);
+    }
+    {
+        BRA_PROF(P_HUF_OFFSETS, s);
+        hipLaunchKernelGGL(k_huff_offsets, dim3(1), dim3(TPB), 0, s, d_meta, nblocks, d_payload_off);
+    }
     const uint32_t grid = std::min<uint32_t>(nt, 8192);
-    hipLaunchKernelGGL(k_huff_tilebits, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.tbits);
-    hipLaunchKernelGGL(k_huff_tilescan, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
-                       d_payload_off, w.tbits, w.tbit0);
+    {
+        BRA_PROF(P_HUF_TILEBITS, s);
+        hipLaunchKernelGGL(k_huff_tilebits, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.tbits);
+    }
+    {
+        BRA_PROF(P_HUF_TILESCAN, s);
+        hipLaunchKernelGGL(k_huff_tilescan, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
+                           d_payload_off, w.tbits, w.tbit0);
+    }
     BRA_HIP_CHECK(hipMemcpyAsync(h_total, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s));
     BRA_HIP_CHECK(hipStreamSynchronize(s));
     if (*h_total + 8 > payload_cap)
@@ -743,8 +756,14 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
         return false;
     }
     uint32_t* words = reinterpret_cast<uint32_t*>(d_payload);
-    hipLaunchKernelGGL(k_huff_zero, dim3(std::min<uint32_t>(div_up(nt, 256), 4096)), dim3(256), 0, s, w.tbits, w.tbit0, nt, words);
-    hipLaunchKernelGGL(k_huff_pack, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.codes, w.tbits, w.tbit0, words);
+    {
+        BRA_PROF(P_HUF_ZERO, s);
+        hipLaunchKernelGGL(k_huff_zero, dim3(std::min<uint32_t>(div_up(nt, 256), 4096)), dim3(256), 0, s, w.tbits, w.tbit0, nt, words);
+    }
+    {
+        BRA_PROF(P_HUF_PACK, s);
+        hipLaunchKernelGGL(k_huff_pack, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.codes, w.tbits, w.tbit0, words);
+    }
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }

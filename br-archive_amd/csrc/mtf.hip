@@ -14,6 +14,7 @@
 // holds, so decoding a segment from the identity table gives labels u_i and an end permutation
 // P_k; the true start tables satisfy S_{k+1}[j] = S_k[P_k[j]] and the output is S_k[u_i].
 #include "mtf.h"
+#include "prof.h"
 
 namespace bra {
 
@@ -265,9 +266,15 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     if (!w.reserve((size_t) nseg * 256 * 4))
         return false;
     int32_t* st = reinterpret_cast<int32_t*>(w.state);
-    hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(nseg, 8192)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
-    hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
-                       nblocks, st);
+    {
+        BRA_PROF(P_MTF_LASTOCC, s);
+        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(nseg, 8192)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
+    }
+    {
+        BRA_PROF(P_MTF_SCAN, s);
+        hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
+                           nblocks, st);
+    }
     const size_t lds = 64 * TPB * 4;
     static bool  attr = false;
     if (!attr)
@@ -276,8 +283,17 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         attr = true;
     }
-    hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
-                       w.tiling.d_pieces, nseg, st);
+    {
+        BRA_PROF(P_MTF_ENCODE, s);
+        hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
+                           w.tiling.d_pieces, nseg, st);
+    }
+    uint64_t N = 0;
+    for (uint32_t b = 0; b < nblocks; ++b)
+        N += h_blocks[b].len;
+    prof_bytes(P_MTF_LASTOCC, (double) N + 1024.0 * nseg);
+    prof_bytes(P_MTF_SCAN, 2048.0 * nseg);
+    prof_bytes(P_MTF_ENCODE, 2.0 * N + 1024.0 * nseg);
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }

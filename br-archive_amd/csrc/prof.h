@@ -29,6 +29,7 @@ struct Prof
     std::vector<hipEvent_t>                             pool;
     double                                              ms[P_NSLOT] = {};
     uint32_t                                            launches[P_NSLOT] = {};
+    double                                              bytes[P_NSLOT] = {};  // algorithmic bytes of the timed launches
     hipEvent_t                                          get();
     void                                                collect();  // waits for the recorded events
     void                                                reset();
@@ -36,6 +37,13 @@ struct Prof
 };
 
 extern Prof* g_prof;  // set by the C-ABI for the duration of a call
+
+// Attribute algorithmic bytes ("algorithmic bytes") to a slot's timed launches.
+inline void prof_bytes(int slot, double b)
+{
+    if (g_prof && (g_prof->mask >> slot & 1))
+        g_prof->bytes[slot] += b;
+}
 
 struct ProfScope
 {

@@ -17,6 +17,7 @@
 //   k_rle_write   classify again, stage the tile's output in LDS, coalesced store, + byte histogram
 //                 of the output (the Huffman frequencies, bra_huffman.c:368-370)
 #include "rle.h"
+#include "prof.h"
 
 namespace bra {
 
@@ -498,12 +499,38 @@ bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_
     TileLink* link = static_cast<TileLink*>(w.link);
     TileGap*  gaps = static_cast<TileGap*>(w.gaps);
     TileOff*  offs = static_cast<TileOff*>(w.offs);
-    hipLaunchKernelGGL(k_rle_runs, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, runs);
-    hipLaunchKernelGGL(k_rle_link, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, runs, link);
-    hipLaunchKernelGGL(k_rle_sizes, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, link, gaps);
-    hipLaunchKernelGGL(k_rle_offsets, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
-                       w.tiling.d_pieces, gaps, offs, d_rle_size);
-    hipLaunchKernelGGL(k_rle_write, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, link, offs, d_rle_base, d_out, d_hist);
+    {
+        BRA_PROF(P_RLE_RUNS, s);
+        hipLaunchKernelGGL(k_rle_runs, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, runs);
+    }
+    {
+        BRA_PROF(P_RLE_LINK, s);
+        hipLaunchKernelGGL(k_rle_link, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, runs, link);
+    }
+    {
+        BRA_PROF(P_RLE_SIZES, s);
+        hipLaunchKernelGGL(k_rle_sizes, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, link, gaps);
+    }
+    {
+        BRA_PROF(P_RLE_OFFSETS, s);
+        hipLaunchKernelGGL(k_rle_offsets, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
+                           w.tiling.d_pieces, gaps, offs, d_rle_size);
+    }
+    {
+        BRA_PROF(P_RLE_WRITE, s);
+        hipLaunchKernelGGL(k_rle_write, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, link, offs, d_rle_base, d_out, d_hist);
+    }
+    if (g_prof && g_prof->mask)
+    {
+        // rle.write (n + r bytes) is charged by the caller once the output sizes are on the host
+        uint64_t N = 0;
+        for (uint32_t b = 0; b < nblocks; ++b)
+            N += h_blocks[b].len;
+        prof_bytes(P_RLE_RUNS, (double) N + 16.0 * nt);
+        prof_bytes(P_RLE_SIZES, (double) N + 24.0 * nt);
+        prof_bytes(P_RLE_LINK, 24.0 * nt);
+        prof_bytes(P_RLE_OFFSETS, 48.0 * nt);
+    }
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }

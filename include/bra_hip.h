@@ -89,7 +89,9 @@ void           bra_gpu_ctx_destroy(bra_gpu_ctx_t* ctx);
 /* Number of blocks `total` bytes split into blocks of `block_size` bytes (last block ragged). */
 uint32_t bra_gpu_num_blocks(uint64_t total, uint32_t block_size);
 
-/* Payload capacity that always suffices for bra_gpu_encode_blocks of this geometry. */
+/* Payload capacity for bra_gpu_encode_blocks of this geometry when no code is longer than 32 bits
+ * (always true below ~3.5 M symbols per block); a call that needs more fails with -2 and leaves the
+ * required size in d_payload_off[nblocks]. */
 uint64_t bra_gpu_payload_bound(uint64_t total, uint32_t block_size);
 
 /*
@@ -119,6 +121,17 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* ctx, const bra_io_chunk_header_t* d_hea
  * at byte offset rle_base[b]), 3 = rle_base (uint64_t[nblocks]), 4 = RLE sizes (uint32_t[nblocks]).
  */
 const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* ctx, int stage);
+
+/*
+ * Kernel timing with HIP events on the launching stream (used by bench.py): `mask` selects the
+ * timing slots (bit i = slot i; 0 = off).  bra_gpu_prof_read waits for the recorded events and
+ * returns the number of slots; for a valid `slot` it reports the slot's name, the summed device
+ * time in ms, the number of launches timed since the last reset and their algorithmic HBM bytes
+ * (the bytes the algorithm must move, DESIGN.md "Roofline"), so bytes / time is achieved GB/s.
+ */
+void bra_gpu_prof_enable(bra_gpu_ctx_t* ctx, uint64_t mask);
+void bra_gpu_prof_reset(bra_gpu_ctx_t* ctx);
+int  bra_gpu_prof_read(bra_gpu_ctx_t* ctx, int slot, const char** name, double* total_ms, uint32_t* launches, double* bytes);
 
 /* Library identification for the loader tests. */
 const char* bra_gpu_version(void);
