@@ -308,7 +308,7 @@ class BlockCodec:
         return out
 
     SLOTS = ("stage.bwt", "stage.mtf", "stage.rle", "stage.huffman",
-             "bwt.l0_hist", "bwt.l0_scatter", "bwt.build_tiles", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.fallback",
+             "bwt.l0_hist", "bwt.l0_scatter", "bwt.build_tiles", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.mjobs", "bwt.fallback",
              "mtf.lastocc", "mtf.scan", "mtf.encode",
              "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
              "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack")
@@ -322,6 +322,19 @@ class BlockCodec:
 
     def stage_ptr(self, stage: int) -> int:
         return lib.bra_gpu_stage_ptr(self.ctx, stage) or 0
+
+    def stage_copy(self, stage: int, nbytes: int):
+        """Host copy (numpy uint8) of the first `nbytes` of an intermediate stage of the last encode."""
+        import numpy as np
+        import torch
+
+        torch.cuda.synchronize()
+        out = np.empty(nbytes, np.uint8)
+        hip = C.CDLL("libamdhip64.so")
+        rc = hip.hipMemcpy(C.c_void_p(out.ctypes.data), C.c_void_p(self.stage_ptr(stage)), C.c_size_t(nbytes), 2)  # D2H
+        if rc != 0:
+            raise RuntimeError(f"hipMemcpy failed ({rc})")
+        return out
 
 
 def parse_header(h: bytes):

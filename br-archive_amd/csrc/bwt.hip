@@ -35,6 +35,7 @@ constexpr int      TILE         = 4096;  // elements per tile (256 threads x 16)
 constexpr int      TPB          = 256;
 constexpr int      PER_THREAD   = TILE / TPB;
 constexpr uint32_t JOB_MAX      = 256;  // elements one wave sorts in registers
+constexpr int      MJ_WAVES_DEF = 8;    // waves of a workgroup job (4, 8 or 16; env BRA_MJ_WAVES)
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
@@ -55,7 +56,7 @@ struct Bucket
 
 struct Job
 {
-    uint32_t start, len, kd, buf, block, gdepth;
+    uint32_t start, len, kd, buf, block, gdepth, d;  // d: depth (bytes shared) of the job's sub-buckets
 };
 
 struct Group
@@ -65,17 +66,32 @@ struct Group
 
 struct Counters
 {
-    uint32_t n_big;       // buckets appended to the next level
-    uint32_t n_jobs;
-    uint32_t n_groups;    // fallback groups appended (next round)
-    uint32_t n_tiles;     // tiles of the current level
-    uint32_t overflow;    // a work list overflowed (fatal)
-    uint32_t g_members;   // members of appended fallback groups
-    uint32_t hmin;        // min depth of appended fallback groups
-    uint32_t n_elems;     // elements in this level's big buckets (k_build_tiles)
-    uint32_t n_moved;     // elements the level's scatter moves (k_scan)
-    uint32_t pad[3];
+    uint32_t n_big;         // buckets appended to the next level      } one 64-bit atomic
+    uint32_t n_tiles_next;  // tiles reserved for the next level        }
+    uint32_t n_jobs;        // wave jobs (<= JOB_MAX elements)
+    uint32_t n_mjobs;       // workgroup jobs (<= mjob_max elements)
+    uint32_t n_groups;      // fallback groups appended (next round)
+    uint32_t n_tiles;       // tiles of the current level
+    uint32_t overflow;      // a work list overflowed (fatal)
+    uint32_t g_members;     // members of appended fallback groups
+    uint32_t hmin;          // min depth of appended fallback groups
+    uint32_t n_elems;       // elements in this level's big buckets (byte accounting)
+    uint32_t n_moved;       // elements the level's scatter moves (byte accounting)
+    uint32_t n_elems_next;
+    uint32_t n_melems;      // elements in workgroup jobs (byte accounting)
+    uint32_t pad;
 };
+
+// Start of an MSD level: the tiles reserved by the previous level become current.
+__global__ void k_level_start(Counters* ctr)
+{
+    ctr->n_tiles      = ctr->n_tiles_next;
+    ctr->n_elems      = ctr->n_elems_next;
+    ctr->n_tiles_next = 0;
+    ctr->n_elems_next = 0;
+    ctr->n_big        = 0;
+    ctr->n_moved      = 0;
+}
 
 // -------------------------------------------------------------------------------------------------
 // level 0: byte histograms of input tiles
@@ -174,40 +190,103 @@ struct ScanArgs
     uint8_t*        nomove;
     Bucket*         next;
     uint32_t        cap_next;
+    uint32_t*       tile_bucket_next;  // tile -> bucket map of the next level
+    uint32_t        cap_tiles;
     Job*            jobs;
     uint32_t        cap_jobs;
+    Job*            mjobs;
+    uint32_t        cap_mjobs;
     Group*          groups;
     uint32_t        cap_groups;
     Counters*       ctr;
-    uint32_t        dcap;  // STRING: depth cap for big buckets
+    uint32_t        dcap;      // STRING: depth cap for big buckets
+    uint32_t        account;   // keep the byte-accounting counters (profiling)
+    uint32_t        mjob_max;  // largest workgroup job (256 * waves; JOB_MAX = no workgroup jobs)
 };
 
+constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into one wave job
+
+__device__ __forceinline__ uint32_t block256_exclusive_max(uint32_t v, uint32_t* tmp)
+{
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t  x    = v;
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        const uint32_t o = __shfl_up(x, d, WAVE);
+        if (lane >= d)
+            x = max(x, o);
+    }
+    if (lane == WAVE - 1)
+        tmp[w] = x;
+    uint32_t ex = __shfl_up(x, 1, WAVE);
+    if (lane == 0)
+        ex = 0;
+    __syncthreads();
+    for (int i = 0; i < w; ++i)
+        ex = max(ex, tmp[i]);
+    __syncthreads();
+    return ex;
+}
+
+// One workgroup per bucket, thread = digit.  Sub-bucket offsets per tile; the sub-buckets become
+// wave jobs (<= JOB_MAX; consecutive ones of <= SMALL_MAX share a job: digits of one run between
+// larger sub-buckets are grouped by floor(prefix / SMALL_MAX), so every job holds < JOB_MAX
+// elements), workgroup jobs (<= mjob_max), next-level buckets (their tiles reserved here, one
+// 64-bit atomic for bucket and tile slots), or fallback groups.
 template <uint32_t MODE>
 __global__ void __launch_bounds__(TPB) k_scan(ScanArgs a)
 {
-    __shared__ uint32_t tot_s[256];
-    __shared__ uint32_t base_s[256];
     __shared__ uint32_t tmp[8];
+    __shared__ uint32_t key_s[256];
+    __shared__ uint32_t jlen_s[256];
+    __shared__ uint32_t jbase_s, mbase_s, bbase_s, tbase_s, gbase_s;
     const uint32_t      dg = threadIdx.x;
     for (uint32_t bi = blockIdx.x; bi < a.nbuckets; bi += gridDim.x)
     {
         const Bucket   B      = a.buckets[bi];
         const uint32_t ntiles = div_up(B.len, TILE);
+        const uint32_t* th    = a.tile_hist + (size_t) B.tile0 * 256 + dg;
         uint32_t       tot    = 0;
-        for (uint32_t t = 0; t < ntiles; ++t)
-            tot += a.tile_hist[(size_t) (B.tile0 + t) * 256 + dg];
-        const uint32_t base = block256_exclusive_sum(tot, tmp);
-        tot_s[dg]           = tot;
-        base_s[dg]          = base;
-        uint32_t run        = B.start + base;
-        for (uint32_t t = 0; t < ntiles; ++t)
         {
-            const size_t o = (size_t) (B.tile0 + t) * 256 + dg;
-            const uint32_t h = a.tile_hist[o];
-            a.tile_off[o]    = run;
-            run += h;
+            uint32_t t = 0;
+            for (; t + 8 <= ntiles; t += 8)
+            {
+                uint32_t h[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    h[u] = th[(size_t) (t + u) * 256];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    tot += h[u];
+            }
+            for (; t < ntiles; ++t)
+                tot += th[(size_t) t * 256];
         }
-        __syncthreads();
+        const uint32_t base = block256_exclusive_sum(tot, tmp);
+        {
+            uint32_t* to  = a.tile_off + (size_t) B.tile0 * 256 + dg;
+            uint32_t  run = B.start + base;
+            uint32_t  t   = 0;
+            for (; t + 8 <= ntiles; t += 8)
+            {
+                uint32_t h[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    h[u] = th[(size_t) (t + u) * 256];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                {
+                    to[(size_t) (t + u) * 256] = run;
+                    run += h[u];
+                }
+            }
+            for (; t < ntiles; ++t)
+            {
+                const uint32_t h          = th[(size_t) t * 256];
+                to[(size_t) t * 256]      = run;
+                run += h;
+            }
+        }
         const bool     nomove = __syncthreads_or(tot == B.len);
         const uint32_t kd     = eff_kd(B, MODE);
         const uint32_t nd     = B.d + 1;
@@ -215,72 +294,97 @@ __global__ void __launch_bounds__(TPB) k_scan(ScanArgs a)
         if (dg == 0)
         {
             a.nomove[bi] = nomove ? 1 : 0;
-            if (!nomove)
+            if (!nomove && a.account)
                 atomicAdd(&a.ctr->n_moved, B.len);
         }
-        // big sub-buckets
-        if (tot > JOB_MAX)
-        {
-            const uint32_t s = B.start + base;
-            bool final_grp   = false;
-            if (MODE == MODE_STRING)
-                final_grp = nd >= a.dcap;
-            else
-                final_grp = nd >= RANK_KEYBYTES;
-            if (final_grp)
-            {
-                const uint32_t gdep = (MODE == MODE_STRING) ? nd : B.gdepth;
-                const uint32_t slot = atomicAdd(&a.ctr->n_groups, 1u);
-                if (slot < a.cap_groups)
-                {
-                    a.groups[slot] = Group{s, tot, gdep, B.block | (obuf << 31)};
-                    atomicAdd(&a.ctr->g_members, tot);
-                    atomicMin(&a.ctr->hmin, gdep);
-                }
-                else
-                    atomicExch(&a.ctr->overflow, 1u);
-            }
-            else
-            {
-                const uint32_t slot = atomicAdd(&a.ctr->n_big, 1u);
-                if (slot < a.cap_next)
-                    a.next[slot] = Bucket{s, tot, nd, kd, B.block, obuf, B.gdepth, 0};
-                else
-                    atomicExch(&a.ctr->overflow, 1u);
-            }
-        }
-        // pack consecutive small sub-buckets into wave jobs (greedy, in slot order)
+        const bool big   = tot > a.mjob_max;
+        const bool med   = tot > JOB_MAX && !big;
+        const bool mid   = tot > SMALL_MAX && tot <= JOB_MAX;
+        const bool small = tot > 0 && tot <= SMALL_MAX;
+        const bool brk   = big || med || mid;
+        // ---- wave jobs ----
+        const uint32_t S     = block256_exclusive_sum(small ? tot : 0, tmp);
+        const uint32_t R0    = block256_exclusive_max(brk ? S : 0, tmp);
+        const uint32_t runid = block256_exclusive_sum(brk ? 1u : 0u, tmp);
+        const uint32_t key   = (runid << 20) | ((S - R0) / SMALL_MAX);
+        const uint32_t prevs = block256_exclusive_max(small ? dg + 1 : 0, tmp);
+        key_s[dg]            = key;
+        jlen_s[dg]           = 0;
+        __syncthreads();
+        const bool     jstart = mid || (small && (prevs == 0 || key_s[prevs - 1] != key));
+        uint32_t       jtot;
+        const uint32_t jex  = block256_exclusive_sum(jstart ? 1u : 0u, tmp, &jtot);
+        const uint32_t jidx = jex + (jstart ? 1u : 0u) - 1u;
+        if (small || mid)
+            atomicAdd(&jlen_s[jidx], tot);
+        // ---- workgroup jobs, next-level buckets, fallback groups ----
+        const bool final_grp = big && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
+        const bool nb_next   = big && !final_grp;
+        uint32_t   btot, ttot, gtot, mtot;
+        const uint32_t ntl = nb_next ? div_up(tot, TILE) : 0;
+        const uint32_t bex = block256_exclusive_sum(nb_next ? 1u : 0u, tmp, &btot);
+        const uint32_t tex = block256_exclusive_sum(ntl, tmp, &ttot);
+        const uint32_t mex = block256_exclusive_sum(med ? 1u : 0u, tmp, &mtot);
+        const uint32_t gex = block256_exclusive_sum(final_grp ? 1u : 0u, tmp, &gtot);
         if (dg == 0)
         {
-            uint32_t js = 0, jl = 0;
-            auto     flush = [&]() {
-                if (jl)
-                {
-                    const uint32_t slot = atomicAdd(&a.ctr->n_jobs, 1u);
-                    if (slot < a.cap_jobs)
-                        a.jobs[slot] = Job{js, jl, kd, obuf, B.block, B.gdepth};
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
-                jl = 0;
-            };
-            for (int x = 0; x < 256; ++x)
+            jbase_s = jtot ? atomicAdd(&a.ctr->n_jobs, jtot) : 0;
+            mbase_s = mtot ? atomicAdd(&a.ctr->n_mjobs, mtot) : 0;
+            if (btot)
             {
-                const uint32_t c = tot_s[x];
-                if (c == 0)
-                    continue;
-                if (c > JOB_MAX)
-                {
-                    flush();
-                    continue;
-                }
-                if (jl + c > JOB_MAX)
-                    flush();
-                if (jl == 0)
-                    js = B.start + base_s[x];
-                jl += c;
+                const unsigned long long old =
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_big), ((unsigned long long) ttot << 32) | btot);
+                bbase_s = (uint32_t) old;
+                tbase_s = (uint32_t) (old >> 32);
             }
-            flush();
+            gbase_s = gtot ? atomicAdd(&a.ctr->n_groups, gtot) : 0;
+        }
+        __syncthreads();
+        const uint32_t s0 = B.start + base;
+        if (jstart)
+        {
+            const uint32_t slot = jbase_s + jidx;
+            if (slot < a.cap_jobs)
+                a.jobs[slot] = Job{s0, jlen_s[jidx], kd, obuf, B.block, B.gdepth, nd};
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+        }
+        if (med)
+        {
+            const uint32_t slot = mbase_s + mex;
+            if (slot < a.cap_mjobs)
+                a.mjobs[slot] = Job{s0, tot, kd, obuf, B.block, B.gdepth, nd};
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+            if (a.account)
+                atomicAdd(&a.ctr->n_melems, tot);
+        }
+        if (nb_next)
+        {
+            const uint32_t slot = bbase_s + bex, t0 = tbase_s + tex;
+            if (slot < a.cap_next && t0 + ntl <= a.cap_tiles)
+            {
+                a.next[slot] = Bucket{s0, tot, nd, kd, B.block, obuf, B.gdepth, t0};
+                for (uint32_t t = 0; t < ntl; ++t)
+                    a.tile_bucket_next[t0 + t] = slot;
+                if (a.account)
+                    atomicAdd(&a.ctr->n_elems_next, tot);
+            }
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+        }
+        if (final_grp)
+        {
+            const uint32_t gdep = (MODE == MODE_STRING) ? nd : B.gdepth;
+            const uint32_t slot = gbase_s + gex;
+            if (slot < a.cap_groups)
+            {
+                a.groups[slot] = Group{s0, tot, gdep, B.block | (obuf << 31)};
+                atomicAdd(&a.ctr->g_members, tot);
+                atomicMin(&a.ctr->hmin, gdep);
+            }
+            else
+                atomicExch(&a.ctr->overflow, 1u);
         }
         __syncthreads();
     }
@@ -436,48 +540,16 @@ __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buck
 }
 
 // -------------------------------------------------------------------------------------------------
-// tiles of the current level's big buckets
-// -------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(TPB) k_build_tiles(Bucket* __restrict__ buckets, uint32_t nb, uint32_t* __restrict__ tile_bucket,
-                                                     uint32_t cap_tiles, Counters* __restrict__ ctr)
-{
-    __shared__ uint32_t tmp[8];
-    __shared__ uint32_t carry, elems;
-    if (threadIdx.x == 0)
-        carry = elems = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < nb; base += TPB)
-    {
-        const uint32_t i  = base + threadIdx.x;
-        const uint32_t nt = (i < nb) ? div_up(buckets[i].len, TILE) : 0;
-        if (i < nb)
-            atomicAdd(&elems, buckets[i].len);
-        uint32_t       total;
-        const uint32_t ex = block256_exclusive_sum(nt, tmp, &total);
-        const uint32_t t0 = carry + ex;
-        if (i < nb)
-        {
-            buckets[i].tile0 = t0;
-            for (uint32_t t = 0; t < nt; ++t)
-                if (t0 + t < cap_tiles)
-                    tile_bucket[t0 + t] = i;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0)
-            carry += total;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0)
-    {
-        ctr->n_tiles = carry;
-        ctr->n_elems = elems;
-        if (carry > cap_tiles)
-            ctr->overflow = 1;
-    }
-}
-
-// -------------------------------------------------------------------------------------------------
-// wave jobs: sort <= 256 elements in registers, refine ties (STRING) or split groups (RANK)
+// jobs: <= 256*W elements sorted by W waves (4 per lane; W = 1 wave jobs, W > 1 workgroup jobs).
+// STRING mode sorts by 128-bit keys: the group id in the top GBITS bits, then the next
+// 128 - GBITS bits of the rotation gathered from the input at the group's depth (15 bytes per round
+// for W = 1, 14 for W > 1).  Round 1's groups are the job's sub-buckets (their digit at depth d-1);
+// every later round only handles the elements still tied, compacted with a job-wide prefix count
+// and re-sorted with a network of the compacted size.  A round's active elements occupy an
+// increasing list of job positions; the sort permutes elements over that list.  STRING mode stops
+// when nothing is tied, when the depth reaches n (ties = identical rotations) or at the depth cap
+// (the tied groups go to the fallback).  RANK mode sorts once by the 32-bit rank key and emits
+// the equal-key groups as the next fallback round's groups.
 // -------------------------------------------------------------------------------------------------
 struct JobArgs
 {
@@ -500,134 +572,373 @@ struct JobArgs
     uint32_t         hstep;  // RANK mode: depth added to a subgroup (min depth of the round)
 };
 
-template <uint32_t MODE>
-__global__ void __launch_bounds__(256) k_jobs(JobArgs a)
+template <int W>
+struct JobLds
 {
-    const int      lane   = lane_id();
-    const uint32_t wid    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t j = wid; j < a.njobs; j += nwaves)
+    uint64_t kh[256 * W];   // cross-wave network exchange, neighbour keys, compaction scratch
+    uint64_t kl[256 * W];
+    uint32_t v[256 * W];
+    uint16_t pos[256 * W];  // job position of each active slot (increasing)
+    uint32_t agg[W];
+};
+
+template <int W>
+__device__ __forceinline__ void job_sync()
+{
+    if (W > 1)
+        __syncthreads();
+    else
     {
-        const Job       J  = a.jobs[j];
-        const BlockDesc BD = a.blocks[J.block];
-        const uint8_t*  blk = a.in + BD.off;
-        const uint64_t* K  = J.buf ? a.key1 : a.key0;
-        const uint32_t* V  = J.buf ? a.pay1 : a.pay0;
-        uint64_t        k[4];
-        uint32_t        v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+template <int W>
+__device__ __forceinline__ bool job_any(bool x)
+{
+    if (W > 1)
+        return __syncthreads_or(x);
+    return __any(x);
+}
+
+// (hi, lo, v) lexicographic "greater than"
+__device__ __forceinline__ bool k3_gt(uint64_t ha, uint64_t la, uint32_t va, uint64_t hb, uint64_t lb, uint32_t vb)
+{
+    if (ha != hb)
+        return ha > hb;
+    if (la != lb)
+        return la > lb;
+    return va > vb;
+}
+
+template <int W>
+__device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], uint32_t (&v)[4], int P, JobLds<W>& S, int wj)
+{
+    const int lane = lane_id();
+    for (int size = 2; size <= P; size <<= 1)
+    {
+        for (int j = size >> 1; j > 0; j >>= 1)
         {
-            const uint32_t e = lane * 4 + r;
-            if (e < J.len)
+            if (W > 1 && j >= 256)
             {
-                k[r] = K[J.start + e];
-                v[r] = V[J.start + e];
+                job_sync<W>();
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const int e = wj * 256 + lane * 4 + r;
+                    S.kh[e]     = kh[r];
+                    S.kl[e]     = kl[r];
+                    S.v[e]      = v[r];
+                }
+                job_sync<W>();
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const int      e    = wj * 256 + lane * 4 + r;
+                    const uint64_t oh   = S.kh[e ^ j];
+                    const uint64_t ol   = S.kl[e ^ j];
+                    const uint32_t ov   = S.v[e ^ j];
+                    const bool     up   = (e & size) == 0;
+                    const bool     low  = (e & j) == 0;
+                    const bool     gt   = k3_gt(kh[r], kl[r], v[r], oh, ol, ov);
+                    const bool     take = (low == up) ? gt : !gt;
+                    if (take)
+                    {
+                        kh[r] = oh;
+                        kl[r] = ol;
+                        v[r]  = ov;
+                    }
+                }
+            }
+            else if (j >= 4)
+            {
+                const int lm = j >> 2;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const int      e    = wj * 256 + lane * 4 + r;
+                    const uint64_t oh   = shfl_xor64(kh[r], lm);
+                    const uint64_t ol   = shfl_xor64(kl[r], lm);
+                    const uint32_t ov   = __shfl_xor(v[r], lm, WAVE);
+                    const bool     up   = (e & size) == 0;
+                    const bool     low  = (e & j) == 0;
+                    const bool     gt   = k3_gt(kh[r], kl[r], v[r], oh, ol, ov);
+                    const bool     take = (low == up) ? gt : !gt;
+                    if (take)
+                    {
+                        kh[r] = oh;
+                        kl[r] = ol;
+                        v[r]  = ov;
+                    }
+                }
             }
             else
             {
-                k[r] = ~0ull;
-                v[r] = ~0u;
-            }
-        }
-        int P = 4;
-        while ((uint32_t) P < J.len)
-            P <<= 1;
-        wave_bitonic_sort4(k, v, P);
-
-        uint32_t g[4], gend[4];
-        bool     tied[4];
-        bool     final_ties = false, to_fallback = false;
-        uint32_t depth      = (MODE == MODE_STRING) ? J.kd + 8 : J.gdepth;
-        for (;;)
-        {
-            // group starts (head = key differs from predecessor)
-            uint64_t prev3 = shfl_up64(k[3], 1);
-            uint32_t h[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-                const uint32_t e  = lane * 4 + r;
-                const uint64_t pk = (r == 0) ? prev3 : k[r - 1];
-                const bool     hd = (e == 0) || e >= J.len || pk != k[r];
-                h[r]              = hd ? e : 0;
-                g[r]              = h[r];
-                gend[r]           = hd ? e : 0xFFFFFFFFu;
-            }
-            wave_max_scan4(g);
-            // group end: next head strictly after e
-            uint32_t nh[4];
-            {
-                uint32_t x[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    x[r] = gend[r];
-                wave_min_rscan4(x);  // x[r] = first head at or after e
-                uint32_t nxt0 = __shfl_down(x[0], 1, WAVE);
-                if (lane == WAVE - 1)
-                    nxt0 = 0xFFFFFFFFu;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    nh[r] = (r < 3) ? x[r + 1] : nxt0;
-            }
-            bool any = false;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-                const uint32_t e   = lane * 4 + r;
-                const uint32_t end = min(nh[r] == 0xFFFFFFFFu ? (uint32_t) P : nh[r], J.len);
-                gend[r]            = end;  // exclusive end of e's group
-                tied[r]            = e < J.len && (end - g[r]) >= 2;
-                any |= tied[r];
-            }
-            any = __any(any);
-            if (MODE == MODE_RANK || !any)
-                break;
-            if (depth >= BD.len)
-            {
-                final_ties = true;
-                break;
-            }
-            if (depth >= a.dcap)
-            {
-                to_fallback = true;
-                break;
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-                const uint32_t e = lane * 4 + r;
-                if (e < J.len)
                 {
-                    uint64_t nk = (uint64_t) g[r] << 56;
-                    if (tied[r])
+                    const int p = r ^ j;
+                    if (p > r)
                     {
-                        const uint32_t idx = v[r] & 0xFFFFFFu;
-                        uint32_t       st  = idx + depth;
-                        if (st >= BD.len)
-                            st -= BD.len;
-                        nk |= load_key8(blk, BD.len, st) >> 8;
+                        const int  e  = wj * 256 + lane * 4 + r;
+                        const bool up = (e & size) == 0;
+                        const bool gt = k3_gt(kh[r], kl[r], v[r], kh[p], kl[p], v[p]);
+                        if (gt == up)
+                        {
+                            uint64_t t0 = kh[r];
+                            kh[r]       = kh[p];
+                            kh[p]       = t0;
+                            uint64_t t1 = kl[r];
+                            kl[r]       = kl[p];
+                            kl[p]       = t1;
+                            uint32_t tv = v[r];
+                            v[r]        = v[p];
+                            v[p]        = tv;
+                        }
                     }
-                    k[r] = nk;
                 }
             }
-            wave_bitonic_sort4(k, v, P);
-            depth += 7;
         }
+    }
+    job_sync<W>();
+}
 
-        // outputs
+// inclusive max-scan / reverse min-scan / exclusive count over the job's 256*W slots
+template <int W>
+__device__ __forceinline__ void job_max_scan(uint32_t (&x)[4], JobLds<W>& S, int wj)
+{
+    wave_max_scan4(x);
+    if (W > 1)
+    {
+        if (lane_id() == 63)
+            S.agg[wj] = x[3];
+        job_sync<W>();
+        uint32_t ex = 0;
+        for (int w = 0; w < wj; ++w)
+            ex = max(ex, S.agg[w]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            x[r] = max(x[r], ex);
+        job_sync<W>();
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void job_min_rscan(uint32_t (&x)[4], JobLds<W>& S, int wj)
+{
+    wave_min_rscan4(x);
+    if (W > 1)
+    {
+        if (lane_id() == 0)
+            S.agg[wj] = x[0];
+        job_sync<W>();
+        uint32_t ex = 0xFFFFFFFFu;
+        for (int w = wj + 1; w < W; ++w)
+            ex = min(ex, S.agg[w]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            x[r] = min(x[r], ex);
+        job_sync<W>();
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex)[4], uint32_t& total, JobLds<W>& S, int wj)
+{
+    const int lane = lane_id();
+    uint32_t  c    = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        ex[r] = c;
+        c += f[r] ? 1u : 0u;
+    }
+    uint32_t x = c;
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        const uint32_t o = __shfl_up(x, d, WAVE);
+        if (lane >= d)
+            x += o;
+    }
+    uint32_t wtot = __shfl(x, 63, WAVE), pre = x - c;
+    if (W > 1)
+    {
+        if (lane == 63)
+            S.agg[wj] = x;
+        job_sync<W>();
+        uint32_t before = 0, all = 0;
+        for (int w = 0; w < W; ++w)
+        {
+            const uint32_t a = S.agg[w];
+            if (w < wj)
+                before += a;
+            all += a;
+        }
+        pre += before;
+        wtot = all;
+        job_sync<W>();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        ex[r] += pre;
+    total = wtot;
+}
+
+// 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian
+__device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint32_t n, uint32_t start, uint64_t& w0, uint64_t& w1)
+{
+    w0          = load_key8(blk, n, start);
+    uint32_t s2 = start + 8;
+    while (s2 >= n)
+        s2 -= n;
+    w1 = load_key8(blk, n, s2);
+}
+
+// Group heads / group ends / ties over the T active slots (keys in S.kh / S.kl must be current).
+template <int W>
+__device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64_t (&kl)[4], uint32_t T, JobLds<W>& S, int wj,
+                                           uint32_t (&g)[4], uint32_t (&gend)[4], bool (&tied)[4])
+{
+    constexpr uint32_t SLOTS = 256 * W;
+    const int          lane  = lane_id();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = wj * 256 + lane * 4 + r;
+        S.kh[c]          = kh[r];
+        S.kl[c]          = kl[r];
+    }
+    job_sync<W>();
+    uint32_t x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c  = wj * 256 + lane * 4 + r;
+        const bool     hd = (c == 0) || c >= T || S.kh[c - 1] != kh[r] || S.kl[c - 1] != kl[r];
+        g[r]              = hd ? c : 0;
+        x[r]              = hd ? c : 0xFFFFFFFFu;
+    }
+    job_max_scan<W>(g, S, wj);
+    job_min_rscan<W>(x, S, wj);
+    uint32_t* nxt = S.v;
+    job_sync<W>();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        nxt[wj * 256 + lane * 4 + r] = x[r];
+    job_sync<W>();
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c   = wj * 256 + lane * 4 + r;
+        const uint32_t nh  = (c + 1 < SLOTS) ? nxt[c + 1] : 0xFFFFFFFFu;
+        const uint32_t end = min(nh == 0xFFFFFFFFu ? SLOTS : nh, T);
+        gend[r]            = end;
+        tied[r]            = c < T && (end - g[r]) >= 2;
+        any |= tied[r];
+    }
+    job_sync<W>();
+    return job_any<W>(any);
+}
+
+template <uint32_t MODE, int W>
+__device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj)
+{
+    constexpr int      GBITS = (W > 1) ? 12 : 8;        // group-id bits
+    constexpr uint32_t ADV   = (128 - GBITS) / 8;       // whole rotation bytes per round
+    const int          lane  = lane_id();
+    const BlockDesc    BD    = a.blocks[J.block];
+    const uint8_t*     blk   = a.in + BD.off;
+    const uint64_t*    K     = J.buf ? a.key1 : a.key0;
+    const uint32_t*    V     = J.buf ? a.pay1 : a.pay0;
+    const uint32_t     boff  = (uint32_t) BD.off;
+    uint64_t           kh[4], kl[4];
+    uint32_t           v[4];
+    uint32_t           pos[4];  // job position of slot c
+    uint32_t           g[4], gend[4];
+    bool               tied[4];
+    uint32_t           T     = J.len;
+    uint32_t           depth = (MODE == MODE_STRING) ? J.d : J.gdepth;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = wj * 256 + lane * 4 + r;
+        pos[r]           = c;
+        if (c < T)
+        {
+            v[r] = V[J.start + c];
+            if (MODE == MODE_RANK)
+            {
+                kh[r] = K[J.start + c];
+                kl[r] = 0;
+            }
+            else
+            {
+                // sub-bucket = digit at depth d-1 (elements of one digit are contiguous)
+                const uint64_t key = K[J.start + c];
+                kh[r]              = (key >> (56 - 8 * (J.d - 1 - J.kd))) & 0xFF;
+                kl[r]              = 0;
+            }
+        }
+        else
+        {
+            kh[r] = kl[r] = ~0ull;
+            v[r]          = ~0u;
+        }
+    }
+    if (MODE == MODE_STRING)
+    {
+        // round 1 groups = sub-buckets; keys = group id | 128-GBITS bits at depth d
+        job_groups<W>(kh, kl, T, S, wj, g, gend, tied);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            const uint32_t e = lane * 4 + r;
-            if (e >= J.len)
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            if (c < T)
+            {
+                const uint32_t idx = v[r] & 0xFFFFFFu;
+                uint32_t       st  = idx + (depth % BD.len);
+                if (st >= BD.len)
+                    st -= BD.len;
+                uint64_t w0, w1;
+                load_key16(blk, BD.len, st, w0, w1);
+                kh[r] = ((uint64_t) g[r] << (64 - GBITS)) | (w0 >> GBITS);
+                kl[r] = (w0 << (64 - GBITS)) | (w1 >> GBITS);
+            }
+        }
+    }
+    int P = 4;
+    while ((uint32_t) P < T)
+        P <<= 1;
+    job_sort<W>(kh, kl, v, P, S, wj);
+    if (MODE == MODE_STRING)
+        depth += ADV;
+    for (;;)
+    {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            S.pos[wj * 256 + lane * 4 + r] = (uint16_t) pos[r];
+        const bool any    = job_groups<W>(kh, kl, T, S, wj, g, gend, tied);
+        bool       finish = (MODE == MODE_RANK) || !any;
+        bool final_ties = false, to_fallback = false;
+        if (!finish && depth >= BD.len)
+            finish = final_ties = true;
+        else if (!finish && depth >= a.dcap)
+            finish = to_fallback = true;
+        // ---- outputs of the resolved slots (all slots when finishing) ----
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            if (c >= T || (!finish && tied[r]))
                 continue;
-            const uint32_t slot = J.start + e;
+            const uint32_t slot = J.start + pos[r];
             const uint32_t idx  = v[r] & 0xFFFFFFu;
-            const uint32_t loc  = slot - (uint32_t) BD.off;
             a.fsa[slot]         = idx;
             a.L[slot]           = (uint8_t) (v[r] >> 24);
-            const uint32_t gst  = J.start + g[r] - (uint32_t) BD.off;  // block-local group start
+            const uint32_t gst  = J.start + S.pos[g[r]] - boff;  // block-local start of the group
             if (MODE == MODE_RANK)
                 a.isa[BD.off + idx] = gst;
             if (idx == 0)
@@ -635,17 +946,17 @@ __global__ void __launch_bounds__(256) k_jobs(JobArgs a)
                 if (MODE == MODE_RANK || final_ties)
                     a.pi[J.block] = gst;
                 else if (!(to_fallback && tied[r]))
-                    a.pi[J.block] = loc;
+                    a.pi[J.block] = slot - boff;
             }
-            const bool emit = (MODE == MODE_RANK) ? tied[r] : (to_fallback && tied[r]);
-            if (emit && g[r] == e)
+            const bool emit = tied[r] && (MODE == MODE_RANK || to_fallback);
+            if (emit && g[r] == c)
             {
-                const uint32_t gl   = gend[r] - e;
-                const uint32_t gd   = (MODE == MODE_RANK) ? J.gdepth + a.hstep : depth;
+                const uint32_t gl    = gend[r] - c;
+                const uint32_t gd    = (MODE == MODE_RANK) ? J.gdepth + a.hstep : depth;
                 const uint32_t slot2 = atomicAdd(&a.ctr->n_groups, 1u);
                 if (slot2 < a.cap_groups)
                 {
-                    a.groups[slot2] = Group{slot, gl, gd, J.block | (1u << 30)};  // bit 30: data already in fsa
+                    a.groups[slot2] = Group{slot, gl, gd, J.block | (1u << 30)};  // bit 30: members already in fsa
                     atomicAdd(&a.ctr->g_members, gl);
                     atomicMin(&a.ctr->hmin, gd);
                 }
@@ -653,6 +964,76 @@ __global__ void __launch_bounds__(256) k_jobs(JobArgs a)
                     atomicExch(&a.ctr->overflow, 1u);
             }
         }
+        if (finish)
+            break;
+        // ---- compact the tied slots; next round on the next ADV bytes ----
+        uint32_t cx[4], T2;
+        job_excl_count<W>(tied, cx, T2, S, wj);
+        job_sync<W>();
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (tied[r])
+            {
+                const uint32_t c = wj * 256 + lane * 4 + r;
+                S.v[cx[r]]       = v[r];
+                S.kh[cx[r]]      = ((uint64_t) (cx[r] - (c - g[r])) << 16) | pos[r];  // new group head | position
+            }
+        job_sync<W>();
+        T = T2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            if (c < T)
+            {
+                const uint64_t gp  = S.kh[c];
+                pos[r]             = (uint32_t) (gp & 0xFFFF);
+                v[r]               = S.v[c];
+                const uint32_t idx = v[r] & 0xFFFFFFu;
+                uint32_t       st  = idx + (depth % BD.len);
+                if (st >= BD.len)
+                    st -= BD.len;
+                uint64_t w0, w1;
+                load_key16(blk, BD.len, st, w0, w1);
+                kh[r] = ((gp >> 16) << (64 - GBITS)) | (w0 >> GBITS);
+                kl[r] = (w0 << (64 - GBITS)) | (w1 >> GBITS);
+            }
+            else
+            {
+                pos[r] = c;
+                kh[r] = kl[r] = ~0ull;
+                v[r]          = ~0u;
+            }
+        }
+        job_sync<W>();
+        P = 4;
+        while ((uint32_t) P < T)
+            P <<= 1;
+        job_sort<W>(kh, kl, v, P, S, wj);
+        depth += ADV;
+    }
+}
+
+template <uint32_t MODE>
+__global__ void __launch_bounds__(256) k_jobs(JobArgs a)
+{
+    __shared__ JobLds<1> lds[4];
+    const int      wl     = threadIdx.x >> 6;
+    const uint32_t wid    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t j = wid; j < a.njobs; j += nwaves)
+        job_run<MODE, 1>(a, a.jobs[j], lds[wl], 0);
+}
+
+template <uint32_t MODE, int W>
+__global__ void __launch_bounds__(64 * W) k_mjobs(JobArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    JobLds<W>& S = *reinterpret_cast<JobLds<W>*>(smem);
+    for (uint32_t j = blockIdx.x; j < a.njobs; j += gridDim.x)
+    {
+        job_run<MODE, W>(a, a.jobs[j], S, threadIdx.x >> 6);
+        __syncthreads();
     }
 }
 
@@ -728,19 +1109,36 @@ __global__ void k_rank_keys(const Group* __restrict__ groups, uint32_t ng, const
     }
 }
 
-// Groups -> RANK buckets (big) and one job per small group.
+// Groups -> RANK buckets (big; tiles reserved for the first level), one workgroup job per medium
+// group, one wave job per small group.
 __global__ void k_groups_to_work(const Group* __restrict__ groups, uint32_t ng, Bucket* __restrict__ big, uint32_t cap_big,
-                                 Job* __restrict__ jobs, uint32_t cap_jobs, Counters* __restrict__ ctr)
+                                 uint32_t* __restrict__ tile_bucket, uint32_t cap_tiles, Job* __restrict__ jobs, uint32_t cap_jobs,
+                                 Job* __restrict__ mjobs, uint32_t cap_mjobs, uint32_t mjob_max, Counters* __restrict__ ctr)
 {
     for (uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x; gi < ng; gi += gridDim.x * blockDim.x)
     {
         const Group    G = groups[gi];
         const uint32_t b = G.block & 0x3FFFFFFFu;
-        if (G.len > JOB_MAX)
+        if (G.len > mjob_max)
         {
-            const uint32_t s = atomicAdd(&ctr->n_big, 1u);
-            if (s < cap_big)
-                big[s] = Bucket{G.start, G.len, 0, 0, b, 0, G.depth, 0};
+            const uint32_t ntl = div_up(G.len, TILE);
+            const unsigned long long old =
+                atomicAdd(reinterpret_cast<unsigned long long*>(&ctr->n_big), ((unsigned long long) ntl << 32) | 1ull);
+            const uint32_t s = (uint32_t) old, t0 = (uint32_t) (old >> 32);
+            if (s < cap_big && t0 + ntl <= cap_tiles)
+            {
+                big[s] = Bucket{G.start, G.len, 0, 0, b, 0, G.depth, t0};
+                for (uint32_t t = 0; t < ntl; ++t)
+                    tile_bucket[t0 + t] = s;
+            }
+            else
+                atomicExch(&ctr->overflow, 1u);
+        }
+        else if (G.len > JOB_MAX)
+        {
+            const uint32_t s = atomicAdd(&ctr->n_mjobs, 1u);
+            if (s < cap_mjobs)
+                mjobs[s] = Job{G.start, G.len, 0, 0, b, G.depth, 0};
             else
                 atomicExch(&ctr->overflow, 1u);
         }
@@ -748,7 +1146,7 @@ __global__ void k_groups_to_work(const Group* __restrict__ groups, uint32_t ng, 
         {
             const uint32_t s = atomicAdd(&ctr->n_jobs, 1u);
             if (s < cap_jobs)
-                jobs[s] = Job{G.start, G.len, 0, 0, b, G.depth};
+                jobs[s] = Job{G.start, G.len, 0, 0, b, G.depth, 0};
             else
                 atomicExch(&ctr->overflow, 1u);
         }
@@ -798,26 +1196,41 @@ __global__ void k_pi_from_isa(const BlockDesc* __restrict__ blocks, const uint8_
 // =================================================================================================
 struct BwtWorkspace
 {
-    uint64_t  cap_n      = 0;
-    uint32_t  cap_blocks = 0;
-    uint64_t* key[2]     = {nullptr, nullptr};
-    uint32_t* pay[2]     = {nullptr, nullptr};
-    uint32_t* fsa        = nullptr;
-    uint32_t* isa        = nullptr;
-    uint32_t* tile_hist  = nullptr;
-    uint32_t* tile_off   = nullptr;
-    uint32_t* tile_bucket = nullptr;
-    uint8_t*  nomove     = nullptr;
-    uint8_t*  flag       = nullptr;
-    Bucket*   big[2]     = {nullptr, nullptr};
-    Job*      jobs       = nullptr;
-    Group*    groups[2]  = {nullptr, nullptr};
-    Counters* ctr        = nullptr;
-    Counters* h_ctr      = nullptr;  // pinned
-    L0Tile*   l0tiles    = nullptr;
-    uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_groups = 0, cap_l0 = 0;
+    uint64_t  cap_n          = 0;
+    uint32_t  cap_blocks     = 0;
+    uint64_t* key[2]         = {nullptr, nullptr};
+    uint32_t* pay[2]         = {nullptr, nullptr};
+    uint32_t* fsa            = nullptr;
+    uint32_t* isa            = nullptr;
+    uint32_t* tile_hist      = nullptr;
+    uint32_t* tile_off       = nullptr;
+    uint32_t* tile_bucket[2] = {nullptr, nullptr};
+    uint8_t*  nomove         = nullptr;
+    uint8_t*  flag           = nullptr;
+    Bucket*   big[2]         = {nullptr, nullptr};
+    Job*      jobs           = nullptr;
+    Job*      mjobs          = nullptr;
+    Group*    groups[2]      = {nullptr, nullptr};
+    Counters* ctr            = nullptr;
+    Counters* h_ctr          = nullptr;  // pinned
+    L0Tile*   l0tiles        = nullptr;
+    uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
     int       grid = 2048;
+    int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
+    uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
+
+template <uint32_t MODE>
+static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
+{
+    const dim3 g(std::min<uint32_t>(n, 2048u));
+    if (waves == 16)
+        hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>), s, a);
+    else if (waves == 8)
+        hipLaunchKernelGGL((k_mjobs<MODE, 8>), g, dim3(64 * 8), sizeof(JobLds<8>), s, a);
+    else
+        hipLaunchKernelGGL((k_mjobs<MODE, 4>), g, dim3(64 * 4), sizeof(JobLds<4>), s, a);
+}
 
 static void ws_free(BwtWorkspace& w)
 {
@@ -827,15 +1240,16 @@ static void ws_free(BwtWorkspace& w)
         (void) hipFree(w.pay[i]);
         (void) hipFree(w.big[i]);
         (void) hipFree(w.groups[i]);
+        (void) hipFree(w.tile_bucket[i]);
     }
     (void) hipFree(w.fsa);
     (void) hipFree(w.isa);
     (void) hipFree(w.tile_hist);
     (void) hipFree(w.tile_off);
-    (void) hipFree(w.tile_bucket);
     (void) hipFree(w.nomove);
     (void) hipFree(w.flag);
     (void) hipFree(w.jobs);
+    (void) hipFree(w.mjobs);
     (void) hipFree(w.ctr);
     (void) hipFree(w.l0tiles);
     if (w.h_ctr)
@@ -855,6 +1269,11 @@ void          bwt_workspace_destroy(BwtWorkspace* w)
 
 static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
 {
+    if (const char* e = getenv("BRA_MJ_WAVES"))  // tuning knob: 0 (off), 4, 8 or 16 waves per workgroup job
+    {
+        const int v = atoi(e);
+        w.mj_waves  = (v == 0 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
+    }
     if (n <= w.cap_n && nblocks <= w.cap_blocks)
         return true;
     ws_free(w);
@@ -867,22 +1286,24 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     w.cap_tiles  = (uint32_t) (N / TILE + w.cap_big + 16);
     w.cap_jobs   = (uint32_t) (N / 8 + B + 1024);
     w.cap_groups = (uint32_t) (N / 64 + B + 4096);
+    w.cap_mjobs  = (uint32_t) (N / JOB_MAX + B + 64);
     for (int i = 0; i < 2; ++i)
     {
         BRA_HIP_CHECK(hipMalloc(&w.key[i], N * 8));
         BRA_HIP_CHECK(hipMalloc(&w.pay[i], N * 4));
         BRA_HIP_CHECK(hipMalloc(&w.big[i], (size_t) w.cap_big * sizeof(Bucket)));
         BRA_HIP_CHECK(hipMalloc(&w.groups[i], (size_t) w.cap_groups * sizeof(Group)));
+        BRA_HIP_CHECK(hipMalloc(&w.tile_bucket[i], (size_t) w.cap_tiles * 4));
     }
     BRA_HIP_CHECK(hipMalloc(&w.fsa, N * 4));
     BRA_HIP_CHECK(hipMalloc(&w.isa, N * 4));
     const uint32_t tmax = std::max(w.cap_tiles, w.cap_l0);
     BRA_HIP_CHECK(hipMalloc(&w.tile_hist, (size_t) tmax * 256 * 4));
     BRA_HIP_CHECK(hipMalloc(&w.tile_off, (size_t) tmax * 256 * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.tile_bucket, (size_t) tmax * 4));
     BRA_HIP_CHECK(hipMalloc(&w.nomove, std::max<uint32_t>(w.cap_big, B)));
     BRA_HIP_CHECK(hipMalloc(&w.flag, B));
     BRA_HIP_CHECK(hipMalloc(&w.jobs, (size_t) w.cap_jobs * sizeof(Job)));
+    BRA_HIP_CHECK(hipMalloc(&w.mjobs, (size_t) w.cap_mjobs * sizeof(Job)));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
     BRA_HIP_CHECK(hipMalloc(&w.l0tiles, (size_t) w.cap_l0 * sizeof(L0Tile)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault));
@@ -904,46 +1325,41 @@ static bool read_ctr(BwtWorkspace& w, hipStream_t s)
 static bool reset_ctr(BwtWorkspace& w, hipStream_t s)
 {
     Counters z{};
-    z.hmin = 0xFFFFFFFFu;
-    // small H2D of a constant: use the pinned staging to stay async-safe
-    *w.h_ctr = z;
+    z.hmin   = 0xFFFFFFFFu;
+    *w.h_ctr = z;  // pinned staging; the copy is ordered before any kernel of this call
     BRA_HIP_CHECK(hipMemcpyAsync(w.ctr, w.h_ctr, sizeof(Counters), hipMemcpyHostToDevice, s));
     return true;
 }
 
 static size_t tile_stage_bytes() { return sizeof(TileStage); }
 
-// Runs the MSD levels + wave jobs for the buckets currently in w.big[cur] (count nbig) and the jobs
-// already queued.  Returns false on error.
+// MSD levels for the buckets in w.big[cur] (tiles already reserved in w.tile_bucket[cur] and
+// ctr->n_tiles_next).  Sub-buckets become jobs / fallback groups (appended to the queues).
 template <uint32_t MODE>
-static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, uint32_t nbig, int cur, uint8_t* d_L,
-                       uint32_t* d_pi, Group* groups_out, uint32_t hstep, hipStream_t s, uint32_t& njobs_total)
+static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, uint32_t nbig, int cur, Group* groups_out,
+                       hipStream_t s)
 {
-    const size_t lds = tile_stage_bytes();
+    const size_t lds  = tile_stage_bytes();
+    const int    grid = w.grid;
     while (nbig > 0)
     {
-        {
-            BRA_PROF(P_BWT_TILES, s);
-            hipLaunchKernelGGL(k_build_tiles, dim3(1), dim3(TPB), 0, s, w.big[cur], nbig, w.tile_bucket, w.cap_tiles, w.ctr);
-        }
-        // zero n_big / n_moved for the next level (keep jobs/groups counters)
-        BRA_HIP_CHECK(hipMemsetAsync(&w.ctr->n_big, 0, 4, s));
-        BRA_HIP_CHECK(hipMemsetAsync(&w.ctr->n_moved, 0, 4, s));
-        const int grid = w.grid;
+        hipLaunchKernelGGL(k_level_start, dim3(1), dim3(1), 0, s, w.ctr);
         {
             BRA_PROF(P_BWT_HIST, s);
-            hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket, w.ctr, w.key[0],
+            hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket[cur], w.ctr, w.key[0],
                                w.key[1], w.pay[0], w.pay[1], w.tile_hist);
         }
-        ScanArgs a{w.big[cur], nbig,    w.tile_hist, w.tile_off, w.nomove,  w.big[cur ^ 1], w.cap_big, w.jobs, w.cap_jobs,
-                   groups_out, w.cap_groups, w.ctr,  MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES};
+        ScanArgs a{w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
+                   w.cap_big,   w.tile_bucket[cur ^ 1],   w.cap_tiles, w.jobs,       w.cap_jobs,
+                   w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
+                   (uint32_t) (g_prof != nullptr), w.mjob_max()};
         {
             BRA_PROF(P_BWT_SCAN, s);
             hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(nbig, 65535u)), dim3(TPB), 0, s, a);
         }
         {
             BRA_PROF(P_BWT_SCATTER, s);
-            hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket, w.ctr, w.tile_off,
+            hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
                                w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
         }
         BRA_HIP_CHECK(hipGetLastError());
@@ -951,15 +1367,12 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             return false;
         // algorithmic bytes: keys read by the histogram, tile histograms, KV moved by the scatter
         const double nt = w.h_ctr->n_tiles, ne = w.h_ctr->n_elems, nm = w.h_ctr->n_moved;
-        prof_bytes(P_BWT_TILES, 32.0 * nbig + 4.0 * nt);
         prof_bytes(P_BWT_HIST, 8.0 * ne + 1024.0 * nt);
         prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * nbig);
         prof_bytes(P_BWT_SCATTER, 24.0 * nm + 1024.0 * nt);
         nbig = w.h_ctr->n_big;
         cur ^= 1;
     }
-    (void) d_L, (void) d_pi, (void) hstep;
-    njobs_total = w.h_ctr->n_jobs;
     return true;
 }
 
@@ -990,8 +1403,13 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (lds + TILE + 16)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>)));
         attr_set = true;
     }
+    const int grid = w.grid;
 
     // ---- level 0 (buckets = blocks, elements read straight from the input) ----
     std::vector<L0Tile> tiles;
@@ -1008,13 +1426,13 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     if (!reset_ctr(w, s))
         return false;
     BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, nblocks, s));
-    const int grid = w.grid;
     {
         BRA_PROF(P_BWT_L0HIST, s);
         hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist);
     }
-    ScanArgs a0{w.big[1], nblocks,  w.tile_hist, w.tile_off, w.nomove, w.big[0], w.cap_big, w.jobs, w.cap_jobs,
-                w.groups[0], w.cap_groups, w.ctr, DCAP_BIG};
+    ScanArgs a0{w.big[1],  nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
+                w.tile_bucket[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
+                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max()};
     {
         BRA_PROF(P_BWT_SCAN, s);
         hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(TPB), 0, s, a0);
@@ -1030,161 +1448,122 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
     prof_bytes(P_BWT_L0SCATTER, 13.0 * N + 1024.0 * nt0);
-    // Level 0 never keeps data in place ("nomove" only matters for level >= 1): all sub-buckets are in buf 0.
-    uint32_t njobs = 0;
-    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, 0, d_L, d_pi, w.groups[0], 0, s, njobs))
+    // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]
+    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, 0, w.groups[0], s))
         return false;
 
     // ---- wave jobs ----
+    const uint32_t njobs = w.h_ctr->n_jobs;
     JobArgs ja{w.jobs,  njobs,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
                w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0};
     if (njobs)
-        {
-            BRA_PROF(P_BWT_JOBS, s);
-            hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(std::min<uint32_t>(div_up(njobs, 4), 8192u)), dim3(256), 0, s, ja);
-        }
+    {
+        BRA_PROF(P_BWT_JOBS, s);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(std::min<uint32_t>(div_up(njobs, 4), 8192u)), dim3(256), 0, s, ja);
+    }
+    const uint32_t nmjobs = w.h_ctr->n_mjobs;
+    if (nmjobs)
+    {
+        JobArgs jm = ja;
+        jm.jobs    = w.mjobs;
+        jm.njobs   = nmjobs;
+        BRA_PROF(P_BWT_MJOBS, s);
+        launch_mjobs<MODE_STRING>(w.mj_waves, nmjobs, jm, s);
+    }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
         return false;
-    prof_bytes(P_BWT_JOBS, 17.0 * N);  // read key+payload, write SA entry + L byte
+    // read key+payload, write SA entry + L byte (split by the elements each kind of job covers)
+    prof_bytes(P_BWT_JOBS, 17.0 * ((double) N - (double) w.h_ctr->n_melems));
+    prof_bytes(P_BWT_MJOBS, 17.0 * (double) w.h_ctr->n_melems);
 
     // ---- fallback: prefix doubling on the groups still tied ----
     uint32_t ng = w.h_ctr->n_groups;
     if (ng == 0)
         return true;
+    BRA_PROF(P_BWT_FALLBACK, s);
     int gcur = 0;
     hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pay[0], w.pay[1], w.fsa);
     // mark blocks, build ranks: singletons rank = own slot, group members = group start
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
-                       w.flag);  // sets flags (isa writes are redone below)
+                       w.flag);  // sets the flags (its rank writes are redone below)
     hipLaunchKernelGGL(k_isa_init, dim3(64, std::min<uint32_t>(nblocks, 65535u)), dim3(256), 0, s, d_blocks, w.flag, nblocks, w.fsa, w.isa);
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
                        w.flag);
-    uint64_t members = w.h_ctr->g_members;
     uint32_t hmin    = w.h_ctr->hmin;
     for (int round = 0; round < 64 && ng > 0; ++round)
     {
-        // keys for this round (all reads of isa happen here, before any rank update)
+        // keys for this round (every read of isa happens here, before any rank update)
         hipLaunchKernelGGL(k_rank_keys, dim3(std::min<uint32_t>(ng, 8192u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, d_in, w.fsa,
                            w.isa, w.key[0], w.pay[0]);
-        Counters z{};
-        z.hmin   = 0xFFFFFFFFu;
-        *w.h_ctr = z;
-        BRA_HIP_CHECK(hipMemcpyAsync(w.ctr, w.h_ctr, sizeof(Counters), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(k_groups_to_work, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.big[0],
-                           w.cap_big, w.jobs, w.cap_jobs, w.ctr);
+        if (!reset_ctr(w, s))
+            return false;
+        hipLaunchKernelGGL(k_groups_to_work, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng,
+                           w.big[0], w.cap_big, w.tile_bucket[0], w.cap_tiles, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs, w.mjob_max(), w.ctr);
         if (!read_ctr(w, s))
             return false;
-        const uint32_t nbig0 = w.h_ctr->n_big;
-        // subgroups go to groups[gcur^1]; their depth = group depth + hmin
         Group* gnext = w.groups[gcur ^ 1];
-        // run the MSD levels in RANK mode
-        {
-            uint32_t nb  = nbig0;
-            int      cur = 0;
-            // big buckets: levels over 4 key bytes; subgroups of equal key > JOB_MAX become groups directly
-            while (nb > 0)
-            {
-                {
-                    BRA_PROF(P_BWT_TILES, s);
-                    hipLaunchKernelGGL(k_build_tiles, dim3(1), dim3(TPB), 0, s, w.big[cur], nb, w.tile_bucket, w.cap_tiles, w.ctr);
-                }
-                BRA_HIP_CHECK(hipMemsetAsync(&w.ctr->n_big, 0, 4, s));
-                {
-                    BRA_PROF(P_BWT_HIST, s);
-                    hipLaunchKernelGGL(k_hist<MODE_RANK>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket, w.ctr,
-                                       w.key[0], w.key[1], w.pay[0], w.pay[1], w.tile_hist);
-                }
-                ScanArgs a{w.big[cur], nb,    w.tile_hist, w.tile_off, w.nomove, w.big[cur ^ 1], w.cap_big, w.jobs, w.cap_jobs,
-                           gnext,      w.cap_groups, w.ctr, RANK_KEYBYTES};
-                {
-                    BRA_PROF(P_BWT_SCAN, s);
-                    hipLaunchKernelGGL(k_scan<MODE_RANK>, dim3(std::min<uint32_t>(nb, 65535u)), dim3(TPB), 0, s, a);
-                }
-                {
-                    BRA_PROF(P_BWT_SCATTER, s);
-                    hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), tile_stage_bytes(), s, w.big[cur], w.nomove, w.tile_bucket, w.ctr,
-                                       w.tile_off, w.key[0], w.key[1], w.pay[0], w.pay[1], (uint32_t) MODE_RANK);
-                }
-                if (!read_ctr(w, s))
-                    return false;
-                nb = w.h_ctr->n_big;
-                cur ^= 1;
-            }
-        }
-        // equal-key big subgroups emitted by k_scan carry depth = gdepth; fix their depth and flush them
+        // sort the groups by rank key: MSD levels over the 4 key bytes; equal-key sub-buckets larger
+        // than a job become next-round groups directly (emitted with the parent's depth)
+        if (!run_levels<MODE_RANK>(w, d_in, d_blocks, w.h_ctr->n_big, 0, gnext, s))
+            return false;
         const uint32_t ng_big = w.h_ctr->n_groups;
         const uint32_t nj     = w.h_ctr->n_jobs;
         JobArgs jr{w.jobs, nj, d_in, d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi, w.isa, gnext, w.cap_groups,
-                   w.ctr, 0, hmin};
+                   w.ctr,  0,  hmin};
         if (ng_big)
             hipLaunchKernelGGL(k_rank_flush, dim3(std::min<uint32_t>(ng_big, 4096u)), dim3(256), 0, s, gnext, ng_big, d_blocks, w.pay[0],
                                w.pay[1], w.fsa, d_L, w.isa, d_pi);
         if (nj)
-            {
-                BRA_PROF(P_BWT_JOBS, s);
-                hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr);
-            }
+            hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr);
+        const uint32_t nmj = w.h_ctr->n_mjobs;
+        if (nmj)
+        {
+            JobArgs jm = jr;
+            jm.jobs    = w.mjobs;
+            jm.njobs   = nmj;
+            launch_mjobs<MODE_RANK>(w.mj_waves, nmj, jm, s);
+        }
         BRA_HIP_CHECK(hipGetLastError());
         if (!read_ctr(w, s))
             return false;
-        const uint32_t ng_new = w.h_ctr->n_groups;
-        // depth update for the big equal-key subgroups (they were emitted with the parent's depth)
-        if (ng_big)
+        uint32_t ng_new = w.h_ctr->n_groups;
+        // the big equal-key subgroups were emitted with the parent's depth: add the round's step,
+        // mark them flushed, drop groups of identical rotations (depth >= n) and find the new step
+        std::vector<Group> all(ng_new);
+        if (ng_new)
         {
-            std::vector<Group> tmpg(ng_big);
-            BRA_HIP_CHECK(hipMemcpyAsync(tmpg.data(), gnext, ng_big * sizeof(Group), hipMemcpyDeviceToHost, s));
+            BRA_HIP_CHECK(hipMemcpyAsync(all.data(), gnext, ng_new * sizeof(Group), hipMemcpyDeviceToHost, s));
             BRA_HIP_CHECK(hipStreamSynchronize(s));
-            for (auto& g : tmpg)
-            {
-                g.depth += hmin;
-                g.block |= (1u << 30);  // now flushed into fsa
-                g.block &= ~(1u << 31);
-            }
-            BRA_HIP_CHECK(hipMemcpyAsync(gnext, tmpg.data(), ng_big * sizeof(Group), hipMemcpyHostToDevice, s));
         }
-        const uint64_t members_new = w.h_ctr->g_members;
-        // no split in this round (same groups, same members) => the partition is final
-        const bool no_split = (ng_new == ng) && (members_new == members);
-        ng                  = ng_new;
-        members             = members_new;
-        // min depth of the new groups: the emitted depths already include hmin; recompute
-        uint32_t newmin = w.h_ctr->hmin;
-        if (ng_big)
-            newmin = std::min<uint32_t>(newmin, 0xFFFFFFFFu);
+        for (uint32_t i = 0; i < ng_big; ++i)
         {
-            // exact min over new groups (host side; the lists are small in practice)
-            std::vector<Group> all(ng);
-            if (ng)
-            {
-                BRA_HIP_CHECK(hipMemcpyAsync(all.data(), gnext, ng * sizeof(Group), hipMemcpyDeviceToHost, s));
-                BRA_HIP_CHECK(hipStreamSynchronize(s));
-            }
-            uint32_t m = 0xFFFFFFFFu;
-            std::vector<Group> keep;
-            keep.reserve(ng);
-            for (auto& g : all)
-            {
-                const uint32_t b = g.block & 0x3FFFFFFFu;
-                if (g.depth >= h_blocks[b].len)
-                    continue;  // identical rotations: final
-                m = std::min(m, g.depth);
-                keep.push_back(g);
-            }
-            if (keep.size() != all.size())
-            {
-                ng = (uint32_t) keep.size();
-                if (ng)
-                    BRA_HIP_CHECK(hipMemcpyAsync(gnext, keep.data(), ng * sizeof(Group), hipMemcpyHostToDevice, s));
-                members = 0;
-                for (auto& g : keep)
-                    members += g.len;
-            }
-            hmin = m;
+            all[i].depth += hmin;
+            all[i].block = (all[i].block & 0x3FFFFFFFu) | (1u << 30);
         }
+        std::vector<Group> keep;
+        keep.reserve(ng_new);
+        uint32_t m = 0xFFFFFFFFu;
+        for (auto& g : all)
+        {
+            if (g.depth >= h_blocks[g.block & 0x3FFFFFFFu].len)
+                continue;  // identical rotations: final
+            m = std::min(m, g.depth);
+            keep.push_back(g);
+        }
+        ng = (uint32_t) keep.size();
+        if (ng)
+            BRA_HIP_CHECK(hipMemcpyAsync(gnext, keep.data(), ng * sizeof(Group), hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));
+        hmin = m;
         gcur ^= 1;
-        if (no_split)
-            break;
+    }
+    // every group's depth grows by the round's minimum depth, so the minimum at least doubles per
+    // round: 64 rounds cover any block
+    if (ng > 0)
+    {
+        bra_hip_report("bwt: prefix doubling did not converge (%u groups left)", ng);
+        return false;
     }
     hipLaunchKernelGGL(k_pi_from_isa, dim3(std::min<uint32_t>(div_up(nblocks, 256), 1024u)), dim3(256), 0, s, d_blocks, w.flag, nblocks,
                        w.isa, d_pi);

@@ -103,7 +103,11 @@ def _encode_check(bra, codec, orc, data: np.ndarray, block_size: int, check_bloc
         blk = data[lo:hi].tobytes()
         ch = orc.encode_block(blk)
         pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
-        assert pi == ch.primary_index, ("pi", b)
+        if pi != ch.primary_index:
+            L = codec.stage_copy(0, total)[lo:hi]
+            ref_L = np.frombuffer(orc.bwt_encode(blk)[0], np.uint8)
+            nbad = int((L != ref_L).sum())
+            raise AssertionError(f"pi block {b}: gpu {pi} ref {ch.primary_index}; L mismatches {nbad}")
         assert lens == ch.lengths, ("lengths", b)
         assert (osz, esz) == (ch.orig_size, ch.encoded_size), ("sizes", b)
         assert int(off_h[b + 1] - off_h[b]) == esz, ("offset", b)
