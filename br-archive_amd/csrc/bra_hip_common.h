@@ -21,6 +21,15 @@
 // Error sink: forwards to the reference's bra_log_error when lib_bra is linked in, else stderr.
 void bra_hip_report(const char* fmt, ...);
 
+// Device-side range checks for debugging (make EXTRA=-DBRA_DEBUG): print the violation and let
+// the caller sanitise the value; compiled out otherwise.
+#ifdef BRA_DEBUG
+#define BRA_DCHECK(cond, ...)                           \
+    (__builtin_expect(!(cond), 0) ? (printf("[bra dcheck] %s:%d ", __FILE__, __LINE__), printf(__VA_ARGS__), printf("\n"), false) : true)
+#else
+#define BRA_DCHECK(cond, ...) true
+#endif
+
 namespace bra {
 
 constexpr int WAVE = 64;

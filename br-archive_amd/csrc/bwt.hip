@@ -35,7 +35,7 @@ constexpr int      TILE         = 4096;  // elements per tile (256 threads x 16)
 constexpr int      TPB          = 256;
 constexpr int      PER_THREAD   = TILE / TPB;
 constexpr uint32_t JOB_MAX      = 256;  // elements one wave sorts in registers
-constexpr int      MJ_WAVES_DEF = 8;    // waves of a workgroup job (4, 8 or 16; env BRA_MJ_WAVES)
+constexpr int      MJ_WAVES_DEF = 4;    // waves of a workgroup job (2, 4, 8 or 16; env BRA_MJ_WAVES)
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
@@ -71,22 +71,23 @@ struct Counters
     uint32_t n_jobs;        // wave jobs (<= JOB_MAX elements)
     uint32_t n_mjobs;       // workgroup jobs (<= mjob_max elements)
     uint32_t n_groups;      // fallback groups appended (next round)
-    uint32_t n_tiles;       // tiles of the current level
+    uint32_t pad0;
     uint32_t overflow;      // a work list overflowed (fatal)
     uint32_t g_members;     // members of appended fallback groups
     uint32_t hmin;          // min depth of appended fallback groups
-    uint32_t n_elems;       // elements in this level's big buckets (byte accounting)
+    uint32_t pad1;
     uint32_t n_moved;       // elements the level's scatter moves (byte accounting)
     uint32_t n_elems_next;
     uint32_t n_melems;      // elements in workgroup jobs (byte accounting)
     uint32_t pad;
 };
 
-// Start of an MSD level: the tiles reserved by the previous level become current.
+// Start of an MSD level.
+// Counters a level's kernels accumulate from zero.  Nothing reads a counter on the device in a
+// later kernel: the host passes the counts (the tile count of a level, say) as kernel arguments,
+// because a plain load in the next kernel can return a stale copy of an atomically updated line.
 __global__ void k_level_start(Counters* ctr)
 {
-    ctr->n_tiles      = ctr->n_tiles_next;
-    ctr->n_elems      = ctr->n_elems_next;
     ctr->n_tiles_next = 0;
     ctr->n_elems_next = 0;
     ctr->n_big        = 0;
@@ -139,10 +140,9 @@ __global__ void __launch_bounds__(TPB) k_hist(const uint8_t* __restrict__ in, co
                                               const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
                                               const Counters* __restrict__ ctr, uint64_t* __restrict__ key0, uint64_t* __restrict__ key1,
                                               const uint32_t* __restrict__ pay0, const uint32_t* __restrict__ pay1,
-                                              uint32_t* __restrict__ tile_hist)
+                                              uint32_t* __restrict__ tile_hist, uint32_t ntiles)
 {
     __shared__ uint32_t h[256];
-    const uint32_t      ntiles = ctr->n_tiles;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         h[threadIdx.x] = 0;
@@ -161,8 +161,10 @@ __global__ void __launch_bounds__(TPB) k_hist(const uint8_t* __restrict__ in, co
             uint64_t     k;
             if (rekey)
             {
-                const uint32_t idx = pay[s] & 0xFFFFFFu;
-                uint32_t       st  = idx + (B.d % BD.len);
+                uint32_t idx = pay[s] & 0xFFFFFFu;
+                if (!BRA_DCHECK(idx < BD.len && s >= BD.off && s < BD.off + BD.len, "hist idx %u n %u slot %llu", idx, BD.len, (unsigned long long) s))
+                    idx = 0;
+                uint32_t st = idx + (B.d % BD.len);
                 if (st >= BD.len)
                     st -= BD.len;
                 k      = load_key8(in + BD.off, BD.len, st);
@@ -183,6 +185,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const uint8_t* __restrict__ in, co
 // -------------------------------------------------------------------------------------------------
 struct ScanArgs
 {
+    const BlockDesc* blocks;
     const Bucket*   buckets;
     uint32_t        nbuckets;
     const uint32_t* tile_hist;
@@ -243,7 +246,15 @@ __global__ void __launch_bounds__(TPB) k_scan(ScanArgs a)
     const uint32_t      dg = threadIdx.x;
     for (uint32_t bi = blockIdx.x; bi < a.nbuckets; bi += gridDim.x)
     {
-        const Bucket   B      = a.buckets[bi];
+        const Bucket B = a.buckets[bi];
+#ifdef BRA_DEBUG
+        if (dg == 0)
+        {
+            const BlockDesc BD = a.blocks[B.block];
+            BRA_DCHECK(B.start >= BD.off && B.start + B.len <= BD.off + BD.len, "scan bucket %u start %u len %u block %u off %llu blen %u d %u",
+                       bi, B.start, B.len, B.block, (unsigned long long) BD.off, BD.len, B.d);
+        }
+#endif
         const uint32_t ntiles = div_up(B.len, TILE);
         const uint32_t* th    = a.tile_hist + (size_t) B.tile0 * 256 + dg;
         uint32_t       tot    = 0;
@@ -406,7 +417,7 @@ struct TileStage
 // Writes the staged tile (already in TileStage.key/pay, count `cnt`, digit base `base`) to global.
 __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k)[PER_THREAD], const uint32_t (&v)[PER_THREAD],
                                                 const uint32_t (&dgt)[PER_THREAD], uint32_t cnt, uint32_t d, uint32_t kd,
-                                                uint64_t* __restrict__ okey, uint32_t* __restrict__ opay)
+                                                uint64_t* __restrict__ okey, uint32_t* __restrict__ opay, uint64_t lo, uint64_t hi)
 {
     uint32_t rank[PER_THREAD];
 #pragma unroll
@@ -441,8 +452,12 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
             const uint64_t kk   = S.key[q];
             const uint32_t dd   = key_digit(kk, d, kd);
             const uint32_t slot = S.goff[dd] + (q - S.base[dd]);
-            okey[slot]          = kk;
-            opay[slot]          = S.pay[q];
+            if (BRA_DCHECK(slot >= lo && slot < hi, "scatter slot %u outside [%llu, %llu) digit %u", slot, (unsigned long long) lo,
+                           (unsigned long long) hi, dd))
+            {
+                okey[slot] = kk;
+                opay[slot] = S.pay[q];
+            }
         }
     }
 }
@@ -490,7 +505,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                 dg[i] = (uint32_t) (kk >> 56);
             }
         }
-        stage_and_write(S, k, v, dg, cnt, 0, 0, okey, opay);
+        stage_and_write(S, k, v, dg, cnt, 0, 0, okey, opay, B.off, B.off + B.len);
         __syncthreads();
     }
 }
@@ -499,11 +514,10 @@ __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buck
                                                  const uint32_t* __restrict__ tile_bucket, const Counters* __restrict__ ctr,
                                                  const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ key0,
                                                  uint64_t* __restrict__ key1, uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1,
-                                                 uint32_t mode)
+                                                 uint32_t mode, uint32_t ntiles)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStage&     S      = *reinterpret_cast<TileStage*>(smem);
-    const uint32_t ntiles = ctr->n_tiles;
+    TileStage& S = *reinterpret_cast<TileStage*>(smem);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const uint32_t bi = tile_bucket[t];
@@ -511,7 +525,9 @@ __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buck
             continue;  // uniform per workgroup
         const Bucket    B     = buckets[bi];
         const uint32_t  first = (t - B.tile0) * TILE;
-        const uint32_t  cnt   = min((uint32_t) TILE, B.len - first);
+        uint32_t        cnt   = min((uint32_t) TILE, B.len - first);
+        if (!BRA_DCHECK(t >= B.tile0 && first < B.len && B.buf < 2, "scatter tile %u bucket %u tile0 %u len %u buf %u", t, bi, B.tile0, B.len, B.buf))
+            cnt = 0;
         const uint32_t  kd    = (mode == MODE_STRING && B.d - B.kd >= 8) ? B.d : B.kd;
         const uint64_t* ik    = B.buf ? key1 : key0;
         const uint32_t* ip    = B.buf ? pay1 : pay0;
@@ -534,7 +550,7 @@ __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buck
                 dg[i]          = key_digit(k[i], B.d, kd);
             }
         }
-        stage_and_write(S, k, v, dg, cnt, B.d, kd, ok, op);
+        stage_and_write(S, k, v, dg, cnt, B.d, kd, ok, op, B.start, (uint64_t) B.start + B.len);
         __syncthreads();
     }
 }
@@ -861,6 +877,9 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     bool               tied[4];
     uint32_t           T     = J.len;
     uint32_t           depth = (MODE == MODE_STRING) ? J.d : J.gdepth;
+    if (!BRA_DCHECK(T <= 256u * W && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job mode %u W %d start %u len %u block %u off %llu blen %u",
+                    MODE, W, J.start, T, J.block, (unsigned long long) BD.off, BD.len))
+        T = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -869,6 +888,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         if (c < T)
         {
             v[r] = V[J.start + c];
+            if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (mode %u buf %u slot %u)", v[r] & 0xFFFFFFu, BD.len, MODE, J.buf, J.start + c))
+                v[r] = 0;
             if (MODE == MODE_RANK)
             {
                 kh[r] = K[J.start + c];
@@ -1065,7 +1086,11 @@ __global__ void k_isa_init(const BlockDesc* __restrict__ blocks, const uint8_t* 
             continue;
         const BlockDesc B = blocks[b];
         for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < B.len; j += gridDim.x * blockDim.x)
-            isa[B.off + fsa[B.off + j]] = j;
+        {
+            const uint32_t f = fsa[B.off + j];
+            if (BRA_DCHECK(f < B.len, "isa_init fsa %u n %u block %u j %u", f, B.len, b, j))
+                isa[B.off + f] = j;
+        }
     }
 }
 
@@ -1078,7 +1103,12 @@ __global__ void k_group_mark(const Group* __restrict__ groups, uint32_t ng, cons
         const uint32_t  b  = G.block & 0x3FFFFFFFu;
         const BlockDesc BD = blocks[b];
         for (uint32_t i = threadIdx.x; i < G.len; i += blockDim.x)
-            isa[BD.off + fsa[G.start + i]] = G.start - (uint32_t) BD.off;
+        {
+            const uint32_t f = fsa[G.start + i];
+            if (BRA_DCHECK(f < BD.len && G.start >= BD.off && G.start + G.len <= BD.off + BD.len, "group_mark fsa %u n %u start %u len %u", f,
+                           BD.len, G.start, G.len))
+                isa[BD.off + f] = G.start - (uint32_t) BD.off;
+        }
         if (threadIdx.x == 0)
             flag[b] = 1;
     }
@@ -1097,8 +1127,10 @@ __global__ void k_rank_keys(const Group* __restrict__ groups, uint32_t ng, const
         for (uint32_t i = threadIdx.x; i < G.len; i += blockDim.x)
         {
             const uint32_t s   = G.start + i;
-            const uint32_t idx = fsa[s];
-            uint32_t       q   = idx + h;
+            uint32_t       idx = fsa[s];
+            if (!BRA_DCHECK(idx < BD.len && s >= BD.off && s < BD.off + BD.len, "rank_keys idx %u n %u slot %u", idx, BD.len, s))
+                idx = 0;
+            uint32_t q = idx + h;
             if (q >= BD.len)
                 q -= BD.len;
             const uint32_t rk = isa[BD.off + q];
@@ -1228,8 +1260,10 @@ static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
         hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>), s, a);
     else if (waves == 8)
         hipLaunchKernelGGL((k_mjobs<MODE, 8>), g, dim3(64 * 8), sizeof(JobLds<8>), s, a);
-    else
+    else if (waves == 4)
         hipLaunchKernelGGL((k_mjobs<MODE, 4>), g, dim3(64 * 4), sizeof(JobLds<4>), s, a);
+    else
+        hipLaunchKernelGGL((k_mjobs<MODE, 2>), g, dim3(64 * 2), sizeof(JobLds<2>), s, a);
 }
 
 static void ws_free(BwtWorkspace& w)
@@ -1269,10 +1303,10 @@ void          bwt_workspace_destroy(BwtWorkspace* w)
 
 static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
 {
-    if (const char* e = getenv("BRA_MJ_WAVES"))  // tuning knob: 0 (off), 4, 8 or 16 waves per workgroup job
+    if (const char* e = getenv("BRA_MJ_WAVES"))  // tuning knob: 0 (off), 2, 4, 8 or 16 waves per workgroup job
     {
         const int v = atoi(e);
-        w.mj_waves  = (v == 0 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
+        w.mj_waves  = (v == 0 || v == 2 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
     }
     if (n <= w.cap_n && nblocks <= w.cap_blocks)
         return true;
@@ -1336,9 +1370,10 @@ static size_t tile_stage_bytes() { return sizeof(TileStage); }
 // MSD levels for the buckets in w.big[cur] (tiles already reserved in w.tile_bucket[cur] and
 // ctr->n_tiles_next).  Sub-buckets become jobs / fallback groups (appended to the queues).
 template <uint32_t MODE>
-static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, uint32_t nbig, int cur, Group* groups_out,
-                       hipStream_t s)
+static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, uint32_t nbig, uint32_t ntiles, int cur,
+                       Group* groups_out, hipStream_t s)
 {
+    uint32_t nelems = w.h_ctr->n_elems_next;
     const size_t lds  = tile_stage_bytes();
     const int    grid = w.grid;
     while (nbig > 0)
@@ -1347,9 +1382,9 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         {
             BRA_PROF(P_BWT_HIST, s);
             hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket[cur], w.ctr, w.key[0],
-                               w.key[1], w.pay[0], w.pay[1], w.tile_hist);
+                               w.key[1], w.pay[0], w.pay[1], w.tile_hist, ntiles);
         }
-        ScanArgs a{w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
+        ScanArgs a{d_blocks, w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
                    w.cap_big,   w.tile_bucket[cur ^ 1],   w.cap_tiles, w.jobs,       w.cap_jobs,
                    w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
                    (uint32_t) (g_prof != nullptr), w.mjob_max()};
@@ -1360,17 +1395,19 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         {
             BRA_PROF(P_BWT_SCATTER, s);
             hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
-                               w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
+                               w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles);
         }
         BRA_HIP_CHECK(hipGetLastError());
         if (!read_ctr(w, s))
             return false;
         // algorithmic bytes: keys read by the histogram, tile histograms, KV moved by the scatter
-        const double nt = w.h_ctr->n_tiles, ne = w.h_ctr->n_elems, nm = w.h_ctr->n_moved;
+        const double nt = ntiles, ne = nelems, nm = w.h_ctr->n_moved;
+        nelems          = w.h_ctr->n_elems_next;
         prof_bytes(P_BWT_HIST, 8.0 * ne + 1024.0 * nt);
         prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * nbig);
         prof_bytes(P_BWT_SCATTER, 24.0 * nm + 1024.0 * nt);
-        nbig = w.h_ctr->n_big;
+        nbig   = w.h_ctr->n_big;
+        ntiles = w.h_ctr->n_tiles_next;
         cur ^= 1;
     }
     return true;
@@ -1397,6 +1434,25 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     if (!ws_reserve(w, N, nblocks))
         return false;
+#ifdef BRA_DEBUG
+    // poison every work buffer so that a read of anything this call did not write shows up
+    for (int i = 0; i < 2; ++i)
+    {
+        BRA_HIP_CHECK(hipMemsetAsync(w.key[i], 0xA5, N * 8, s));
+        BRA_HIP_CHECK(hipMemsetAsync(w.pay[i], 0xA5, N * 4, s));
+        BRA_HIP_CHECK(hipMemsetAsync(w.big[i], 0xA5, (size_t) w.cap_big * sizeof(Bucket), s));
+        BRA_HIP_CHECK(hipMemsetAsync(w.groups[i], 0xA5, (size_t) w.cap_groups * sizeof(Group), s));
+        BRA_HIP_CHECK(hipMemsetAsync(w.tile_bucket[i], 0xA5, (size_t) w.cap_tiles * 4, s));
+    }
+    BRA_HIP_CHECK(hipMemsetAsync(w.fsa, 0xA5, N * 4, s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.isa, 0xA5, N * 4, s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.jobs, 0xA5, (size_t) w.cap_jobs * sizeof(Job), s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.mjobs, 0xA5, (size_t) w.cap_mjobs * sizeof(Job), s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.nomove, 0xA5, std::max<uint32_t>(w.cap_big, nblocks), s));
+    BRA_HIP_CHECK(hipMemsetAsync(d_L, 0xA5, N, s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.tile_hist, 0xA5, (size_t) std::max(w.cap_tiles, w.cap_l0) * 256 * 4, s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.tile_off, 0xA5, (size_t) std::max(w.cap_tiles, w.cap_l0) * 256 * 4, s));
+#endif
     static bool attr_set = false;
     if (!attr_set)
     {
@@ -1430,7 +1486,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         BRA_PROF(P_BWT_L0HIST, s);
         hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist);
     }
-    ScanArgs a0{w.big[1],  nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
+    ScanArgs a0{d_blocks, w.big[1],  nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max()};
     {
@@ -1449,7 +1505,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
     prof_bytes(P_BWT_L0SCATTER, 13.0 * N + 1024.0 * nt0);
     // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]
-    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, 0, w.groups[0], s))
+    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, w.h_ctr->n_tiles_next, 0, w.groups[0], s))
         return false;
 
     // ---- wave jobs ----
@@ -1505,7 +1561,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         Group* gnext = w.groups[gcur ^ 1];
         // sort the groups by rank key: MSD levels over the 4 key bytes; equal-key sub-buckets larger
         // than a job become next-round groups directly (emitted with the parent's depth)
-        if (!run_levels<MODE_RANK>(w, d_in, d_blocks, w.h_ctr->n_big, 0, gnext, s))
+        if (!run_levels<MODE_RANK>(w, d_in, d_blocks, w.h_ctr->n_big, w.h_ctr->n_tiles_next, 0, gnext, s))
             return false;
         const uint32_t ng_big = w.h_ctr->n_groups;
         const uint32_t nj     = w.h_ctr->n_jobs;

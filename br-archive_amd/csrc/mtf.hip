@@ -100,6 +100,101 @@ __device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st,
     tbl[lane * TPB + owner] = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
 }
 
+// One MTF step on a table whose first RK dwords (4 entries each, entry 0 = low byte) live in
+// registers and the rest in LDS (tbl[w * TPB], w >= RK).  Returns the symbol's position.
+template <int RK>
+__device__ __forceinline__ uint32_t mtf_step(uint32_t (&R)[RK], uint32_t* tbl, uint32_t c)
+{
+    const uint32_t cc = c * 0x01010101u;
+    uint32_t       w = 0, z = 0;
+    bool           hit = false;
+#pragma unroll
+    for (int k = 0; k < RK; ++k)
+    {
+        const uint32_t zk = haszero8(R[k] ^ cc);
+        if (!hit && zk)
+        {
+            hit = true;
+            w   = k;
+            z   = zk;
+        }
+    }
+    uint32_t b;
+    if (hit)
+    {
+        b                   = (uint32_t) __builtin_ctz(z) >> 3;
+        const uint32_t keep = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
+#pragma unroll
+        for (int k = RK - 1; k >= 0; --k)
+        {
+            const uint32_t below   = k ? R[k - 1] : c << 24;
+            const uint32_t shifted = (R[k] << 8) | (below >> 24);
+            if ((uint32_t) k < w)
+                R[k] = shifted;
+            else if ((uint32_t) k == w)
+                R[k] = (R[k] & keep) | (shifted & ~keep);
+        }
+        return w * 4 + b;
+    }
+    uint32_t cur = 0;
+    for (w = RK; w < 64; ++w)  // always found: the table is a permutation of 0..255
+    {
+        cur = tbl[w * TPB];
+        z   = haszero8(cur ^ cc);
+        if (z)
+            break;
+    }
+    b                   = (uint32_t) __builtin_ctz(z) >> 3;
+    const uint32_t keep = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
+    uint32_t       below = (w > RK) ? tbl[(w - 1) * TPB] : R[RK - 1];
+    tbl[w * TPB]         = (cur & keep) | (((cur << 8) | (below >> 24)) & ~keep);
+    for (uint32_t x = w - 1; x >= RK; --x)
+    {
+        const uint32_t lo = (x > RK) ? tbl[(x - 1) * TPB] : R[RK - 1];
+        tbl[x * TPB]      = (below << 8) | (lo >> 24);
+        below             = lo;
+    }
+#pragma unroll
+    for (int k = RK - 1; k >= 0; --k)
+        R[k] = (R[k] << 8) | ((k ? R[k - 1] : c << 24) >> 24);
+    return w * 4 + b;
+}
+
+// Sequential MTF of one segment on this thread's table (tbl = its column).  Input is read and
+// output written 16 bytes at a time (the next 16 input bytes are loaded before the current ones
+// are coded) whenever the segment is 16-byte aligned; the ragged tail goes byte by byte.
+__device__ __forceinline__ void mtf_encode_segment(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece P, uint32_t* tbl)
+{
+    constexpr int  RK  = 2;
+    const uint8_t* src = in + P.off;
+    uint8_t*       dst = out + P.off;
+    uint32_t       R[RK];
+#pragma unroll
+    for (int k = 0; k < RK; ++k)
+        R[k] = tbl[k * TPB];
+    uint32_t i = 0;
+    if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0 && P.len >= 16)
+    {
+        const uint32_t nv  = P.len / 16;
+        uint4          nxt = reinterpret_cast<const uint4*>(src)[0];
+        for (uint32_t v = 0; v < nv; ++v)
+        {
+            const uint4 cur = nxt;
+            if (v + 1 < nv)
+                nxt = reinterpret_cast<const uint4*>(src)[v + 1];
+            const uint32_t iw[4] = {cur.x, cur.y, cur.z, cur.w};
+            uint32_t       ow[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                ow[j >> 2] |= mtf_step<RK>(R, tbl, (iw[j >> 2] >> (8 * (j & 3))) & 0xFF) << (8 * (j & 3));
+            reinterpret_cast<uint4*>(dst)[v] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+        i = nv * 16;
+    }
+    for (; i < P.len; ++i)
+        dst[i] = (uint8_t) mtf_step<RK>(R, tbl, src[i]);
+}
+
 __global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
                                                     uint32_t nseg, const int32_t* __restrict__ state)
 {
@@ -124,43 +219,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ 
         __syncthreads();
         const uint32_t s = g0 + t;
         if (s < nseg)
-        {
-            const Piece    P   = segs[s];
-            const uint8_t* src = in + P.off;
-            uint8_t*       dst = out + P.off;
-            for (uint32_t i = 0; i < P.len; ++i)
-            {
-                const uint32_t c  = src[i];
-                const uint32_t cc = c * 0x01010101u;
-                uint32_t       w = 0, z = 0;
-                uint32_t       cur = 0;
-                for (; w < 64; ++w)  // always found: the table is a permutation of 0..255
-                {
-                    cur = tbl[w * TPB + t];
-                    z   = haszero8(cur ^ cc);
-                    if (z)
-                        break;
-                }
-                if (w == 64)
-                    break;
-                const uint32_t b = (uint32_t) __builtin_ctz(z) >> 3;
-                dst[i]           = (uint8_t) (w * 4 + b);
-                // move to front: entries [0, p) shift up by one, entry 0 = c
-                {
-                    const uint32_t below   = w ? tbl[(w - 1) * TPB + t] : c << 24;
-                    const uint32_t shifted = (cur << 8) | (below >> 24);
-                    const uint32_t keep    = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
-                    tbl[w * TPB + t]       = (cur & keep) | (shifted & ~keep);
-                    uint32_t hi            = below;
-                    for (int x = (int) w - 1; x >= 0; --x)
-                    {
-                        const uint32_t lo  = x ? tbl[(x - 1) * TPB + t] : c << 24;
-                        tbl[x * TPB + t]   = (hi << 8) | (lo >> 24);
-                        hi                 = lo;
-                    }
-                }
-            }
-        }
+            mtf_encode_segment(in, out, segs[s], tbl + t);
         __syncthreads();
     }
 }

@@ -169,6 +169,17 @@ __device__ __forceinline__ void load16(const uint8_t* p, uint32_t cnt, uint32_t 
     }
 }
 
+// All per-thread loops below are fully unrolled over the PT positions (static register indices);
+// positions >= n (tile end) are masked.
+__device__ __forceinline__ uint32_t sel(const uint8_t (&x)[PT], uint32_t i)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < PT; ++j)
+        r = ((uint32_t) j == i) ? x[j] : r;
+    return r;
+}
+
 __device__ __forceinline__ RunSum thread_runsum(const uint8_t (&x)[PT], uint32_t n)
 {
     RunSum s;
@@ -181,77 +192,96 @@ __device__ __forceinline__ RunSum thread_runsum(const uint8_t (&x)[PT], uint32_t
         s.all            = 1;
         return s;
     }
-    s.first    = x[0];
-    s.last     = x[n - 1];
-    uint32_t p = 1;
-    while (p < n && x[p] == x[0])
-        ++p;
-    s.pre      = p;
-    uint32_t q = 1;
-    while (q < n && x[n - 1 - q] == x[n - 1])
-        ++q;
-    s.suf = q;
-    s.all = (p == n);
+    const uint32_t last = sel(x, n - 1);
+    uint32_t       p = 1, q = 1;
+    bool           pr = true, qr = true;
+#pragma unroll
+    for (int i = 1; i < PT; ++i)
+    {
+        pr = pr && (uint32_t) i < n && x[i] == x[0];
+        p += pr ? 1 : 0;
+    }
+    // backwards from n-1: position n-1-j for j = 1..
+#pragma unroll
+    for (int i = PT - 2; i >= 0; --i)
+    {
+        const bool in = (uint32_t) i < n - 1;  // strictly before the last position
+        // walk i = n-2, n-3, ... : positions above n-2 are skipped (not yet in the run walk)
+        if (in)
+        {
+            qr = qr && x[i] == last;
+            q += qr ? 1 : 0;
+        }
+    }
+    s.first = x[0];
+    s.last  = (uint8_t) last;
+    s.pre   = p;
+    s.suf   = q;
+    s.all   = (p == n);
     return s;
 }
 
 // Per-position classification.  kind: 0 literal, 1 run-block start, 2 run continuation.
-// For run-block starts clen = block length.
+// For run-block starts clen = block length.  `left` / `right`: run extension into this thread's
+// positions from before / after them (same byte as x[0] / x[n-1]).
 __device__ __forceinline__ void classify(const uint8_t (&x)[PT], uint32_t n, uint32_t left, uint32_t right, uint8_t (&kind)[PT],
                                          uint8_t (&clen)[PT])
 {
-    uint32_t i0 = 0;
-    while (i0 < n)
+    uint32_t k[PT];  // position inside its maximal run
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+        k[i] = (i == 0) ? left : (x[i] == x[i - 1] ? k[i - 1] + 1 : 0);
+    uint32_t nxt = 0;
+#pragma unroll
+    for (int i = PT - 1; i >= 0; --i)
     {
-        uint32_t i1 = i0 + 1;
-        while (i1 < n && x[i1] == x[i0])
-            ++i1;
-        const uint32_t k0   = (i0 == 0) ? left : 0;
-        const uint32_t L    = k0 + (i1 - i0) + (i1 == n ? right : 0);
-        const uint32_t full = L >> 7, r = L & 127;
-        for (uint32_t i = i0; i < i1; ++i)
+        uint32_t r;  // positions from i to the end of its run, inclusive
+        if ((uint32_t) i >= n)
+            r = 0;
+        else if ((uint32_t) i == n - 1)
+            r = 1 + right;
+        else
+            r = (x[i] == x[i + 1]) ? nxt + 1 : 1;
+        nxt                 = r;
+        const uint32_t L    = k[i] + r;
+        const uint32_t full = L >> 7, rm = L & 127, q = k[i] >> 7;
+        uint8_t        kd = 0, cl = 0;
+        if (L >= 3)
         {
-            const uint32_t k = k0 + (i - i0);
-            if (L < 3)
-            {
-                kind[i] = 0;
-                continue;
-            }
-            const uint32_t q = k >> 7;
             if (q < full)
             {
-                kind[i] = (k & 127) == 0 ? 1 : 2;
-                clen[i] = 128;
+                kd = (k[i] & 127) == 0 ? 1 : 2;
+                cl = 128;
             }
-            else if (r >= 3)
+            else if (rm >= 3)
             {
-                kind[i] = (k == (full << 7)) ? 1 : 2;
-                clen[i] = (uint8_t) r;
+                kd = (k[i] == (full << 7)) ? 1 : 2;
+                cl = (uint8_t) rm;
             }
-            else
-                kind[i] = 0;
         }
-        i0 = i1;
+        kind[i] = kd;
+        clen[i] = cl;
     }
 }
 
 __device__ __forceinline__ GapSum thread_gapsum(const uint8_t (&kind)[PT], uint32_t n)
 {
-    GapSum g{n, 0, 0, 0};
-    uint32_t i = 0;
-    while (i < n && kind[i] == 0)
-        ++i;
-    g.lead = i;
-    if (i == n)
+    GapSum   g{n, 0, 0, 0};
+    bool     lead = true;
+    uint32_t trail = 0;
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
     {
-        g.trail = n;
-        return g;
+        if ((uint32_t) i < n)
+        {
+            const bool lit = kind[i] == 0;
+            lead           = lead && lit;
+            g.lead += lead ? 1 : 0;
+            g.has |= lit ? 0u : 1u;
+            trail = lit ? trail + 1 : 0;
+        }
     }
-    g.has      = 1;
-    uint32_t j = n;
-    while (j > 0 && kind[j - 1] == 0)
-        --j;
-    g.trail = n - j;
+    g.trail = trail;
     return g;
 }
 
@@ -326,7 +356,7 @@ __device__ __forceinline__ void tile_classify(const uint8_t* __restrict__ in, co
     if (threadIdx.x == 0)
         edge[0] = v.x[0];
     if (base < P.len && base + v.n == P.len)
-        edge[1] = v.x[v.n - 1];
+        edge[1] = (uint8_t) sel(v.x, v.n - 1);
     __syncthreads();
     RunSum sl{L.left, L.left, L.left, edge[0], edge[0], 1, 0};
     RunSum sr{L.right, L.right, L.right, edge[1], edge[1], 1, 0};
@@ -334,36 +364,41 @@ __device__ __forceinline__ void tile_classify(const uint8_t* __restrict__ in, co
     RunSum E    = block_scan_fwd(s, sl, sl, lds, comb, shfl_run);
     RunSum F    = block_scan_bwd(s, sr, lds, comb, shfl_run);
     uint32_t left  = (v.n && E.len && E.last == v.x[0]) ? E.suf : 0;
-    uint32_t right = (v.n && F.len && F.first == v.x[v.n - 1]) ? F.pre : 0;
+    uint32_t right = (v.n && F.len && F.first == sel(v.x, v.n - 1)) ? F.pre : 0;
     classify(v.x, v.n, left, right, v.kind, v.clen);
 }
 
 // Output bytes of this thread's positions given the gap offset of its first position (go0) and
 // the literal count following its last position (rem_after).  Optionally writes them to `stage`.
+template <bool WRITE>
 __device__ __forceinline__ uint32_t emit_thread(const TileView& v, uint32_t go0, uint32_t rem_after, uint8_t* stage, uint32_t pos)
 {
     // remaining literals from position i to the gap end (inclusive), computed backwards
     uint32_t rem[PT];
     uint32_t run = rem_after;
-    for (int i = (int) v.n - 1; i >= 0; --i)
+#pragma unroll
+    for (int i = PT - 1; i >= 0; --i)
     {
-        run    = (v.kind[i] == 0) ? run + 1 : 0;
+        if ((uint32_t) i < v.n)
+            run = (v.kind[i] == 0) ? run + 1 : 0;
         rem[i] = run;
     }
     uint32_t go = go0, bytes = 0;
-    for (uint32_t i = 0; i < v.n; ++i)
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
     {
+        if ((uint32_t) i >= v.n)
+            continue;
         if (v.kind[i] == 0)
         {
-            if ((go & 127) == 0)
+            const bool ctl = (go & 127) == 0;
+            if (WRITE)
             {
-                if (stage)
+                if (ctl)
                     stage[pos + bytes] = (uint8_t) (min(rem[i], 128u) - 1);
-                ++bytes;
+                stage[pos + bytes + (ctl ? 1 : 0)] = v.x[i];
             }
-            if (stage)
-                stage[pos + bytes] = v.x[i];
-            ++bytes;
+            bytes += ctl ? 2 : 1;
             ++go;
         }
         else
@@ -371,7 +406,7 @@ __device__ __forceinline__ uint32_t emit_thread(const TileView& v, uint32_t go0,
             go = 0;
             if (v.kind[i] == 1)
             {
-                if (stage)
+                if (WRITE)
                 {
                     stage[pos + bytes]     = (uint8_t) (int8_t) (1 - (int) v.clen[i]);
                     stage[pos + bytes + 1] = v.x[i];
@@ -399,7 +434,7 @@ __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ i
         const GapSum z{0, 0, 0, 0};
         const GapSum E = block_scan_fwd(gs, z, z, glds, comb, shfl_gap);
         const GapSum F = block_scan_bwd(gs, z, glds, comb, shfl_gap);
-        const uint32_t bytes = emit_thread(v, E.trail, F.lead, nullptr, 0);
+        const uint32_t bytes = emit_thread<false>(v, E.trail, F.lead, nullptr, 0);
         uint32_t       total;
         block256_exclusive_sum(bytes, tmp, &total);
         if (threadIdx.x == TPB - 1)
@@ -464,10 +499,10 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
         const GapSum sr{O.rem_after, O.rem_after, O.rem_after, 0};
         const GapSum E     = block_scan_fwd(gs, sl, z, glds, comb, shfl_gap);
         const GapSum F     = block_scan_bwd(gs, sr, glds, comb, shfl_gap);
-        const uint32_t by  = emit_thread(v, E.trail, F.lead, nullptr, 0);
+        const uint32_t by  = emit_thread<false>(v, E.trail, F.lead, nullptr, 0);
         uint32_t       total;
         const uint32_t pos = block256_exclusive_sum(by, tmp, &total);
-        emit_thread(v, E.trail, F.lead, stage, pos);
+        emit_thread<true>(v, E.trail, F.lead, stage, pos);
         __syncthreads();
         uint8_t* dst = out + rle_base[P.block] + O.out_off;
         for (uint32_t i = threadIdx.x; i < total; i += TPB)
