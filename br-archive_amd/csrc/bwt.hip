@@ -585,8 +585,29 @@ struct JobArgs
     uint32_t         cap_groups;
     Counters*        ctr;
     uint32_t         dcap;
-    uint32_t         hstep;  // RANK mode: depth added to a subgroup (min depth of the round)
+    uint32_t         hstep;    // RANK mode: depth added to a subgroup (min depth of the round)
+    uint32_t         xcd_major;  // jobs ordered by job_order(): XCD x works on jobs [xseg[x], xseg[x+1])
+    uint32_t         xseg[9];
 };
+
+// Job index ranges per workgroup.  With xcd_major, workgroup w runs on XCD w % 8 (the dispatcher's
+// round-robin; only speed depends on it) and walks that XCD's list, where the jobs of the blocks
+// b = x (mod 8) are stored in block order: the workgroups of one XCD then gather from the same one
+// or two blocks at a time, which stay resident in that XCD's 4 MiB L2.
+struct JobRange
+{
+    uint32_t first, end, step;
+};
+
+__device__ __forceinline__ JobRange job_range(const JobArgs& a, uint32_t unit, uint32_t units_per_wg)
+{
+    if (a.xcd_major)
+    {
+        const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, g = gridDim.x >> 3;
+        return JobRange{a.xseg[x] + l * units_per_wg + unit, a.xseg[x + 1], g * units_per_wg};
+    }
+    return JobRange{blockIdx.x * units_per_wg + unit, a.njobs, gridDim.x * units_per_wg};
+}
 
 template <int W>
 struct JobLds
@@ -1039,10 +1060,9 @@ template <uint32_t MODE>
 __global__ void __launch_bounds__(256) k_jobs(JobArgs a)
 {
     __shared__ JobLds<1> lds[4];
-    const int      wl     = threadIdx.x >> 6;
-    const uint32_t wid    = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t j = wid; j < a.njobs; j += nwaves)
+    const int      wl = threadIdx.x >> 6;
+    const JobRange R  = job_range(a, wl, 4);
+    for (uint32_t j = R.first; j < R.end; j += R.step)
         job_run<MODE, 1>(a, a.jobs[j], lds[wl], 0);
 }
 
@@ -1050,11 +1070,30 @@ template <uint32_t MODE, int W>
 __global__ void __launch_bounds__(64 * W) k_mjobs(JobArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    JobLds<W>& S = *reinterpret_cast<JobLds<W>*>(smem);
-    for (uint32_t j = blockIdx.x; j < a.njobs; j += gridDim.x)
+    JobLds<W>&     S = *reinterpret_cast<JobLds<W>*>(smem);
+    const JobRange R = job_range(a, 0, 1);
+    for (uint32_t j = R.first; j < R.end; j += R.step)
     {
         job_run<MODE, W>(a, a.jobs[j], S, threadIdx.x >> 6);
         __syncthreads();
+    }
+}
+
+// Block-major, XCD-major job order: key(b) = (b % 8) * kb + b / 8.
+__device__ __forceinline__ uint32_t job_key(uint32_t b, uint32_t kb) { return (b & 7u) * kb + (b >> 3); }
+
+__global__ void k_job_count(const Job* __restrict__ jobs, uint32_t n, uint32_t kb, uint32_t* __restrict__ cnt)
+{
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+        atomicAdd(&cnt[job_key(jobs[j].block, kb)], 1u);
+}
+
+__global__ void k_job_scatter(const Job* __restrict__ in, uint32_t n, uint32_t kb, uint32_t* __restrict__ cursor, Job* __restrict__ out)
+{
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    {
+        const Job J = in[j];
+        out[atomicAdd(&cursor[job_key(J.block, kb)], 1u)] = J;
     }
 }
 
@@ -1242,6 +1281,10 @@ struct BwtWorkspace
     Bucket*   big[2]         = {nullptr, nullptr};
     Job*      jobs           = nullptr;
     Job*      mjobs          = nullptr;
+    Job*      jobs_sorted    = nullptr;  // block-major, XCD-major copies (order_jobs)
+    Job*      mjobs_sorted   = nullptr;
+    uint32_t* job_cnt        = nullptr;  // 2 lists x 8 * ceil(blocks / 8) keys, then the cursors
+    uint32_t* h_job_cnt      = nullptr;  // pinned: counts back, cursors out
     Group*    groups[2]      = {nullptr, nullptr};
     Counters* ctr            = nullptr;
     Counters* h_ctr          = nullptr;  // pinned
@@ -1252,10 +1295,54 @@ struct BwtWorkspace
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
+// Reorder the wave-job and workgroup-job lists block-major per XCD (see job_range): count jobs per
+// key on the device, prefix on the host (the counts come back with one small copy), scatter.
+static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, JobArgs& ja, JobArgs& jm, hipStream_t s)
+{
+    const uint32_t kb = div_up(nblocks, 8), nk = 8 * kb;
+    const uint32_t n[2] = {ja.njobs, jm.njobs};
+    const Job*     src[2] = {w.jobs, w.mjobs};
+    Job*           dst[2] = {w.jobs_sorted, w.mjobs_sorted};
+    JobArgs*       args[2] = {&ja, &jm};
+    BRA_HIP_CHECK(hipMemsetAsync(w.job_cnt, 0, 2 * (size_t) nk * 4, s));
+    for (int l = 0; l < 2; ++l)
+        if (n[l])
+            hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb,
+                               w.job_cnt + (size_t) l * nk);
+    BRA_HIP_CHECK(hipMemcpyAsync(w.h_job_cnt, w.job_cnt, 2 * (size_t) nk * 4, hipMemcpyDeviceToHost, s));
+    BRA_HIP_CHECK(hipStreamSynchronize(s));
+    uint32_t* cur = w.h_job_cnt + 2 * (size_t) nk;  // cursors (exclusive prefix per list)
+    for (int l = 0; l < 2; ++l)
+    {
+        uint32_t run = 0;
+        for (uint32_t k = 0; k < nk; ++k)
+        {
+            if (k % kb == 0)
+                args[l]->xseg[k / kb] = run;
+            cur[(size_t) l * nk + k] = run;
+            run += w.h_job_cnt[(size_t) l * nk + k];
+        }
+        args[l]->xseg[8]   = run;
+        args[l]->xcd_major = 1;
+    }
+    BRA_HIP_CHECK(hipMemcpyAsync(w.job_cnt + 2 * (size_t) nk, cur, 2 * (size_t) nk * 4, hipMemcpyHostToDevice, s));
+    for (int l = 0; l < 2; ++l)
+        if (n[l])
+        {
+            hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb,
+                               w.job_cnt + 2 * (size_t) nk + (size_t) l * nk, dst[l]);
+            args[l]->jobs = dst[l];
+        }
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+static uint32_t round8(uint32_t g) { return (g + 7u) & ~7u; }
+
 template <uint32_t MODE>
 static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
 {
-    const dim3 g(std::min<uint32_t>(n, 2048u));
+    const dim3 g(round8(std::min<uint32_t>(n, 2048u)));
     if (waves == 16)
         hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>), s, a);
     else if (waves == 8)
@@ -1283,6 +1370,10 @@ static void ws_free(BwtWorkspace& w)
     (void) hipFree(w.nomove);
     (void) hipFree(w.flag);
     (void) hipFree(w.jobs);
+    (void) hipFree(w.jobs_sorted);
+    (void) hipFree(w.mjobs_sorted);
+    (void) hipFree(w.job_cnt);
+    (void) hipHostFree(w.h_job_cnt);
     (void) hipFree(w.mjobs);
     (void) hipFree(w.ctr);
     (void) hipFree(w.l0tiles);
@@ -1338,6 +1429,11 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     BRA_HIP_CHECK(hipMalloc(&w.flag, B));
     BRA_HIP_CHECK(hipMalloc(&w.jobs, (size_t) w.cap_jobs * sizeof(Job)));
     BRA_HIP_CHECK(hipMalloc(&w.mjobs, (size_t) w.cap_mjobs * sizeof(Job)));
+    BRA_HIP_CHECK(hipMalloc(&w.jobs_sorted, (size_t) w.cap_jobs * sizeof(Job)));
+    BRA_HIP_CHECK(hipMalloc(&w.mjobs_sorted, (size_t) w.cap_mjobs * sizeof(Job)));
+    const size_t nkeys = 8 * (size_t) div_up(B, 8);
+    BRA_HIP_CHECK(hipMalloc(&w.job_cnt, 4 * nkeys * 4));
+    BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 4 * nkeys * 4, hipHostMallocDefault));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
     BRA_HIP_CHECK(hipMalloc(&w.l0tiles, (size_t) w.cap_l0 * sizeof(L0Tile)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault));
@@ -1511,18 +1607,20 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     // ---- wave jobs ----
     const uint32_t njobs = w.h_ctr->n_jobs;
     JobArgs ja{w.jobs,  njobs,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
-               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0};
+               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}};
+    const uint32_t nmjobs = w.h_ctr->n_mjobs;
+    JobArgs        jm     = ja;
+    jm.jobs               = w.mjobs;
+    jm.njobs              = nmjobs;
+    if (!order_jobs(w, nblocks, ja, jm, s))
+        return false;
     if (njobs)
     {
         BRA_PROF(P_BWT_JOBS, s);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(std::min<uint32_t>(div_up(njobs, 4), 8192u)), dim3(256), 0, s, ja);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), 8192u))), dim3(256), 0, s, ja);
     }
-    const uint32_t nmjobs = w.h_ctr->n_mjobs;
     if (nmjobs)
     {
-        JobArgs jm = ja;
-        jm.jobs    = w.mjobs;
-        jm.njobs   = nmjobs;
         BRA_PROF(P_BWT_MJOBS, s);
         launch_mjobs<MODE_STRING>(w.mj_waves, nmjobs, jm, s);
     }
@@ -1566,7 +1664,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         const uint32_t ng_big = w.h_ctr->n_groups;
         const uint32_t nj     = w.h_ctr->n_jobs;
         JobArgs jr{w.jobs, nj, d_in, d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi, w.isa, gnext, w.cap_groups,
-                   w.ctr,  0,  hmin};
+                   w.ctr,  0,  hmin, 0, {}};
         if (ng_big)
             hipLaunchKernelGGL(k_rank_flush, dim3(std::min<uint32_t>(ng_big, 4096u)), dim3(256), 0, s, gnext, ng_big, d_blocks, w.pay[0],
                                w.pay[1], w.fsa, d_L, w.isa, d_pi);
