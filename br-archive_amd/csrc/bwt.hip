@@ -10,13 +10,19 @@
 //   level 0      bucket every position of every block by its first byte (tile histograms in LDS,
 //                per-block scan, LDS-staged scatter).  Each element carries an 8-byte key (the
 //                rotation's bytes [kd, kd+8), big-endian) and a payload (prev byte << 24 | index).
-//   level >= 1   MSD radix passes on the next key byte for buckets larger than JOB_MAX, with the
-//                key re-gathered from the input every 8 bytes.  Sub-buckets of <= JOB_MAX elements
-//                are packed into wave jobs.
-//   wave jobs    one wave sorts <= 256 elements in registers (bitonic, 4 per lane), then refines
-//                groups of equal keys by gathering 7 more bytes per round (group id in the top 8
-//                bits keeps groups in place) until no ties remain, the depth reaches n (ties are
-//                then identical rotations), or a depth cap sends the group to the fallback.
+//   level >= 1   MSD radix passes on the next key byte for buckets larger than a workgroup job,
+//                with the key re-gathered from the input every 8 bytes.  Sub-buckets of
+//                <= JOB_MAX elements are packed into wave jobs, larger ones up to 256 * waves
+//                become workgroup jobs.  The host passes every count a kernel needs (tile counts,
+//                list lengths) as kernel arguments; no kernel re-reads a counter another kernel
+//                updated with atomics.
+//   jobs         a wave (<= 256 elements) or a workgroup (<= 256 * waves) sorts in registers
+//                (bitonic, 4 per lane) on 128-bit keys: group id in the top bits, then 15 (wave)
+//                or 14 (workgroup) rotation bytes gathered at the group's depth.  Groups still tied
+//                are compacted and re-sorted on the next bytes until no ties remain, the depth
+//                reaches n (ties are then identical rotations), or a depth cap sends the group to
+//                the fallback.  Job lists are reordered block-major per XCD so the gathers of the
+//                workgroups of one XCD hit the same one or two blocks in its L2.
 //   fallback     Larsson-Sadakane style prefix doubling on ranks for the groups still tied (only
 //                pathological, highly repetitive blocks get here), using the same MSD/wave
 //                machinery on 32-bit rank keys.
