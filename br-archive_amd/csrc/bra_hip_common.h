@@ -157,6 +157,40 @@ __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
         x[r] = max(x[r], ex);
 }
 
+// Exclusive sum over 256 elements (4 per lane, element = lane * 4 + r); *total = sum of all.
+__device__ __forceinline__ void wave_excl_sum4(const uint32_t (&x)[4], uint32_t (&ex)[4], uint32_t* total = nullptr)
+{
+    const uint32_t l1 = x[0], l2 = l1 + x[1], l3 = l2 + x[2], l4 = l3 + x[3];
+    uint32_t       agg = l4;
+    for (int d = 1; d < WAVE; d <<= 1)
+    {
+        const uint32_t o = __shfl_up(agg, d, WAVE);
+        if (lane_id() >= d)
+            agg += o;
+    }
+    if (total)
+        *total = __shfl(agg, WAVE - 1, WAVE);
+    const uint32_t pre = agg - l4;
+    ex[0]              = pre;
+    ex[1]              = pre + l1;
+    ex[2]              = pre + l2;
+    ex[3]              = pre + l3;
+}
+
+// Exclusive max-scan over 256 elements (4 per lane); 0 for the first element.
+__device__ __forceinline__ void wave_excl_max4(const uint32_t (&x)[4], uint32_t (&ex)[4])
+{
+    uint32_t inc[4] = {x[0], x[1], x[2], x[3]};
+    wave_max_scan4(inc);
+    uint32_t prev = __shfl_up(inc[3], 1, WAVE);
+    if (lane_id() == 0)
+        prev = 0;
+    ex[0] = prev;
+    ex[1] = inc[0];
+    ex[2] = inc[1];
+    ex[3] = inc[2];
+}
+
 // Inclusive min-scan over 256 elements (4 per lane) in REVERSE element order.
 __device__ __forceinline__ void wave_min_rscan4(uint32_t (&x)[4])
 {

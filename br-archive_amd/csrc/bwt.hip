@@ -215,193 +215,288 @@ struct ScanArgs
 
 constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into one wave job
 
-__device__ __forceinline__ uint32_t block256_exclusive_max(uint32_t v, uint32_t* tmp)
-{
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    uint32_t  x    = v;
-    for (int d = 1; d < WAVE; d <<= 1)
-    {
-        const uint32_t o = __shfl_up(x, d, WAVE);
-        if (lane >= d)
-            x = max(x, o);
-    }
-    if (lane == WAVE - 1)
-        tmp[w] = x;
-    uint32_t ex = __shfl_up(x, 1, WAVE);
-    if (lane == 0)
-        ex = 0;
-    __syncthreads();
-    for (int i = 0; i < w; ++i)
-        ex = max(ex, tmp[i]);
-    __syncthreads();
-    return ex;
-}
 
-// One workgroup per bucket, thread = digit.  Sub-bucket offsets per tile; the sub-buckets become
-// wave jobs (<= JOB_MAX; consecutive ones of <= SMALL_MAX share a job: digits of one run between
-// larger sub-buckets are grouped by floor(prefix / SMALL_MAX), so every job holds < JOB_MAX
-// elements), workgroup jobs (<= mjob_max), next-level buckets (their tiles reserved here, one
-// 64-bit atomic for bucket and tile slots), or fallback groups.
-template <uint32_t MODE>
-__global__ void __launch_bounds__(TPB) k_scan(ScanArgs a)
+// One wave per bucket (4 buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
+// per tile; the sub-buckets become wave jobs (<= JOB_MAX; consecutive ones of <= SMALL_MAX share
+// a job: digits of one run between larger sub-buckets are grouped by floor(prefix / SMALL_MAX),
+// so every job holds < JOB_MAX elements), workgroup jobs (<= mjob_max), next-level buckets (with
+// their tiles) or fallback groups.  The four waves' list slots are reserved with one atomic per
+// list per workgroup (jobs and workgroup jobs share a 64-bit atomic, so do buckets and tiles).
+constexpr int SCAN_WAVES = 4;
+
+struct ScanWaveCounts
 {
-    __shared__ uint32_t tmp[8];
-    __shared__ uint32_t key_s[256];
-    __shared__ uint32_t jlen_s[256];
-    __shared__ uint32_t jbase_s, mbase_s, bbase_s, tbase_s, gbase_s;
-    const uint32_t      dg = threadIdx.x;
-    for (uint32_t bi = blockIdx.x; bi < a.nbuckets; bi += gridDim.x)
+    uint32_t jobs, mjobs, big, tiles, groups, moved, melems, elems_next, gmembers, hmin;
+};
+
+template <uint32_t MODE>
+__global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
+{
+    __shared__ uint32_t       key_s[SCAN_WAVES][256];
+    __shared__ uint32_t       jlen_s[SCAN_WAVES][256];
+    __shared__ ScanWaveCounts cnt_s[SCAN_WAVES];
+    __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
+    const int                 lane = lane_id(), w = threadIdx.x >> 6;
+    for (uint32_t b0 = blockIdx.x * SCAN_WAVES; b0 < a.nbuckets; b0 += gridDim.x * SCAN_WAVES)
     {
-        const Bucket B = a.buckets[bi];
+        const uint32_t bi     = b0 + w;
+        const bool     active = bi < a.nbuckets;
+        Bucket         B{};
+        if (active)
+            B = a.buckets[bi];
 #ifdef BRA_DEBUG
-        if (dg == 0)
+        if (active && lane == 0)
         {
             const BlockDesc BD = a.blocks[B.block];
             BRA_DCHECK(B.start >= BD.off && B.start + B.len <= BD.off + BD.len, "scan bucket %u start %u len %u block %u off %llu blen %u d %u",
                        bi, B.start, B.len, B.block, (unsigned long long) BD.off, BD.len, B.d);
         }
 #endif
-        const uint32_t ntiles = div_up(B.len, TILE);
-        const uint32_t* th    = a.tile_hist + (size_t) B.tile0 * 256 + dg;
-        uint32_t       tot    = 0;
+        const uint32_t ntiles = active ? div_up(B.len, TILE) : 0;
+        const uint4*   th     = reinterpret_cast<const uint4*>(a.tile_hist + (size_t) B.tile0 * 256) + lane;
+        uint32_t       tot[4] = {0, 0, 0, 0};
         {
             uint32_t t = 0;
             for (; t + 8 <= ntiles; t += 8)
             {
-                uint32_t h[8];
+                uint4 h[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
-                    h[u] = th[(size_t) (t + u) * 256];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    tot += h[u];
-            }
-            for (; t < ntiles; ++t)
-                tot += th[(size_t) t * 256];
-        }
-        const uint32_t base = block256_exclusive_sum(tot, tmp);
-        {
-            uint32_t* to  = a.tile_off + (size_t) B.tile0 * 256 + dg;
-            uint32_t  run = B.start + base;
-            uint32_t  t   = 0;
-            for (; t + 8 <= ntiles; t += 8)
-            {
-                uint32_t h[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    h[u] = th[(size_t) (t + u) * 256];
+                    h[u] = th[(size_t) (t + u) * 64];
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
                 {
-                    to[(size_t) (t + u) * 256] = run;
-                    run += h[u];
+                    tot[0] += h[u].x;
+                    tot[1] += h[u].y;
+                    tot[2] += h[u].z;
+                    tot[3] += h[u].w;
                 }
             }
             for (; t < ntiles; ++t)
             {
-                const uint32_t h          = th[(size_t) t * 256];
-                to[(size_t) t * 256]      = run;
-                run += h;
+                const uint4 h = th[(size_t) t * 64];
+                tot[0] += h.x;
+                tot[1] += h.y;
+                tot[2] += h.z;
+                tot[3] += h.w;
             }
         }
-        const bool     nomove = __syncthreads_or(tot == B.len);
+        uint32_t base[4];
+        wave_excl_sum4(tot, base);
+        {
+            uint4*   to     = reinterpret_cast<uint4*>(a.tile_off + (size_t) B.tile0 * 256) + lane;
+            uint32_t run[4] = {B.start + base[0], B.start + base[1], B.start + base[2], B.start + base[3]};
+            for (uint32_t t = 0; t < ntiles; ++t)
+            {
+                const uint4 h        = th[(size_t) t * 64];
+                to[(size_t) t * 64] = make_uint4(run[0], run[1], run[2], run[3]);
+                run[0] += h.x;
+                run[1] += h.y;
+                run[2] += h.z;
+                run[3] += h.w;
+            }
+        }
+        const bool     nomove = active && __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
         const uint32_t kd     = eff_kd(B, MODE);
         const uint32_t nd     = B.d + 1;
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
-        if (dg == 0)
-        {
+        if (active && lane == 0)
             a.nomove[bi] = nomove ? 1 : 0;
-            if (!nomove && a.account)
-                atomicAdd(&a.ctr->n_moved, B.len);
-        }
-        const bool big   = tot > a.mjob_max;
-        const bool med   = tot > JOB_MAX && !big;
-        const bool mid   = tot > SMALL_MAX && tot <= JOB_MAX;
-        const bool small = tot > 0 && tot <= SMALL_MAX;
-        const bool brk   = big || med || mid;
-        // ---- wave jobs ----
-        const uint32_t S     = block256_exclusive_sum(small ? tot : 0, tmp);
-        const uint32_t R0    = block256_exclusive_max(brk ? S : 0, tmp);
-        const uint32_t runid = block256_exclusive_sum(brk ? 1u : 0u, tmp);
-        const uint32_t key   = (runid << 20) | ((S - R0) / SMALL_MAX);
-        const uint32_t prevs = block256_exclusive_max(small ? dg + 1 : 0, tmp);
-        key_s[dg]            = key;
-        jlen_s[dg]           = 0;
-        __syncthreads();
-        const bool     jstart = mid || (small && (prevs == 0 || key_s[prevs - 1] != key));
-        uint32_t       jtot;
-        const uint32_t jex  = block256_exclusive_sum(jstart ? 1u : 0u, tmp, &jtot);
-        const uint32_t jidx = jex + (jstart ? 1u : 0u) - 1u;
-        if (small || mid)
-            atomicAdd(&jlen_s[jidx], tot);
-        // ---- workgroup jobs, next-level buckets, fallback groups ----
-        const bool final_grp = big && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
-        const bool nb_next   = big && !final_grp;
-        uint32_t   btot, ttot, gtot, mtot;
-        const uint32_t ntl = nb_next ? div_up(tot, TILE) : 0;
-        const uint32_t bex = block256_exclusive_sum(nb_next ? 1u : 0u, tmp, &btot);
-        const uint32_t tex = block256_exclusive_sum(ntl, tmp, &ttot);
-        const uint32_t mex = block256_exclusive_sum(med ? 1u : 0u, tmp, &mtot);
-        const uint32_t gex = block256_exclusive_sum(final_grp ? 1u : 0u, tmp, &gtot);
-        if (dg == 0)
+        bool big[4], med[4], mid[4], small[4], fin[4], nbn[4];
+        uint32_t xs[4], xb[4], xp[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
         {
-            jbase_s = jtot ? atomicAdd(&a.ctr->n_jobs, jtot) : 0;
-            mbase_s = mtot ? atomicAdd(&a.ctr->n_mjobs, mtot) : 0;
-            if (btot)
+            big[r]   = tot[r] > a.mjob_max;
+            med[r]   = tot[r] > JOB_MAX && !big[r];
+            mid[r]   = tot[r] > SMALL_MAX && tot[r] <= JOB_MAX;
+            small[r] = tot[r] > 0 && tot[r] <= SMALL_MAX;
+            fin[r]   = big[r] && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
+            nbn[r]   = big[r] && !fin[r];
+            xs[r]    = small[r] ? tot[r] : 0;
+            xb[r]    = (big[r] || med[r] || mid[r]) ? 1u : 0u;
+            xp[r]    = small[r] ? (uint32_t) (lane * 4 + r + 1) : 0u;
+        }
+        // ---- wave jobs: runs of small sub-buckets between larger ones, chopped by SMALL_MAX ----
+        uint32_t S[4], R0[4], runid[4], prevs[4], tmp4[4];
+        wave_excl_sum4(xs, S);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            tmp4[r] = xb[r] ? S[r] : 0;
+        wave_excl_max4(tmp4, R0);
+        wave_excl_sum4(xb, runid);
+        wave_excl_max4(xp, prevs);
+        uint32_t key[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            key[r]                    = (runid[r] << 20) | ((S[r] - R0[r]) / SMALL_MAX);
+            key_s[w][lane * 4 + r]  = key[r];
+            jlen_s[w][lane * 4 + r] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        bool     jstart[4];
+        uint32_t js[4], jex[4], jtot;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            jstart[r] = mid[r] || (small[r] && (prevs[r] == 0 || key_s[w][prevs[r] - 1] != key[r]));
+            js[r]     = jstart[r] ? 1u : 0u;
+        }
+        wave_excl_sum4(js, jex, &jtot);
+        uint32_t jidx[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            jidx[r] = jex[r] + js[r] - 1u;
+            if (small[r] || mid[r])
+                atomicAdd(&jlen_s[w][jidx[r]], tot[r]);
+        }
+        // ---- workgroup jobs, next-level buckets, fallback groups ----
+        uint32_t cm[4], cb[4], ct[4], cg[4], mex[4], bex[4], tex[4], gex[4], ntl[4];
+        uint32_t melems = 0, enext = 0, gmem = 0, gmin = 0xFFFFFFFFu;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            ntl[r] = nbn[r] ? div_up(tot[r], TILE) : 0;
+            cm[r]  = med[r] ? 1u : 0u;
+            cb[r]  = nbn[r] ? 1u : 0u;
+            ct[r]  = ntl[r];
+            cg[r]  = fin[r] ? 1u : 0u;
+            melems += med[r] ? tot[r] : 0;
+            enext += nbn[r] ? tot[r] : 0;
+            gmem += fin[r] ? tot[r] : 0;
+        }
+        ScanWaveCounts C{};
+        wave_excl_sum4(cm, mex, &C.mjobs);
+        wave_excl_sum4(cb, bex, &C.big);
+        wave_excl_sum4(ct, tex, &C.tiles);
+        wave_excl_sum4(cg, gex, &C.groups);
+        C.jobs = active ? jtot : 0;
+        if (!active)
+            C.mjobs = C.big = C.tiles = C.groups = 0;
+        if (a.account || C.groups)
+        {
+            for (int d = 32; d >= 1; d >>= 1)
+            {
+                melems += __shfl_xor(melems, d, WAVE);
+                enext += __shfl_xor(enext, d, WAVE);
+                gmem += __shfl_xor(gmem, d, WAVE);
+            }
+            C.melems     = active ? melems : 0;
+            C.elems_next = active ? enext : 0;
+            C.gmembers   = active ? gmem : 0;
+            C.moved      = (active && !nomove) ? B.len : 0;
+            gmin         = C.groups ? ((MODE == MODE_STRING) ? nd : B.gdepth) : 0xFFFFFFFFu;
+        }
+        C.hmin = gmin;
+        if (lane == 0)
+            cnt_s[w] = C;
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            uint32_t pre[5] = {0, 0, 0, 0, 0}, tj = 0, tm = 0, tb = 0, tt = 0, tg = 0;
+            ScanWaveCounts T{};
+            T.hmin = 0xFFFFFFFFu;
+            for (int v = 0; v < SCAN_WAVES; ++v)
+            {
+                const ScanWaveCounts& c = cnt_s[v];
+                base_s[v][0] = tj;
+                base_s[v][1] = tm;
+                base_s[v][2] = tb;
+                base_s[v][3] = tt;
+                base_s[v][4] = tg;
+                tj += c.jobs;
+                tm += c.mjobs;
+                tb += c.big;
+                tt += c.tiles;
+                tg += c.groups;
+                T.moved += c.moved;
+                T.melems += c.melems;
+                T.elems_next += c.elems_next;
+                T.gmembers += c.gmembers;
+                T.hmin = min(T.hmin, c.hmin);
+            }
+            if (tj || tm)
             {
                 const unsigned long long old =
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_big), ((unsigned long long) ttot << 32) | btot);
-                bbase_s = (uint32_t) old;
-                tbase_s = (uint32_t) (old >> 32);
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) tm << 32) | tj);
+                pre[0] = (uint32_t) old;
+                pre[1] = (uint32_t) (old >> 32);
             }
-            gbase_s = gtot ? atomicAdd(&a.ctr->n_groups, gtot) : 0;
+            if (tb)
+            {
+                const unsigned long long old =
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_big), ((unsigned long long) tt << 32) | tb);
+                pre[2] = (uint32_t) old;
+                pre[3] = (uint32_t) (old >> 32);
+            }
+            if (tg)
+            {
+                pre[4] = atomicAdd(&a.ctr->n_groups, tg);
+                atomicAdd(&a.ctr->g_members, T.gmembers);
+                atomicMin(&a.ctr->hmin, T.hmin);
+            }
+            if (a.account)
+            {
+                if (T.moved)
+                    atomicAdd(&a.ctr->n_moved, T.moved);
+                if (T.melems)
+                    atomicAdd(&a.ctr->n_melems, T.melems);
+                if (T.elems_next)
+                    atomicAdd(&a.ctr->n_elems_next, T.elems_next);
+            }
+            for (int v = 0; v < SCAN_WAVES; ++v)
+                for (int q = 0; q < 5; ++q)
+                    base_s[v][q] += pre[q];
         }
         __syncthreads();
-        const uint32_t s0 = B.start + base;
-        if (jstart)
+        if (active)
         {
-            const uint32_t slot = jbase_s + jidx;
-            if (slot < a.cap_jobs)
-                a.jobs[slot] = Job{s0, jlen_s[jidx], kd, obuf, B.block, B.gdepth, nd};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (med)
-        {
-            const uint32_t slot = mbase_s + mex;
-            if (slot < a.cap_mjobs)
-                a.mjobs[slot] = Job{s0, tot, kd, obuf, B.block, B.gdepth, nd};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-            if (a.account)
-                atomicAdd(&a.ctr->n_melems, tot);
-        }
-        if (nb_next)
-        {
-            const uint32_t slot = bbase_s + bex, t0 = tbase_s + tex;
-            if (slot < a.cap_next && t0 + ntl <= a.cap_tiles)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
             {
-                a.next[slot] = Bucket{s0, tot, nd, kd, B.block, obuf, B.gdepth, t0};
-                for (uint32_t t = 0; t < ntl; ++t)
-                    a.tile_bucket_next[t0 + t] = slot;
-                if (a.account)
-                    atomicAdd(&a.ctr->n_elems_next, tot);
+                const uint32_t s0 = B.start + base[r];
+                if (jstart[r])
+                {
+                    const uint32_t slot = base_s[w][0] + jidx[r];
+                    if (slot < a.cap_jobs)
+                        a.jobs[slot] = Job{s0, jlen_s[w][jidx[r]], kd, obuf, B.block, B.gdepth, nd};
+                    else
+                        atomicExch(&a.ctr->overflow, 1u);
+                }
+                if (med[r])
+                {
+                    const uint32_t slot = base_s[w][1] + mex[r];
+                    if (slot < a.cap_mjobs)
+                        a.mjobs[slot] = Job{s0, tot[r], kd, obuf, B.block, B.gdepth, nd};
+                    else
+                        atomicExch(&a.ctr->overflow, 1u);
+                }
+                if (nbn[r])
+                {
+                    const uint32_t slot = base_s[w][2] + bex[r], t0 = base_s[w][3] + tex[r];
+                    if (slot < a.cap_next && t0 + ntl[r] <= a.cap_tiles)
+                    {
+                        a.next[slot] = Bucket{s0, tot[r], nd, kd, B.block, obuf, B.gdepth, t0};
+                        for (uint32_t t = 0; t < ntl[r]; ++t)
+                            a.tile_bucket_next[t0 + t] = slot;
+                    }
+                    else
+                        atomicExch(&a.ctr->overflow, 1u);
+                }
+                if (fin[r])
+                {
+                    const uint32_t gdep = (MODE == MODE_STRING) ? nd : B.gdepth;
+                    const uint32_t slot = base_s[w][4] + gex[r];
+                    if (slot < a.cap_groups)
+                        a.groups[slot] = Group{s0, tot[r], gdep, B.block | (obuf << 31)};
+                    else
+                        atomicExch(&a.ctr->overflow, 1u);
+                }
             }
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (final_grp)
-        {
-            const uint32_t gdep = (MODE == MODE_STRING) ? nd : B.gdepth;
-            const uint32_t slot = gbase_s + gex;
-            if (slot < a.cap_groups)
-            {
-                a.groups[slot] = Group{s0, tot, gdep, B.block | (obuf << 31)};
-                atomicAdd(&a.ctr->g_members, tot);
-                atomicMin(&a.ctr->hmin, gdep);
-            }
-            else
-                atomicExch(&a.ctr->overflow, 1u);
         }
         __syncthreads();
     }
@@ -1492,7 +1587,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                    (uint32_t) (g_prof != nullptr), w.mjob_max()};
         {
             BRA_PROF(P_BWT_SCAN, s);
-            hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(nbig, 65535u)), dim3(TPB), 0, s, a);
+            hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(div_up(nbig, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a);
         }
         {
             BRA_PROF(P_BWT_SCATTER, s);
@@ -1593,7 +1688,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max()};
     {
         BRA_PROF(P_BWT_SCAN, s);
-        hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(TPB), 0, s, a0);
+        hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(div_up(nblocks, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a0);
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
