@@ -157,6 +157,42 @@ __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
         x[r] = max(x[r], ex);
 }
 
+// Value of x held by lane (lane ^ LM), LM in {1, 2, 4, 8, 16, 32}, without going through LDS:
+// DPP quad permutes / row rotate / row shifts inside a row of 16, permlane swaps across rows.
+template <int LM>
+__device__ __forceinline__ uint32_t xlane(uint32_t x)
+{
+    if constexpr (LM == 1)
+        return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (LM == 2)
+        return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    else if constexpr (LM == 4)
+    {
+        const uint32_t up = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x104, 0xF, 0xF, false);  // row_shl:4, lane i <- i+4
+        const uint32_t dn = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x114, 0xF, 0xF, false);  // row_shr:4, lane i <- i-4
+        return (lane_id() & 4) ? dn : up;
+    }
+    else if constexpr (LM == 8)
+        return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (LM == 16)
+    {
+        const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane_id() & 16) ? p[0] : p[1];
+    }
+    else
+    {
+        static_assert(LM == 32, "lane distance");
+        const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane_id() & 32) ? p[0] : p[1];
+    }
+}
+
+template <int LM>
+__device__ __forceinline__ uint64_t xlane64(uint64_t x)
+{
+    return ((uint64_t) xlane<LM>((uint32_t) (x >> 32)) << 32) | xlane<LM>((uint32_t) x);
+}
+
 // Exclusive sum over 256 elements (4 per lane, element = lane * 4 + r); *total = sum of all.
 __device__ __forceinline__ void wave_excl_sum4(const uint32_t (&x)[4], uint32_t (&ex)[4], uint32_t* total = nullptr)
 {

@@ -715,7 +715,8 @@ struct JobLds
 {
     uint64_t kh[256 * W];   // cross-wave network exchange, neighbour keys, compaction scratch
     uint64_t kl[256 * W];
-    uint32_t v[256 * W];
+    uint32_t v[256 * W];    // payload of every slot of the current round (the keys carry the slot)
+    uint32_t nx[256 * W];   // group-end scratch
     uint16_t pos[256 * W];  // job position of each active slot (increasing)
     uint32_t agg[W];
 };
@@ -733,6 +734,7 @@ __device__ __forceinline__ void job_sync()
     }
 }
 
+
 template <int W>
 __device__ __forceinline__ bool job_any(bool x)
 {
@@ -741,109 +743,8 @@ __device__ __forceinline__ bool job_any(bool x)
     return __any(x);
 }
 
-// (hi, lo, v) lexicographic "greater than"
-__device__ __forceinline__ bool k3_gt(uint64_t ha, uint64_t la, uint32_t va, uint64_t hb, uint64_t lb, uint32_t vb)
-{
-    if (ha != hb)
-        return ha > hb;
-    if (la != lb)
-        return la > lb;
-    return va > vb;
-}
 
-template <int W>
-__device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], uint32_t (&v)[4], int P, JobLds<W>& S, int wj)
-{
-    const int lane = lane_id();
-    for (int size = 2; size <= P; size <<= 1)
-    {
-        for (int j = size >> 1; j > 0; j >>= 1)
-        {
-            if (W > 1 && j >= 256)
-            {
-                job_sync<W>();
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const int e = wj * 256 + lane * 4 + r;
-                    S.kh[e]     = kh[r];
-                    S.kl[e]     = kl[r];
-                    S.v[e]      = v[r];
-                }
-                job_sync<W>();
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const int      e    = wj * 256 + lane * 4 + r;
-                    const uint64_t oh   = S.kh[e ^ j];
-                    const uint64_t ol   = S.kl[e ^ j];
-                    const uint32_t ov   = S.v[e ^ j];
-                    const bool     up   = (e & size) == 0;
-                    const bool     low  = (e & j) == 0;
-                    const bool     gt   = k3_gt(kh[r], kl[r], v[r], oh, ol, ov);
-                    const bool     take = (low == up) ? gt : !gt;
-                    if (take)
-                    {
-                        kh[r] = oh;
-                        kl[r] = ol;
-                        v[r]  = ov;
-                    }
-                }
-            }
-            else if (j >= 4)
-            {
-                const int lm = j >> 2;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const int      e    = wj * 256 + lane * 4 + r;
-                    const uint64_t oh   = shfl_xor64(kh[r], lm);
-                    const uint64_t ol   = shfl_xor64(kl[r], lm);
-                    const uint32_t ov   = __shfl_xor(v[r], lm, WAVE);
-                    const bool     up   = (e & size) == 0;
-                    const bool     low  = (e & j) == 0;
-                    const bool     gt   = k3_gt(kh[r], kl[r], v[r], oh, ol, ov);
-                    const bool     take = (low == up) ? gt : !gt;
-                    if (take)
-                    {
-                        kh[r] = oh;
-                        kl[r] = ol;
-                        v[r]  = ov;
-                    }
-                }
-            }
-            else
-            {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const int p = r ^ j;
-                    if (p > r)
-                    {
-                        const int  e  = wj * 256 + lane * 4 + r;
-                        const bool up = (e & size) == 0;
-                        const bool gt = k3_gt(kh[r], kl[r], v[r], kh[p], kl[p], v[p]);
-                        if (gt == up)
-                        {
-                            uint64_t t0 = kh[r];
-                            kh[r]       = kh[p];
-                            kh[p]       = t0;
-                            uint64_t t1 = kl[r];
-                            kl[r]       = kl[p];
-                            kl[p]       = t1;
-                            uint32_t tv = v[r];
-                            v[r]        = v[p];
-                            v[p]        = tv;
-                        }
-                    }
-                }
-            }
-        }
-    }
-    job_sync<W>();
-}
 
-// inclusive max-scan / reverse min-scan / exclusive count over the job's 256*W slots
 template <int W>
 __device__ __forceinline__ void job_max_scan(uint32_t (&x)[4], JobLds<W>& S, int wj)
 {
@@ -863,6 +764,7 @@ __device__ __forceinline__ void job_max_scan(uint32_t (&x)[4], JobLds<W>& S, int
     }
 }
 
+
 template <int W>
 __device__ __forceinline__ void job_min_rscan(uint32_t (&x)[4], JobLds<W>& S, int wj)
 {
@@ -881,6 +783,7 @@ __device__ __forceinline__ void job_min_rscan(uint32_t (&x)[4], JobLds<W>& S, in
         job_sync<W>();
     }
 }
+
 
 template <int W>
 __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex)[4], uint32_t& total, JobLds<W>& S, int wj)
@@ -934,9 +837,102 @@ __device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint
     w1 = load_key8(blk, n, s2);
 }
 
-// Group heads / group ends / ties over the T active slots (keys in S.kh / S.kl must be current).
+
+// 128-bit key (kh, kl) "greater than"; keys are unique (the slot is in the low bits of kl).
+__device__ __forceinline__ bool k2_gt(uint64_t ha, uint64_t la, uint64_t hb, uint64_t lb) { return ha > hb || (ha == hb && la > lb); }
+
+// One bitonic stage whose partners sit LM lanes away (same register r): exchanged with DPP /
+// permlane swaps.  keep_min: this lane keeps the smaller key of each pair.
+template <int LM>
+__device__ __forceinline__ void net_stage_lanes(uint64_t (&kh)[4], uint64_t (&kl)[4], bool keep_min)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint64_t oh = xlane64<LM>(kh[r]), ol = xlane64<LM>(kl[r]);
+        if (k2_gt(kh[r], kl[r], oh, ol) == keep_min)
+        {
+            kh[r] = oh;
+            kl[r] = ol;
+        }
+    }
+}
+
+// Bitonic sort of the job's 256*W slots (4 consecutive per lane, slot e = wj*256 + lane*4 + r)
+// over the first P (power of two) slots.
 template <int W>
-__device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64_t (&kl)[4], uint32_t T, JobLds<W>& S, int wj,
+__device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], int P, JobLds<W>& S, int wj)
+{
+    const int      lane = lane_id();
+    const uint32_t e0   = wj * 256 + lane * 4;
+    for (int size = 2; size <= P; size <<= 1)
+    {
+        for (int j = size >> 1; j > 0; j >>= 1)
+        {
+            if (W > 1 && j >= 256)
+            {
+                job_sync<W>();
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    S.kh[e0 + r] = kh[r];
+                    S.kl[e0 + r] = kl[r];
+                }
+                job_sync<W>();
+                const bool keep_min = ((e0 & size) == 0) == ((e0 & j) == 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const uint64_t oh = S.kh[(e0 + r) ^ j], ol = S.kl[(e0 + r) ^ j];
+                    if (k2_gt(kh[r], kl[r], oh, ol) == keep_min)
+                    {
+                        kh[r] = oh;
+                        kl[r] = ol;
+                    }
+                }
+            }
+            else if (j >= 4)
+            {
+                const bool keep_min = ((e0 & size) == 0) == ((e0 & j) == 0);
+                switch (j >> 2)
+                {
+                case 1: net_stage_lanes<1>(kh, kl, keep_min); break;
+                case 2: net_stage_lanes<2>(kh, kl, keep_min); break;
+                case 4: net_stage_lanes<4>(kh, kl, keep_min); break;
+                case 8: net_stage_lanes<8>(kh, kl, keep_min); break;
+                case 16: net_stage_lanes<16>(kh, kl, keep_min); break;
+                default: net_stage_lanes<32>(kh, kl, keep_min); break;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const int q = r ^ j;
+                    if (q > r)
+                    {
+                        const bool up = ((e0 + r) & size) == 0;
+                        if (k2_gt(kh[r], kl[r], kh[q], kl[q]) == up)
+                        {
+                            const uint64_t th = kh[r], tl = kl[r];
+                            kh[r]             = kh[q];
+                            kl[r]             = kl[q];
+                            kh[q]             = th;
+                            kl[q]             = tl;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    job_sync<W>();
+}
+
+// Group heads / group ends / ties over the T active slots; kh / km are the keys without the slot
+// bits.
+template <int W>
+__device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64_t (&km)[4], uint32_t T, JobLds<W>& S, int wj,
                                            uint32_t (&g)[4], uint32_t (&gend)[4], bool (&tied)[4])
 {
     constexpr uint32_t SLOTS = 256 * W;
@@ -946,7 +942,7 @@ __device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64
     {
         const uint32_t c = wj * 256 + lane * 4 + r;
         S.kh[c]          = kh[r];
-        S.kl[c]          = kl[r];
+        S.kl[c]          = km[r];
     }
     job_sync<W>();
     uint32_t x[4];
@@ -954,24 +950,22 @@ __device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64
     for (int r = 0; r < 4; ++r)
     {
         const uint32_t c  = wj * 256 + lane * 4 + r;
-        const bool     hd = (c == 0) || c >= T || S.kh[c - 1] != kh[r] || S.kl[c - 1] != kl[r];
+        const bool     hd = (c == 0) || c >= T || S.kh[c - 1] != kh[r] || S.kl[c - 1] != km[r];
         g[r]              = hd ? c : 0;
         x[r]              = hd ? c : 0xFFFFFFFFu;
     }
     job_max_scan<W>(g, S, wj);
     job_min_rscan<W>(x, S, wj);
-    uint32_t* nxt = S.v;
-    job_sync<W>();
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-        nxt[wj * 256 + lane * 4 + r] = x[r];
+        S.nx[wj * 256 + lane * 4 + r] = x[r];
     job_sync<W>();
     bool any = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         const uint32_t c   = wj * 256 + lane * 4 + r;
-        const uint32_t nh  = (c + 1 < SLOTS) ? nxt[c + 1] : 0xFFFFFFFFu;
+        const uint32_t nh  = (c + 1 < SLOTS) ? S.nx[c + 1] : 0xFFFFFFFFu;
         const uint32_t end = min(nh == 0xFFFFFFFFu ? SLOTS : nh, T);
         gend[r]            = end;
         tied[r]            = c < T && (end - g[r]) >= 2;
@@ -981,24 +975,41 @@ __device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64
     return job_any<W>(any);
 }
 
+template <int W>
+struct JobGeom
+{
+    static constexpr int      LOGS  = (W == 1) ? 8 : (W == 2) ? 9 : (W == 4) ? 10 : (W == 8) ? 11 : 12;  // log2(256 * W)
+    static constexpr int      GBITS = LOGS;                                // group id bits (top of kh)
+    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;                  // slot bits (bottom of kl)
+    static constexpr uint32_t ADV   = (128 - GBITS - LOGS) / 8;            // whole rotation bytes per key
+};
+
+// key = group | the rotation's 16 bytes (w0:w1) shifted right by GBITS, low LOGS bits = slot
+template <int W>
+__device__ __forceinline__ void make_key(uint32_t grp, uint32_t slot, uint64_t w0, uint64_t w1, uint64_t& kh, uint64_t& kl)
+{
+    using G = JobGeom<W>;
+    kh      = ((uint64_t) grp << (64 - G::GBITS)) | (w0 >> G::GBITS);
+    kl      = (((w0 << (64 - G::GBITS)) | (w1 >> G::GBITS)) & ~G::SMASK) | slot;
+}
+
 template <uint32_t MODE, int W>
 __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj)
 {
-    constexpr int      GBITS = (W > 1) ? 12 : 8;        // group-id bits
-    constexpr uint32_t ADV   = (128 - GBITS) / 8;       // whole rotation bytes per round
-    const int          lane  = lane_id();
-    const BlockDesc    BD    = a.blocks[J.block];
-    const uint8_t*     blk   = a.in + BD.off;
-    const uint64_t*    K     = J.buf ? a.key1 : a.key0;
-    const uint32_t*    V     = J.buf ? a.pay1 : a.pay0;
-    const uint32_t     boff  = (uint32_t) BD.off;
-    uint64_t           kh[4], kl[4];
-    uint32_t           v[4];
-    uint32_t           pos[4];  // job position of slot c
-    uint32_t           g[4], gend[4];
-    bool               tied[4];
-    uint32_t           T     = J.len;
-    uint32_t           depth = (MODE == MODE_STRING) ? J.d : J.gdepth;
+    using G                 = JobGeom<W>;
+    const int       lane    = lane_id();
+    const BlockDesc BD      = a.blocks[J.block];
+    const uint8_t*  blk     = a.in + BD.off;
+    const uint64_t* K       = J.buf ? a.key1 : a.key0;
+    const uint32_t* V       = J.buf ? a.pay1 : a.pay0;
+    const uint32_t  boff    = (uint32_t) BD.off;
+    uint64_t        kh[4], kl[4], km[4];
+    uint32_t        v[4];
+    uint32_t        pos[4];  // job position of slot c
+    uint32_t        g[4], gend[4];
+    bool            tied[4];
+    uint32_t        T     = J.len;
+    uint32_t        depth = (MODE == MODE_STRING) ? J.d : J.gdepth;
     if (!BRA_DCHECK(T <= 256u * W && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job mode %u W %d start %u len %u block %u off %llu blen %u",
                     MODE, W, J.start, T, J.block, (unsigned long long) BD.off, BD.len))
         T = 0;
@@ -1007,33 +1018,31 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     {
         const uint32_t c = wj * 256 + lane * 4 + r;
         pos[r]           = c;
+        v[r]             = 0;
+        kh[r] = kl[r] = ~0ull;
         if (c < T)
         {
             v[r] = V[J.start + c];
-            if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (mode %u buf %u slot %u)", v[r] & 0xFFFFFFu, BD.len, MODE, J.buf, J.start + c))
+            if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (mode %u buf %u slot %u)", v[r] & 0xFFFFFFu, BD.len, MODE, J.buf,
+                            J.start + c))
                 v[r] = 0;
             if (MODE == MODE_RANK)
             {
                 kh[r] = K[J.start + c];
-                kl[r] = 0;
+                kl[r] = c;
             }
             else
             {
                 // sub-bucket = digit at depth d-1 (elements of one digit are contiguous)
-                const uint64_t key = K[J.start + c];
-                kh[r]              = (key >> (56 - 8 * (J.d - 1 - J.kd))) & 0xFF;
-                kl[r]              = 0;
+                kh[r] = (K[J.start + c] >> (56 - 8 * (J.d - 1 - J.kd))) & 0xFF;
+                kl[r] = 0;
             }
         }
-        else
-        {
-            kh[r] = kl[r] = ~0ull;
-            v[r]          = ~0u;
-        }
+        S.v[c] = v[r];
     }
     if (MODE == MODE_STRING)
     {
-        // round 1 groups = sub-buckets; keys = group id | 128-GBITS bits at depth d
+        // round 1 groups = sub-buckets; keys = group | rotation bytes from depth d | slot
         job_groups<W>(kh, kl, T, S, wj, g, gend, tied);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -1041,29 +1050,35 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             const uint32_t c = wj * 256 + lane * 4 + r;
             if (c < T)
             {
-                const uint32_t idx = v[r] & 0xFFFFFFu;
-                uint32_t       st  = idx + (depth % BD.len);
+                uint32_t st = (v[r] & 0xFFFFFFu) + (depth % BD.len);
                 if (st >= BD.len)
                     st -= BD.len;
                 uint64_t w0, w1;
                 load_key16(blk, BD.len, st, w0, w1);
-                kh[r] = ((uint64_t) g[r] << (64 - GBITS)) | (w0 >> GBITS);
-                kl[r] = (w0 << (64 - GBITS)) | (w1 >> GBITS);
+                make_key<W>(g[r], c, w0, w1, kh[r], kl[r]);
             }
+            else
+                kh[r] = kl[r] = ~0ull;
         }
     }
     int P = 4;
     while ((uint32_t) P < T)
         P <<= 1;
-    job_sort<W>(kh, kl, v, P, S, wj);
+    job_sort<W>(kh, kl, P, S, wj);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        v[r]  = S.v[(uint32_t) (kl[r] & G::SMASK)];
+        km[r] = kl[r] & ~G::SMASK;
+    }
     if (MODE == MODE_STRING)
-        depth += ADV;
+        depth += G::ADV;
     for (;;)
     {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             S.pos[wj * 256 + lane * 4 + r] = (uint16_t) pos[r];
-        const bool any    = job_groups<W>(kh, kl, T, S, wj, g, gend, tied);
+        const bool any    = job_groups<W>(kh, km, T, S, wj, g, gend, tied);
         bool       finish = (MODE == MODE_RANK) || !any;
         bool final_ties = false, to_fallback = false;
         if (!finish && depth >= BD.len)
@@ -1129,31 +1144,33 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             const uint32_t c = wj * 256 + lane * 4 + r;
             if (c < T)
             {
-                const uint64_t gp  = S.kh[c];
-                pos[r]             = (uint32_t) (gp & 0xFFFF);
-                v[r]               = S.v[c];
-                const uint32_t idx = v[r] & 0xFFFFFFu;
-                uint32_t       st  = idx + (depth % BD.len);
+                const uint64_t gp = S.kh[c];
+                pos[r]            = (uint32_t) (gp & 0xFFFF);
+                uint32_t st       = (S.v[c] & 0xFFFFFFu) + (depth % BD.len);
                 if (st >= BD.len)
                     st -= BD.len;
                 uint64_t w0, w1;
                 load_key16(blk, BD.len, st, w0, w1);
-                kh[r] = ((gp >> 16) << (64 - GBITS)) | (w0 >> GBITS);
-                kl[r] = (w0 << (64 - GBITS)) | (w1 >> GBITS);
+                make_key<W>((uint32_t) (gp >> 16), c, w0, w1, kh[r], kl[r]);
             }
             else
             {
                 pos[r] = c;
                 kh[r] = kl[r] = ~0ull;
-                v[r]          = ~0u;
             }
         }
         job_sync<W>();
         P = 4;
         while ((uint32_t) P < T)
             P <<= 1;
-        job_sort<W>(kh, kl, v, P, S, wj);
-        depth += ADV;
+        job_sort<W>(kh, kl, P, S, wj);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            v[r]  = S.v[(uint32_t) (kl[r] & G::SMASK)];
+            km[r] = kl[r] & ~G::SMASK;
+        }
+        depth += G::ADV;
     }
 }
 
