@@ -35,6 +35,21 @@
 
 namespace bra {
 
+#ifdef BRA_DEBUG
+#define BRA_DSYNC(st)                                                                                     \
+    do                                                                                                    \
+    {                                                                                                     \
+        hipError_t _e = hipStreamSynchronize(st);                                                         \
+        if (_e != hipSuccess)                                                                             \
+            fprintf(stderr, "[bra dsync] %s after the launch at %s:%d\n", hipGetErrorString(_e), __FILE__, __LINE__); \
+    } while (0)
+#else
+#define BRA_DSYNC(st) \
+    do                \
+    {                 \
+    } while (0)
+#endif
+
 namespace {
 
 constexpr int      TILE         = 4096;  // elements per tile (256 threads x 16)
@@ -827,9 +842,28 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
     total = wtot;
 }
 
-// 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian
+// 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian.  Non-wrapping reads
+// take one or two aligned 16-byte loads (the second only for an unaligned start: then both hold
+// in-range bytes, so the read never leaves the buffer's pages) and a funnel shift.
 __device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint32_t n, uint32_t start, uint64_t& w0, uint64_t& w1)
 {
+    if (start + 16u <= n)
+    {
+        const uintptr_t a  = (uintptr_t) (blk + start);
+        const uint4*    p  = (const uint4*) (a & ~(uintptr_t) 15);
+        const uint4     q0 = p[0];
+        const uint4     q1 = (a & 15) ? p[1] : make_uint4(0, 0, 0, 0);  // an aligned start needs 16 bytes only
+        const uint64_t  u0 = ((uint64_t) q0.y << 32) | q0.x, u1 = ((uint64_t) q0.w << 32) | q0.z;
+        const uint64_t  u2 = ((uint64_t) q1.y << 32) | q1.x, u3 = ((uint64_t) q1.w << 32) | q1.z;
+        const bool      hi = (a & 8) != 0;
+        const uint64_t  A = hi ? u1 : u0, B = hi ? u2 : u1, C = hi ? u3 : u2;
+        const uint32_t  sh = (uint32_t) (a & 7) * 8;
+        const uint64_t  r0 = sh ? (A >> sh) | (B << (64 - sh)) : A;
+        const uint64_t  r1 = sh ? (B >> sh) | (C << (64 - sh)) : B;
+        w0                 = __builtin_bswap64(r0);
+        w1                 = __builtin_bswap64(r1);
+        return;
+    }
     w0          = load_key8(blk, n, start);
     uint32_t s2 = start + 8;
     while (s2 >= n)
@@ -982,7 +1016,16 @@ struct JobGeom
     static constexpr int      GBITS = LOGS;                                // group id bits (top of kh)
     static constexpr uint64_t SMASK = (1ull << LOGS) - 1;                  // slot bits (bottom of kl)
     static constexpr uint32_t ADV   = (128 - GBITS - LOGS) / 8;            // whole rotation bytes per key
+    static constexpr uint32_t ADV1  = (128 - LOGS) / 8;                    // round 1: no group bits
 };
+
+// round-1 key: the rotation's 16 bytes from depth d-1, low LOGS bits = slot
+template <int W>
+__device__ __forceinline__ void make_key1(uint32_t slot, uint64_t w0, uint64_t w1, uint64_t& kh, uint64_t& kl)
+{
+    kh = w0;
+    kl = (w1 & ~JobGeom<W>::SMASK) | slot;
+}
 
 // key = group | the rotation's 16 bytes (w0:w1) shifted right by GBITS, low LOGS bits = slot
 template <int W>
@@ -993,9 +1036,30 @@ __device__ __forceinline__ void make_key(uint32_t grp, uint32_t slot, uint64_t w
     kl      = (((w0 << (64 - G::GBITS)) | (w1 >> G::GBITS)) & ~G::SMASK) | slot;
 }
 
+#ifdef BRA_PHASES
+// Phase profile of the job kernels (make EXTRA=-DBRA_PHASES): [wave jobs, workgroup jobs] x
+// {setup, gathers, sorts, groups+outputs, compaction, rounds, sum of P, jobs}; shader cycles of
+// the job's first wave.
+__device__ unsigned long long g_phase[2][8];
+#define PH_T(v) const unsigned long long v = (wj == 0) ? clock64() : 0
+#define PH_ADD(i, x)                                                                \
+    do                                                                              \
+    {                                                                               \
+        if (wj == 0 && lane_id() == 0)                                              \
+            atomicAdd(&g_phase[W > 1][i], (unsigned long long) (x));               \
+    } while (0)
+#else
+#define PH_T(v)
+#define PH_ADD(i, x)
+#endif
+
 template <uint32_t MODE, int W>
 __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj)
 {
+    PH_T(t_start);
+#ifdef BRA_PHASES
+    unsigned long long t_setup = t_start;
+#endif
     using G                 = JobGeom<W>;
     const int       lane    = lane_id();
     const BlockDesc BD      = a.blocks[J.block];
@@ -1013,6 +1077,9 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     if (!BRA_DCHECK(T <= 256u * W && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job mode %u W %d start %u len %u block %u off %llu blen %u",
                     MODE, W, J.start, T, J.block, (unsigned long long) BD.off, BD.len))
         T = 0;
+    // Round 1.  STRING: all elements share their first d-1 bytes (one parent bucket), so the key
+    // is the rotation's bytes from depth d-1 -- its first byte orders the packed sub-buckets, no
+    // group id and no carried key needed.  RANK: the 32-bit rank key.
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -1033,38 +1100,34 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             }
             else
             {
-                // sub-bucket = digit at depth d-1 (elements of one digit are contiguous)
-                kh[r] = (K[J.start + c] >> (56 - 8 * (J.d - 1 - J.kd))) & 0xFF;
-                kl[r] = 0;
-            }
-        }
-        S.v[c] = v[r];
-    }
-    if (MODE == MODE_STRING)
-    {
-        // round 1 groups = sub-buckets; keys = group | rotation bytes from depth d | slot
-        job_groups<W>(kh, kl, T, S, wj, g, gend, tied);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            const uint32_t c = wj * 256 + lane * 4 + r;
-            if (c < T)
-            {
-                uint32_t st = (v[r] & 0xFFFFFFu) + (depth % BD.len);
+                uint32_t st = (v[r] & 0xFFFFFFu) + ((depth - 1) % BD.len);
                 if (st >= BD.len)
                     st -= BD.len;
                 uint64_t w0, w1;
                 load_key16(blk, BD.len, st, w0, w1);
-                make_key<W>(g[r], c, w0, w1, kh[r], kl[r]);
+                make_key1<W>(c, w0, w1, kh[r], kl[r]);
             }
-            else
-                kh[r] = kl[r] = ~0ull;
         }
+        S.v[c] = v[r];
     }
+#ifdef BRA_PHASES
+    t_setup = (wj == 0) ? clock64() : 0;
+    PH_ADD(0, t_setup - t_start);
+    PH_ADD(7, 1);
+#endif
     int P = 4;
     while ((uint32_t) P < T)
         P <<= 1;
+    PH_T(t_g1);
+#ifdef BRA_PHASES
+    if (MODE == MODE_STRING)
+        PH_ADD(1, t_g1 - t_setup);
+#endif
     job_sort<W>(kh, kl, P, S, wj);
+    PH_T(t_s1);
+    PH_ADD(2, t_s1 - t_g1);
+    PH_ADD(5, 1);
+    PH_ADD(6, P);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -1072,9 +1135,10 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         km[r] = kl[r] & ~G::SMASK;
     }
     if (MODE == MODE_STRING)
-        depth += G::ADV;
+        depth += G::ADV1 - 1;
     for (;;)
     {
+        PH_T(t_r0);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             S.pos[wj * 256 + lane * 4 + r] = (uint16_t) pos[r];
@@ -1122,6 +1186,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                     atomicExch(&a.ctr->overflow, 1u);
             }
         }
+        PH_T(t_r1);
+        PH_ADD(3, t_r1 - t_r0);
         if (finish)
             break;
         // ---- compact the tied slots; next round on the next ADV bytes ----
@@ -1138,6 +1204,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             }
         job_sync<W>();
         T = T2;
+        PH_T(t_r2);
+        PH_ADD(4, t_r2 - t_r1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -1163,7 +1231,13 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         P = 4;
         while ((uint32_t) P < T)
             P <<= 1;
+        PH_T(t_r3);
+        PH_ADD(1, t_r3 - t_r2);
         job_sort<W>(kh, kl, P, S, wj);
+        PH_T(t_r4);
+        PH_ADD(2, t_r4 - t_r3);
+        PH_ADD(5, 1);
+        PH_ADD(6, P);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -1426,7 +1500,7 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, JobArgs& ja, JobArgs& 
     for (int l = 0; l < 2; ++l)
         if (n[l])
             hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb,
-                               w.job_cnt + (size_t) l * nk);
+                               w.job_cnt + (size_t) l * nk); BRA_DSYNC(s);
     BRA_HIP_CHECK(hipMemcpyAsync(w.h_job_cnt, w.job_cnt, 2 * (size_t) nk * 4, hipMemcpyDeviceToHost, s));
     BRA_HIP_CHECK(hipStreamSynchronize(s));
     uint32_t* cur = w.h_job_cnt + 2 * (size_t) nk;  // cursors (exclusive prefix per list)
@@ -1448,7 +1522,7 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, JobArgs& ja, JobArgs& 
         if (n[l])
         {
             hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb,
-                               w.job_cnt + 2 * (size_t) nk + (size_t) l * nk, dst[l]);
+                               w.job_cnt + 2 * (size_t) nk + (size_t) l * nk, dst[l]); BRA_DSYNC(s);
             args[l]->jobs = dst[l];
         }
     BRA_HIP_CHECK(hipGetLastError());
@@ -1469,6 +1543,10 @@ static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
         hipLaunchKernelGGL((k_mjobs<MODE, 4>), g, dim3(64 * 4), sizeof(JobLds<4>), s, a);
     else
         hipLaunchKernelGGL((k_mjobs<MODE, 2>), g, dim3(64 * 2), sizeof(JobLds<2>), s, a);
+#ifdef BRA_DEBUG
+    if (hipStreamSynchronize(s) != hipSuccess)
+        fprintf(stderr, "[bra dsync] k_mjobs mode %u waves %d n %u xcd_major %u failed\n", MODE, waves, n, a.xcd_major);
+#endif
 }
 
 static void ws_free(BwtWorkspace& w)
@@ -1592,11 +1670,11 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
     const int    grid = w.grid;
     while (nbig > 0)
     {
-        hipLaunchKernelGGL(k_level_start, dim3(1), dim3(1), 0, s, w.ctr);
+        hipLaunchKernelGGL(k_level_start, dim3(1), dim3(1), 0, s, w.ctr); BRA_DSYNC(s);
         {
             BRA_PROF(P_BWT_HIST, s);
             hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket[cur], w.ctr, w.key[0],
-                               w.key[1], w.pay[0], w.pay[1], w.tile_hist, ntiles);
+                               w.key[1], w.pay[0], w.pay[1], w.tile_hist, ntiles); BRA_DSYNC(s);
         }
         ScanArgs a{d_blocks, w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
                    w.cap_big,   w.tile_bucket[cur ^ 1],   w.cap_tiles, w.jobs,       w.cap_jobs,
@@ -1604,12 +1682,12 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                    (uint32_t) (g_prof != nullptr), w.mjob_max()};
         {
             BRA_PROF(P_BWT_SCAN, s);
-            hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(div_up(nbig, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a);
+            hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(div_up(nbig, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
         }
         {
             BRA_PROF(P_BWT_SCATTER, s);
             hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
-                               w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles);
+                               w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles); BRA_DSYNC(s);
         }
         BRA_HIP_CHECK(hipGetLastError());
         if (!read_ctr(w, s))
@@ -1698,19 +1776,19 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, nblocks, s));
     {
         BRA_PROF(P_BWT_L0HIST, s);
-        hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist);
+        hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist); BRA_DSYNC(s);
     }
     ScanArgs a0{d_blocks, w.big[1],  nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max()};
     {
         BRA_PROF(P_BWT_SCAN, s);
-        hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(div_up(nblocks, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a0);
+        hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(div_up(nblocks, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a0); BRA_DSYNC(s);
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
         hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), tile_stage_bytes() + TILE + 16, s, d_in, d_blocks,
-                           w.l0tiles, nt0, w.tile_off, w.key[0], w.pay[0]);
+                           w.l0tiles, nt0, w.tile_off, w.key[0], w.pay[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
@@ -1735,7 +1813,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     if (njobs)
     {
         BRA_PROF(P_BWT_JOBS, s);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), 8192u))), dim3(256), 0, s, ja);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), 8192u))), dim3(256), 0, s, ja); BRA_DSYNC(s);
     }
     if (nmjobs)
     {
@@ -1745,6 +1823,17 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
         return false;
+#ifdef BRA_PHASES
+    {
+        unsigned long long ph[2][8];
+        BRA_HIP_CHECK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof ph));
+        for (int k = 0; k < 2; ++k)
+            fprintf(stderr, "[phases %s] setup %llu gather %llu sort %llu groups+out %llu compact %llu | rounds %llu sumP %llu jobs %llu\n",
+                    k ? "mjobs" : "jobs", ph[k][0], ph[k][1], ph[k][2], ph[k][3], ph[k][4], ph[k][5], ph[k][6], ph[k][7]);
+        std::memset(ph, 0, sizeof ph);
+        BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof ph));
+    }
+#endif
     // read key+payload, write SA entry + L byte (split by the elements each kind of job covers)
     prof_bytes(P_BWT_JOBS, 17.0 * ((double) N - (double) w.h_ctr->n_melems));
     prof_bytes(P_BWT_MJOBS, 17.0 * (double) w.h_ctr->n_melems);
@@ -1755,23 +1844,23 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return true;
     BRA_PROF(P_BWT_FALLBACK, s);
     int gcur = 0;
-    hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pay[0], w.pay[1], w.fsa);
+    hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pay[0], w.pay[1], w.fsa); BRA_DSYNC(s);
     // mark blocks, build ranks: singletons rank = own slot, group members = group start
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
-                       w.flag);  // sets the flags (its rank writes are redone below)
-    hipLaunchKernelGGL(k_isa_init, dim3(64, std::min<uint32_t>(nblocks, 65535u)), dim3(256), 0, s, d_blocks, w.flag, nblocks, w.fsa, w.isa);
+                       w.flag); BRA_DSYNC(s);  // sets the flags (its rank writes are redone below)
+    hipLaunchKernelGGL(k_isa_init, dim3(64, std::min<uint32_t>(nblocks, 65535u)), dim3(256), 0, s, d_blocks, w.flag, nblocks, w.fsa, w.isa); BRA_DSYNC(s);
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
-                       w.flag);
+                       w.flag); BRA_DSYNC(s);
     uint32_t hmin    = w.h_ctr->hmin;
     for (int round = 0; round < 64 && ng > 0; ++round)
     {
         // keys for this round (every read of isa happens here, before any rank update)
         hipLaunchKernelGGL(k_rank_keys, dim3(std::min<uint32_t>(ng, 8192u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, d_in, w.fsa,
-                           w.isa, w.key[0], w.pay[0]);
+                           w.isa, w.key[0], w.pay[0]); BRA_DSYNC(s);
         if (!reset_ctr(w, s))
             return false;
         hipLaunchKernelGGL(k_groups_to_work, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng,
-                           w.big[0], w.cap_big, w.tile_bucket[0], w.cap_tiles, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs, w.mjob_max(), w.ctr);
+                           w.big[0], w.cap_big, w.tile_bucket[0], w.cap_tiles, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs, w.mjob_max(), w.ctr); BRA_DSYNC(s);
         if (!read_ctr(w, s))
             return false;
         Group* gnext = w.groups[gcur ^ 1];
@@ -1785,9 +1874,9 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
                    w.ctr,  0,  hmin, 0, {}};
         if (ng_big)
             hipLaunchKernelGGL(k_rank_flush, dim3(std::min<uint32_t>(ng_big, 4096u)), dim3(256), 0, s, gnext, ng_big, d_blocks, w.pay[0],
-                               w.pay[1], w.fsa, d_L, w.isa, d_pi);
+                               w.pay[1], w.fsa, d_L, w.isa, d_pi); BRA_DSYNC(s);
         if (nj)
-            hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr);
+            hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr); BRA_DSYNC(s);
         const uint32_t nmj = w.h_ctr->n_mjobs;
         if (nmj)
         {
@@ -1838,7 +1927,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return false;
     }
     hipLaunchKernelGGL(k_pi_from_isa, dim3(std::min<uint32_t>(div_up(nblocks, 256), 1024u)), dim3(256), 0, s, d_blocks, w.flag, nblocks,
-                       w.isa, d_pi);
+                       w.isa, d_pi); BRA_DSYNC(s);
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }
