@@ -78,7 +78,10 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
     }
 }
 
-// LDS table of thread t, dword w (4 table entries, little-endian) lives at tbl[w * TPB + t].
+// Encode: the table of thread t occupies TSTRIDE dwords at tbl[t * TSTRIDE] (dword w holds entries
+// 4w..4w+3, little-endian); the 4-dword pad makes 16-byte reads of 16 consecutive lanes hit
+// disjoint banks.  (Decode keeps its own interleaved layout, tbl[w * TPB + t].)
+constexpr uint32_t TSTRIDE = 68;
 __device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st, uint32_t* tbl, uint32_t owner)
 {
     // K(c) = last-occurrence time + 256 for seen symbols, 255 - c for unseen: the table is the
@@ -97,81 +100,104 @@ __device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st,
         v[r]             = c;
     }
     wave_bitonic_sort4(k, v, 256);
-    tbl[lane * TPB + owner] = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
+    tbl[owner * TSTRIDE + lane] = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
 }
 
-// One MTF step on a table whose first RK dwords (4 entries each, entry 0 = low byte) live in
-// registers and the rest in LDS (tbl[w * TPB], w >= RK).  Returns the symbol's position.
-template <int RK>
-__device__ __forceinline__ uint32_t mtf_step(uint32_t (&R)[RK], uint32_t* tbl, uint32_t c)
+// Shift one table dword up by one entry: entry 0 becomes the top entry of the previous dword.
+__device__ __forceinline__ uint32_t shift1(uint32_t cur, uint32_t below_top) { return (cur << 8) | below_top; }
+
+// Partial shift of the dword holding the symbol at byte b: entries [0, b] move up by one (the
+// symbol's own slot is overwritten), entries above b stay.
+__device__ __forceinline__ uint32_t shift_upto(uint32_t cur, uint32_t below_top, uint32_t b)
+{
+    const uint32_t keep = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
+    return (cur & keep) | (((cur << 8) | below_top) & ~keep);
+}
+
+// One MTF step.  Entries 0..15 live in registers R; entries 16..255 in this thread's LDS table,
+// read, checked and written back shifted 16 entries at a time (one ds_read_b128 / ds_write_b128
+// pair per chunk) until the chunk holding the symbol.  Returns the symbol's position.
+__device__ __forceinline__ uint32_t mtf_step(uint32_t (&R)[4], uint32_t* tbl, uint32_t c)
 {
     const uint32_t cc = c * 0x01010101u;
-    uint32_t       w = 0, z = 0;
-    bool           hit = false;
+    uint32_t       z[4];
 #pragma unroll
-    for (int k = 0; k < RK; ++k)
+    for (int k = 0; k < 4; ++k)
+        z[k] = haszero8(R[k] ^ cc);
+    if (z[0] | z[1] | z[2] | z[3])
     {
-        const uint32_t zk = haszero8(R[k] ^ cc);
-        if (!hit && zk)
+        const uint32_t k = z[0] ? 0 : z[1] ? 1 : z[2] ? 2 : 3;
+        const uint32_t zz = z[0] ? z[0] : z[1] ? z[1] : z[2] ? z[2] : z[3];
+        const uint32_t b = (uint32_t) __builtin_ctz(zz) >> 3;
+        uint32_t       top = c;  // entry entering dword 0
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
         {
-            hit = true;
-            w   = k;
-            z   = zk;
+            const uint32_t cur = R[q], ntop = cur >> 24;
+            if ((uint32_t) q < k)
+                R[q] = shift1(cur, top);
+            else if ((uint32_t) q == k)
+                R[q] = shift_upto(cur, top, b);
+            top = ntop;
         }
+        return k * 4 + b;
     }
-    uint32_t b;
-    if (hit)
-    {
-        b                   = (uint32_t) __builtin_ctz(z) >> 3;
-        const uint32_t keep = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
+    // not in the register chunk: shift it fully, carry its top entry into the LDS chunks
+    uint32_t top = c;
 #pragma unroll
-        for (int k = RK - 1; k >= 0; --k)
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t cur = R[q], ntop = cur >> 24;
+        R[q]                = shift1(cur, top);
+        top                 = ntop;
+    }
+    for (uint32_t ch = 1; ch < 16; ++ch)
+    {
+        uint4          v = *reinterpret_cast<const uint4*>(tbl + ch * 4);
+        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+        uint32_t       zc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            zc[k] = haszero8(d[k] ^ cc);
+        uint32_t o[4];
+        if (zc[0] | zc[1] | zc[2] | zc[3])
         {
-            const uint32_t below   = k ? R[k - 1] : c << 24;
-            const uint32_t shifted = (R[k] << 8) | (below >> 24);
-            if ((uint32_t) k < w)
-                R[k] = shifted;
-            else if ((uint32_t) k == w)
-                R[k] = (R[k] & keep) | (shifted & ~keep);
-        }
-        return w * 4 + b;
-    }
-    uint32_t cur = 0;
-    for (w = RK; w < 64; ++w)  // always found: the table is a permutation of 0..255
-    {
-        cur = tbl[w * TPB];
-        z   = haszero8(cur ^ cc);
-        if (z)
-            break;
-    }
-    b                   = (uint32_t) __builtin_ctz(z) >> 3;
-    const uint32_t keep = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
-    uint32_t       below = (w > RK) ? tbl[(w - 1) * TPB] : R[RK - 1];
-    tbl[w * TPB]         = (cur & keep) | (((cur << 8) | (below >> 24)) & ~keep);
-    for (uint32_t x = w - 1; x >= RK; --x)
-    {
-        const uint32_t lo = (x > RK) ? tbl[(x - 1) * TPB] : R[RK - 1];
-        tbl[x * TPB]      = (below << 8) | (lo >> 24);
-        below             = lo;
-    }
+            const uint32_t k  = zc[0] ? 0 : zc[1] ? 1 : zc[2] ? 2 : 3;
+            const uint32_t zz = zc[0] ? zc[0] : zc[1] ? zc[1] : zc[2] ? zc[2] : zc[3];
+            const uint32_t b  = (uint32_t) __builtin_ctz(zz) >> 3;
 #pragma unroll
-    for (int k = RK - 1; k >= 0; --k)
-        R[k] = (R[k] << 8) | ((k ? R[k - 1] : c << 24) >> 24);
-    return w * 4 + b;
+            for (int q = 0; q < 4; ++q)
+            {
+                const uint32_t ntop = d[q] >> 24;
+                o[q]                = ((uint32_t) q < k) ? shift1(d[q], top) : ((uint32_t) q == k) ? shift_upto(d[q], top, b) : d[q];
+                top                 = ntop;
+            }
+            *reinterpret_cast<uint4*>(tbl + ch * 4) = make_uint4(o[0], o[1], o[2], o[3]);
+            return ch * 16 + k * 4 + b;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            const uint32_t ntop = d[q] >> 24;
+            o[q]                = shift1(d[q], top);
+            top                 = ntop;
+        }
+        *reinterpret_cast<uint4*>(tbl + ch * 4) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    return 255;  // unreachable: the table is a permutation of 0..255
 }
 
-// Sequential MTF of one segment on this thread's table (tbl = its column).  Input is read and
-// output written 16 bytes at a time (the next 16 input bytes are loaded before the current ones
-// are coded) whenever the segment is 16-byte aligned; the ragged tail goes byte by byte.
+// Sequential MTF of one segment on this thread's table (tbl = its TSTRIDE dwords).  Input is read
+// and output written 16 bytes at a time (the next 16 input bytes are loaded before the current
+// ones are coded) whenever the segment is 16-byte aligned; the ragged tail goes byte by byte.
 __device__ __forceinline__ void mtf_encode_segment(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece P, uint32_t* tbl)
 {
-    constexpr int  RK  = 2;
     const uint8_t* src = in + P.off;
     uint8_t*       dst = out + P.off;
-    uint32_t       R[RK];
+    uint32_t       R[4];
 #pragma unroll
-    for (int k = 0; k < RK; ++k)
-        R[k] = tbl[k * TPB];
+    for (int k = 0; k < 4; ++k)
+        R[k] = tbl[k];
     uint32_t i = 0;
     if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0 && P.len >= 16)
     {
@@ -186,19 +212,19 @@ __device__ __forceinline__ void mtf_encode_segment(const uint8_t* __restrict__ i
             uint32_t       ow[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int j = 0; j < 16; ++j)
-                ow[j >> 2] |= mtf_step<RK>(R, tbl, (iw[j >> 2] >> (8 * (j & 3))) & 0xFF) << (8 * (j & 3));
+                ow[j >> 2] |= mtf_step(R, tbl, (iw[j >> 2] >> (8 * (j & 3))) & 0xFF) << (8 * (j & 3));
             reinterpret_cast<uint4*>(dst)[v] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
         i = nv * 16;
     }
     for (; i < P.len; ++i)
-        dst[i] = (uint8_t) mtf_step<RK>(R, tbl, src[i]);
+        dst[i] = (uint8_t) mtf_step(R, tbl, src[i]);
 }
 
 __global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
                                                     uint32_t nseg, const int32_t* __restrict__ state)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];  // 64 * TPB dwords
+    extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];  // TSTRIDE * TPB dwords
     const uint32_t t    = threadIdx.x;
     const int      lane = lane_id();
     const uint32_t wave = t >> 6;
@@ -212,14 +238,14 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ 
             if (s >= nseg)
                 break;
             if (segs[s].start == 0)
-                tbl[lane * TPB + owner] = (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u;
+                tbl[owner * TSTRIDE + lane] = (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u;
             else
                 build_table_wave(state + (size_t) s * 256, tbl, owner);
         }
         __syncthreads();
         const uint32_t s = g0 + t;
         if (s < nseg)
-            mtf_encode_segment(in, out, segs[s], tbl + t);
+            mtf_encode_segment(in, out, segs[s], tbl + t * TSTRIDE);
         __syncthreads();
     }
 }
@@ -334,12 +360,11 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
         hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
                            nblocks, st);
     }
-    const size_t lds = 64 * TPB * 4;
+    const size_t lds = (size_t) TSTRIDE * TPB * 4;
     static bool  attr = false;
     if (!attr)
     {
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         attr = true;
     }
     {
@@ -370,7 +395,6 @@ bool mtf_decode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, uin
     static bool  attr = false;
     if (!attr)
     {
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         attr = true;
     }
