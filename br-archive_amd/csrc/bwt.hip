@@ -135,8 +135,17 @@ __global__ void __launch_bounds__(TPB) k_l0_hist(const uint8_t* __restrict__ in,
         const BlockDesc B   = blocks[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
         const uint8_t*  p   = in + B.off + T.start;
-        for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
-            atomicAdd(&h[p[i]], 1u);
+        if (cnt == TILE && (((uintptr_t) p) & 15) == 0)
+        {
+            const uint4    q    = reinterpret_cast<const uint4*>(p)[threadIdx.x];  // 16 bytes per thread
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                atomicAdd(&h[(w[i >> 2] >> (8 * (i & 3))) & 0xFF], 1u);
+        }
+        else
+            for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
+                atomicAdd(&h[p[i]], 1u);
         __syncthreads();
         tile_hist[(size_t) t * 256 + threadIdx.x] = h[threadIdx.x];
         __syncthreads();
@@ -585,21 +594,30 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStage& S   = *reinterpret_cast<TileStage*>(smem);
-    uint8_t*   win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStage));  // TILE + 16 bytes
+    uint8_t*   win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStage));  // TILE + 32 bytes, 16-aligned
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile    T   = tiles[t];
         const BlockDesc B   = blocks[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
         const uint8_t*  blk = in + B.off;
-        // window of bytes [start-1, start+cnt+7], cyclic in the block
-        for (uint32_t i = threadIdx.x; i < cnt + 9; i += TPB)
+        // window: win[i + 15] = byte (start - 1 + i) of the block, cyclic; i in [0, cnt + 9)
+        const uint8_t* src = blk + T.start;
+        if (T.start >= 16 && T.start + cnt + 16 <= B.len && (((uintptr_t) src) & 15) == 0)
         {
-            int64_t q = (int64_t) T.start - 1 + i;
-            q %= (int64_t) B.len;
-            if (q < 0)
-                q += B.len;
-            win[i] = blk[q];
+            // interior tile: 16-byte copies of [start - 16, start + cnt + 16)
+            for (uint32_t i = threadIdx.x; i < (cnt + 32) / 16; i += TPB)
+                reinterpret_cast<uint4*>(win)[i] = reinterpret_cast<const uint4*>(src - 16)[i];
+        }
+        else
+        {
+            for (uint32_t i = threadIdx.x; i < cnt + 9; i += TPB)
+            {
+                uint32_t q = T.start + i + B.len - 1;  // >= 0, < 3 * len for any block length
+                while (q >= B.len)
+                    q -= B.len;
+                win[i + 15] = blk[q];
+            }
         }
         S.cnt[threadIdx.x]  = 0;
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x];
@@ -612,13 +630,15 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
             const uint32_t e = threadIdx.x + i * TPB;
             if (e < cnt)
             {
-                uint64_t kk = 0;
-#pragma unroll
-                for (int b = 0; b < 8; ++b)
-                    kk = (kk << 8) | win[e + 1 + b];
-                k[i]  = kk;
-                v[i]  = ((uint32_t) win[e] << 24) | (T.start + e);
-                dg[i] = (uint32_t) (kk >> 56);
+                // bytes [e + 16, e + 24) of the window = rotation bytes 0..7; win[e + 15] = previous byte
+                const uint32_t  o  = e + 16;
+                const uint32_t* w4 = reinterpret_cast<const uint32_t*>(win) + (o >> 2);
+                const uint32_t  a0 = w4[0], a1 = w4[1], a2 = w4[2], sh = o & 3;
+                const uint32_t  lo = __builtin_amdgcn_alignbyte(a1, a0, sh), hi = __builtin_amdgcn_alignbyte(a2, a1, sh);
+                const uint64_t  kk = __builtin_bswap64(((uint64_t) hi << 32) | lo);
+                k[i]               = kk;
+                v[i]               = ((uint32_t) win[e + 15] << 24) | (T.start + e);
+                dg[i]              = (uint32_t) (kk >> 56);
             }
         }
         stage_and_write(S, k, v, dg, cnt, 0, 0, okey, opay, B.off, B.off + B.len);
@@ -1272,20 +1292,26 @@ __global__ void __launch_bounds__(64 * W) k_mjobs(JobArgs a)
 }
 
 // Block-major, XCD-major job order: key(b) = (b % 8) * kb + b / 8.
-__device__ __forceinline__ uint32_t job_key(uint32_t b, uint32_t kb) { return (b & 7u) * kb + (b >> 3); }
-
-__global__ void k_job_count(const Job* __restrict__ jobs, uint32_t n, uint32_t kb, uint32_t* __restrict__ cnt)
+// Size class first (jobs longer than split_len after the others; split_len 0 = one class).
+__device__ __forceinline__ uint32_t job_key(const Job& J, uint32_t kb, uint32_t split_len)
 {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
-        atomicAdd(&cnt[job_key(jobs[j].block, kb)], 1u);
+    const uint32_t sc = (split_len && J.len > split_len) ? 1u : 0u;
+    return sc * 8 * kb + (J.block & 7u) * kb + (J.block >> 3);
 }
 
-__global__ void k_job_scatter(const Job* __restrict__ in, uint32_t n, uint32_t kb, uint32_t* __restrict__ cursor, Job* __restrict__ out)
+__global__ void k_job_count(const Job* __restrict__ jobs, uint32_t n, uint32_t kb, uint32_t split_len, uint32_t* __restrict__ cnt)
+{
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+        atomicAdd(&cnt[job_key(jobs[j], kb, split_len)], 1u);
+}
+
+__global__ void k_job_scatter(const Job* __restrict__ in, uint32_t n, uint32_t kb, uint32_t split_len, uint32_t* __restrict__ cursor,
+                              Job* __restrict__ out)
 {
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
     {
         const Job J = in[j];
-        out[atomicAdd(&cursor[job_key(J.block, kb)], 1u)] = J;
+        out[atomicAdd(&cursor[job_key(J, kb, split_len)], 1u)] = J;
     }
 }
 
@@ -1475,7 +1501,7 @@ struct BwtWorkspace
     Job*      mjobs          = nullptr;
     Job*      jobs_sorted    = nullptr;  // block-major, XCD-major copies (order_jobs)
     Job*      mjobs_sorted   = nullptr;
-    uint32_t* job_cnt        = nullptr;  // 2 lists x 8 * ceil(blocks / 8) keys, then the cursors
+    uint32_t* job_cnt        = nullptr;  // 2 lists x 2 size classes x 8 * ceil(blocks / 8) keys, then the cursors
     uint32_t* h_job_cnt      = nullptr;  // pinned: counts back, cursors out
     Group*    groups[2]      = {nullptr, nullptr};
     Counters* ctr            = nullptr;
@@ -1488,42 +1514,64 @@ struct BwtWorkspace
 };
 
 // Reorder the wave-job and workgroup-job lists block-major per XCD (see job_range): count jobs per
-// key on the device, prefix on the host (the counts come back with one small copy), scatter.
-static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, JobArgs& ja, JobArgs& jm, hipStream_t s)
+// key on the device, prefix on the host (the counts come back with one small copy), scatter.  The
+// workgroup jobs are also split into two size classes (<= half the workgroup-job size, larger):
+// out[0] wave jobs, out[1] small workgroup jobs, out[2] large ones.
+static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[3], hipStream_t s)
 {
-    const uint32_t kb = div_up(nblocks, 8), nk = 8 * kb;
-    const uint32_t n[2] = {ja.njobs, jm.njobs};
-    const Job*     src[2] = {w.jobs, w.mjobs};
-    Job*           dst[2] = {w.jobs_sorted, w.mjobs_sorted};
-    JobArgs*       args[2] = {&ja, &jm};
-    BRA_HIP_CHECK(hipMemsetAsync(w.job_cnt, 0, 2 * (size_t) nk * 4, s));
+    const uint32_t kb = div_up(nblocks, 8), nk = 8 * kb;  // keys per size class
+    const uint32_t n[2]     = {ja.njobs, jm.njobs};
+    const uint32_t split[2] = {0, w.mjob_max() / 2};
+    const Job*     src[2]   = {w.jobs, w.mjobs};
+    Job*           dst[2]   = {w.jobs_sorted, w.mjobs_sorted};
+    uint32_t*      dcnt     = w.job_cnt;                    // [list][class][nk] counts
+    uint32_t*      dcur     = w.job_cnt + 4 * (size_t) nk;  // cursors, same layout
+    BRA_HIP_CHECK(hipMemsetAsync(dcnt, 0, 4 * (size_t) nk * 4, s));
     for (int l = 0; l < 2; ++l)
         if (n[l])
-            hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb,
-                               w.job_cnt + (size_t) l * nk); BRA_DSYNC(s);
-    BRA_HIP_CHECK(hipMemcpyAsync(w.h_job_cnt, w.job_cnt, 2 * (size_t) nk * 4, hipMemcpyDeviceToHost, s));
+        {
+            hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb, split[l],
+                               dcnt + (size_t) l * 2 * nk);
+            BRA_DSYNC(s);
+        }
+    BRA_HIP_CHECK(hipMemcpyAsync(w.h_job_cnt, dcnt, 4 * (size_t) nk * 4, hipMemcpyDeviceToHost, s));
     BRA_HIP_CHECK(hipStreamSynchronize(s));
-    uint32_t* cur = w.h_job_cnt + 2 * (size_t) nk;  // cursors (exclusive prefix per list)
+    uint32_t* cur = w.h_job_cnt + 4 * (size_t) nk;
+    out[0]        = ja;
+    out[1]        = jm;
+    out[2]        = jm;
     for (int l = 0; l < 2; ++l)
     {
         uint32_t run = 0;
-        for (uint32_t k = 0; k < nk; ++k)
+        for (uint32_t c = 0; c < 2; ++c)
         {
-            if (k % kb == 0)
-                args[l]->xseg[k / kb] = run;
-            cur[(size_t) l * nk + k] = run;
-            run += w.h_job_cnt[(size_t) l * nk + k];
+            const bool used = (l == 1 || c == 0);
+            JobArgs&   A    = out[l == 0 ? 0 : 1 + c];
+            uint32_t*  hc   = w.h_job_cnt + ((size_t) l * 2 + c) * nk;
+            uint32_t*  hu   = cur + ((size_t) l * 2 + c) * nk;
+            for (uint32_t k = 0; k < nk; ++k)
+            {
+                if (used && k % kb == 0)
+                    A.xseg[k / kb] = run;
+                hu[k] = run;
+                run += hc[k];
+            }
+            if (used)
+            {
+                A.xseg[8]   = run;
+                A.xcd_major = 1;
+                A.jobs      = dst[l];
+                A.njobs     = run - A.xseg[0];
+            }
         }
-        args[l]->xseg[8]   = run;
-        args[l]->xcd_major = 1;
     }
-    BRA_HIP_CHECK(hipMemcpyAsync(w.job_cnt + 2 * (size_t) nk, cur, 2 * (size_t) nk * 4, hipMemcpyHostToDevice, s));
+    BRA_HIP_CHECK(hipMemcpyAsync(dcur, cur, 4 * (size_t) nk * 4, hipMemcpyHostToDevice, s));
     for (int l = 0; l < 2; ++l)
         if (n[l])
         {
-            hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb,
-                               w.job_cnt + 2 * (size_t) nk + (size_t) l * nk, dst[l]); BRA_DSYNC(s);
-            args[l]->jobs = dst[l];
+            hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb, split[l],
+                               dcur + (size_t) l * 2 * nk, dst[l]);
+            BRA_DSYNC(s);
         }
     BRA_HIP_CHECK(hipGetLastError());
     return true;
@@ -1628,8 +1676,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     BRA_HIP_CHECK(hipMalloc(&w.jobs_sorted, (size_t) w.cap_jobs * sizeof(Job)));
     BRA_HIP_CHECK(hipMalloc(&w.mjobs_sorted, (size_t) w.cap_mjobs * sizeof(Job)));
     const size_t nkeys = 8 * (size_t) div_up(B, 8);
-    BRA_HIP_CHECK(hipMalloc(&w.job_cnt, 4 * nkeys * 4));
-    BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 4 * nkeys * 4, hipHostMallocDefault));
+    BRA_HIP_CHECK(hipMalloc(&w.job_cnt, 8 * nkeys * 4));
+    BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
     BRA_HIP_CHECK(hipMalloc(&w.l0tiles, (size_t) w.cap_l0 * sizeof(L0Tile)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault));
@@ -1750,7 +1798,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (lds + TILE + 16)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (lds + TILE + 48)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>)));
@@ -1787,7 +1835,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
-        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), tile_stage_bytes() + TILE + 16, s, d_in, d_blocks,
+        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), tile_stage_bytes() + TILE + 48, s, d_in, d_blocks,
                            w.l0tiles, nt0, w.tile_off, w.key[0], w.pay[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
@@ -1808,17 +1856,24 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     JobArgs        jm     = ja;
     jm.jobs               = w.mjobs;
     jm.njobs              = nmjobs;
-    if (!order_jobs(w, nblocks, ja, jm, s))
+    JobArgs ord[3];
+    if (!order_jobs(w, nblocks, ja, jm, ord, s))
         return false;
     if (njobs)
     {
         BRA_PROF(P_BWT_JOBS, s);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), 8192u))), dim3(256), 0, s, ja); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), 8192u))), dim3(256), 0, s, ord[0]);
+        BRA_DSYNC(s);
     }
     if (nmjobs)
     {
+        // workgroup jobs of at most half the size run on half the waves
         BRA_PROF(P_BWT_MJOBS, s);
-        launch_mjobs<MODE_STRING>(w.mj_waves, nmjobs, jm, s);
+        const int half = w.mj_waves / 2;
+        if (ord[1].njobs)
+            launch_mjobs<MODE_STRING>(half >= 2 ? half : w.mj_waves, ord[1].njobs, ord[1], s);
+        if (ord[2].njobs)
+            launch_mjobs<MODE_STRING>(w.mj_waves, ord[2].njobs, ord[2], s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
