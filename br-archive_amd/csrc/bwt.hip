@@ -60,6 +60,9 @@ constexpr int      MJ_WAVES_DEF = 4;    // waves of a workgroup job (2, 4, 8 or 
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
+#ifndef JOB_MIN_WAVES
+#define JOB_MIN_WAVES 1                  // min waves per SIMD the job kernels are compiled for (1 = compiler choice; 6 and 8 measured slower)
+#endif
 
 enum : uint32_t { MODE_STRING = 0, MODE_RANK = 1 };
 
@@ -1269,7 +1272,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
 }
 
 template <uint32_t MODE>
-__global__ void __launch_bounds__(256) k_jobs(JobArgs a)
+__global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
 {
     __shared__ JobLds<1> lds[4];
     const int      wl = threadIdx.x >> 6;
@@ -1279,7 +1282,7 @@ __global__ void __launch_bounds__(256) k_jobs(JobArgs a)
 }
 
 template <uint32_t MODE, int W>
-__global__ void __launch_bounds__(64 * W) k_mjobs(JobArgs a)
+__global__ void __launch_bounds__(64 * W, JOB_MIN_WAVES) k_mjobs(JobArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     JobLds<W>&     S = *reinterpret_cast<JobLds<W>*>(smem);
@@ -1510,6 +1513,7 @@ struct BwtWorkspace
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
     int       grid = 2048;
     int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
+    uint32_t  jobs_grid = 8192;         // workgroups of the wave-job launch (env BRA_JOBS_GRID)
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
@@ -1579,10 +1583,12 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, con
 
 static uint32_t round8(uint32_t g) { return (g + 7u) & ~7u; }
 
+static uint32_t g_mjobs_grid = 2048;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID)
+
 template <uint32_t MODE>
 static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
 {
-    const dim3 g(round8(std::min<uint32_t>(n, 2048u)));
+    const dim3 g(round8(std::min<uint32_t>(n, g_mjobs_grid)));
     if (waves == 16)
         hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>), s, a);
     else if (waves == 8)
@@ -1643,6 +1649,10 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
         const int v = atoi(e);
         w.mj_waves  = (v == 0 || v == 2 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
     }
+    if (const char* e = getenv("BRA_JOBS_GRID"))
+        w.jobs_grid = std::max(8, atoi(e));
+    if (const char* e = getenv("BRA_MJOBS_GRID"))
+        g_mjobs_grid = std::max(8, atoi(e));
     if (n <= w.cap_n && nblocks <= w.cap_blocks)
         return true;
     ws_free(w);
@@ -1862,7 +1872,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     if (njobs)
     {
         BRA_PROF(P_BWT_JOBS, s);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), 8192u))), dim3(256), 0, s, ord[0]);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), w.jobs_grid))), dim3(256), 0, s, ord[0]);
         BRA_DSYNC(s);
     }
     if (nmjobs)
