@@ -353,7 +353,10 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
         hipMemcpyAsync(c->d_rle_size, rsz.data(), nb * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return -1;
     hipLaunchKernelGGL(k_split_headers, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, d_headers, nb, c->d_pi, c->d_meta);
-    if (!huff_decode_device(c->huf, c->d_meta, nb, d_payload, d_payload_off, c->d_rle, d_rbase, c->d_status, s))
+    std::vector<uint32_t> esz(nb);
+    for (uint32_t b = 0; b < nb; ++b)
+        esz[b] = hh[b].huffman.encoded_size;
+    if (!huff_decode_device(c->huf, c->d_meta, esz.data(), nb, d_payload, d_payload_off, c->d_rle, d_rbase, c->d_status, s))
         return -1;
     uint32_t* d_dec_size = c->d_hist;           // nb words
     uint32_t* d_nrec     = c->d_hist + nb;      // nb words
@@ -818,7 +821,8 @@ uint8_t* bra_huffman_decode(const bra_huffman_t* meta, const uint8_t* data, uint
         hipMemcpyAsync(c->d_off, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemcpyAsync(c->d_rle_base, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return nullptr;
-    if (!huff_decode_device(c->huf, c->d_meta, 1, c->d_io, c->d_off, c->d_tmp, c->d_rle_base, c->d_status, c->stream))
+    const uint32_t esz = meta->encoded_size;
+    if (!huff_decode_device(c->huf, c->d_meta, &esz, 1, c->d_io, c->d_off, c->d_tmp, c->d_rle_base, c->d_status, c->stream))
         return nullptr;
     uint32_t st = 1;
     if (!download(c, &st, c->d_status, 4) || st)

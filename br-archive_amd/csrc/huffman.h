@@ -26,9 +26,16 @@ struct HuffWorkspace
     uint8_t*  tree_sym   = nullptr;
     uint32_t* table      = nullptr;
     uint32_t* status     = nullptr;
-    uint32_t  cap_b = 0, cap_t = 0, cap_tree = 0;
+    void*     seg        = nullptr;  // segment-parallel decode: 3 x cap_seg segment records
+    uint32_t* seg_off    = nullptr;
+    uint32_t* seg_base   = nullptr;
+    uint64_t* end_pos    = nullptr;
+    uint32_t* flag       = nullptr;
+    uint32_t* h_flag     = nullptr;  // pinned: flag, then the segment bases
+    uint32_t  cap_b = 0, cap_t = 0, cap_tree = 0, cap_seg = 0, cap_segb = 0;
     bool      reserve(uint32_t nblocks, uint32_t ntiles);
     bool      reserve_tree(uint32_t nblocks);
+    bool      reserve_segs(uint32_t nseg, uint32_t nblocks);
     void      release();
 };
 
@@ -40,9 +47,9 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
                         uint64_t* h_total, hipStream_t s);
 
 // Decode every block: d_out + d_out_base[b] receives meta[b].orig_size bytes; d_status[b] != 0 on
-// a stream the reference would reject.
-bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, uint32_t nblocks, const uint8_t* d_payload, const uint64_t* d_payload_off,
-                        uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s);
+// a stream the reference would reject.  h_encoded_size: host copy of meta[b].encoded_size.
+bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint32_t* h_encoded_size, uint32_t nblocks, const uint8_t* d_payload,
+                        const uint64_t* d_payload_off, uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s);
 
 // Byte histograms of blocks (d_hist[b * 256 + c]).
 bool histogram_device(Tiling& tiling, const uint8_t* d_in, const BlockDesc* h_blocks, uint32_t nblocks, uint32_t* d_hist, hipStream_t s);

@@ -530,136 +530,301 @@ __global__ void k_huff_table(const int32_t* __restrict__ child, const uint8_t* _
     }
 }
 
-// One thread per block walks the stream; out_status[b] = 0 ok, else error.
-__global__ void k_huff_decode(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
-                              const uint64_t* __restrict__ payload_off, const int32_t* __restrict__ child, const uint8_t* __restrict__ sym,
-                              const uint32_t* __restrict__ table, const uint32_t* __restrict__ tree_status, uint8_t* __restrict__ out,
-                              const uint64_t* __restrict__ out_base, uint32_t* __restrict__ out_status)
+// ------------------------------------------------------------------------------------------------
+// Segment-parallel decode (self-synchronisation).  A block's bit stream is cut into SEG_BITS-bit
+// segments.  Pass 1 decodes every segment speculatively from its first bit up to the first
+// codeword boundary at or past its end.  Pass 2 restarts each segment from the previous segment's
+// exit (the true boundary) and walks the speculative path alongside until the two meet (Huffman
+// codes resynchronise within a few codewords): the counts after the meeting point are reused.  A
+// segment whose true path does not meet changes its exit, so pass 2 repeats until no exit moves.
+// Pass 3 prefix-sums the symbol counts per block, pass 4 decodes each segment's true path into
+// its output range, and a per-block pass applies the reference's end-of-stream rules (decode stops
+// at orig_size; a stream that ends early or holds a dead edge before it is rejected; :455-498).
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t SEG_BITS = 2048;
+
+__device__ __forceinline__ uint32_t hd_peek(const uint8_t* __restrict__ src, uint32_t nbytes, uint64_t p, int n)
+{
+    const uint32_t byt = (uint32_t) (p >> 3);
+    uint64_t       w;
+    if (byt + 8 <= nbytes)
+    {
+        const uintptr_t a  = (uintptr_t) (src + byt);
+        const uint64_t* q  = (const uint64_t*) (a & ~(uintptr_t) 7);
+        const uint32_t  sh = (uint32_t) (a & 7) * 8;
+        const uint64_t  lo = q[0];
+        const uint64_t  x  = sh ? (lo >> sh) | (q[1] << (64 - sh)) : lo;  // q[1] holds byte byt + 7 < nbytes
+        w                  = __builtin_bswap64(x);
+    }
+    else
+    {
+        w = 0;
+        for (int i = 0; i < 8; ++i)
+            w = (w << 8) | (byt + i < nbytes ? src[byt + i] : 0);
+    }
+    return (uint32_t) ((w << (p & 7)) >> (64 - n));
+}
+
+struct HdBlock
+{
+    const uint8_t*  src;
+    uint32_t        nbytes;
+    uint64_t        nbits;
+    const uint32_t* tb;
+    const int32_t*  ch;
+    const uint8_t*  sy;
+};
+
+__device__ __forceinline__ HdBlock hd_block(const HuffMetaRec* meta, const uint8_t* payload, const uint64_t* payload_off, const int32_t* child,
+                                            const uint8_t* sym, const uint32_t* table, uint32_t b)
+{
+    HdBlock B;
+    B.src    = payload + payload_off[b];
+    B.nbytes = meta[b].encoded_size;
+    B.nbits  = (uint64_t) B.nbytes * 8;
+    B.tb     = table + (size_t) b * (1u << PEEK);
+    B.ch     = child + (size_t) b * TREE_CAP * 2;
+    B.sy     = sym + (size_t) b * TREE_CAP;
+    return B;
+}
+
+// One codeword at pos (the reference's walk, :455-482, through the 11-bit table): true and the
+// symbol, or false on a dead edge / the end of the data.
+__device__ __forceinline__ bool hd_step(const HdBlock& B, uint64_t& pos, uint32_t& sym)
+{
+    if (pos >= B.nbits)
+        return false;
+    const uint32_t e    = B.tb[hd_peek(B.src, B.nbytes, pos, PEEK)];
+    const uint32_t kind = e >> 28, used = (e >> 24) & 15;
+    if (pos + used > B.nbits || kind == 1)
+    {
+        uint32_t cur = 0;
+        if (!(pos + used > B.nbits))
+        {
+            cur = e & 0xFFFFFF;
+            pos += PEEK;
+        }
+        while (pos < B.nbits)
+        {
+            const int nx = B.ch[2 * cur + (int) hd_peek(B.src, B.nbytes, pos, 1)];
+            ++pos;
+            if (nx < 0)
+                return false;
+            cur = (uint32_t) nx;
+            if (B.ch[2 * cur] < 0 && B.ch[2 * cur + 1] < 0)
+            {
+                sym = B.sy[cur];
+                return true;
+            }
+        }
+        return false;
+    }
+    if (kind == 2)
+        return false;
+    sym = e & 0xFFFFFF;
+    pos += used;
+    return true;
+}
+
+struct HdSeg
+{
+    uint32_t exit;   // bit position of the first codeword boundary at or past the segment end
+    uint32_t cnt;    // symbols decoded in the segment
+    uint32_t start;  // true start (pass 2)
+    uint32_t bad;    // the path met a dead edge / the end of the data
+};
+
+__device__ __forceinline__ uint32_t hd_seg_block(const uint32_t* __restrict__ seg_base, uint32_t nblocks, uint32_t g)
+{
+    uint32_t lo = 0, hi = nblocks;  // last b with seg_base[b] <= g
+    while (hi - lo > 1)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg_base[mid] <= g)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_hd_spec(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
+                          const uint64_t* __restrict__ payload_off, const int32_t* __restrict__ child, const uint8_t* __restrict__ sym,
+                          const uint32_t* __restrict__ table, const uint32_t* __restrict__ tree_status, const uint32_t* __restrict__ seg_base,
+                          uint32_t nseg, HdSeg* __restrict__ seg)
+{
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x)
+    {
+        const uint32_t b = hd_seg_block(seg_base, nblocks, g), j = g - seg_base[b];
+        HdSeg          S{0, 0, 0, 1};
+        if (!tree_status[b])
+        {
+            const HdBlock  B   = hd_block(meta, payload, payload_off, child, sym, table, b);
+            const uint64_t end = min((uint64_t) (j + 1) * SEG_BITS, B.nbits);
+            uint64_t       pos = (uint64_t) j * SEG_BITS;
+            uint32_t       cnt = 0, sy;
+            bool           ok  = true;
+            while (pos < end && (ok = hd_step(B, pos, sy)))
+                ++cnt;
+            S = HdSeg{(uint32_t) pos, cnt, (uint32_t) ((uint64_t) j * SEG_BITS), ok ? 0u : 1u};
+        }
+        seg[g] = S;
+    }
+}
+
+// Pass 2: cur[] -> nxt[]; *changed is set when a segment's exit moved.
+__global__ void k_hd_sync(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
+                          const uint64_t* __restrict__ payload_off, const int32_t* __restrict__ child, const uint8_t* __restrict__ sym,
+                          const uint32_t* __restrict__ table, const uint32_t* __restrict__ tree_status, const uint32_t* __restrict__ seg_base,
+                          uint32_t nseg, const HdSeg* __restrict__ spec, const HdSeg* __restrict__ cur, HdSeg* __restrict__ nxt,
+                          uint32_t* __restrict__ changed)
+{
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x)
+    {
+        const uint32_t b = hd_seg_block(seg_base, nblocks, g), j = g - seg_base[b];
+        if (j == 0 || tree_status[b])
+        {
+            nxt[g] = cur[g];
+            continue;
+        }
+        const HdSeg P = cur[g - 1];
+        HdSeg       R;
+        if (P.bad)
+            R = HdSeg{P.exit, 0, P.exit, 1};  // the true path already failed: nothing here counts
+        else
+        {
+            const HdBlock  B   = hd_block(meta, payload, payload_off, child, sym, table, b);
+            const uint64_t end = min((uint64_t) (j + 1) * SEG_BITS, B.nbits);
+            const HdSeg    Sp  = spec[g];
+            uint64_t       a = P.exit, q = (uint64_t) j * SEG_BITS;
+            uint32_t       ca = 0, cq = 0, sy;
+            bool           aok = true, qok = true, synced = false;
+            while (aok && a < end)
+            {
+                if (a == q && qok)
+                {
+                    synced = true;
+                    break;
+                }
+                if (qok && q < a)
+                {
+                    if (hd_step(B, q, sy))
+                        ++cq;
+                    else
+                        qok = false;
+                }
+                else if ((aok = hd_step(B, a, sy)))
+                    ++ca;
+            }
+            if (synced)
+                R = HdSeg{Sp.exit, Sp.cnt - cq + ca, (uint32_t) P.exit, Sp.bad};
+            else
+                R = HdSeg{(uint32_t) a, ca, (uint32_t) P.exit, aok ? 0u : 1u};
+        }
+        if (R.exit != cur[g].exit || R.bad != cur[g].bad)  // what the next segment starts from
+            atomicExch(changed, 1u);
+        nxt[g] = R;
+    }
+}
+
+// Pass 3: per block, exclusive prefix of the symbol counts; status for failures before orig_size.
+__global__ void __launch_bounds__(256) k_hd_prefix(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint32_t* __restrict__ tree_status,
+                                                   const uint32_t* __restrict__ seg_base, const HdSeg* __restrict__ seg, uint32_t* __restrict__ off,
+                                                   uint32_t* __restrict__ status)
+{
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t fail;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const uint32_t g0 = seg_base[b], n = seg_base[b + 1] - g0, osz = meta[b].orig_size;
+        if (threadIdx.x == 0)
+            fail = tree_status[b] ? 1u : 0u;
+        __syncthreads();
+        uint32_t run = 0;
+        for (uint32_t i0 = 0; i0 < n; i0 += 256)
+        {
+            const uint32_t i   = i0 + threadIdx.x;
+            const HdSeg    S   = i < n ? seg[g0 + i] : HdSeg{0, 0, 0, 0};
+            uint32_t       tot;
+            const uint32_t ex  = block256_exclusive_sum(S.cnt, tmp, &tot);
+            if (i < n)
+            {
+                off[g0 + i] = run + ex;
+                if (S.bad && run + ex + S.cnt < osz)
+                    atomicExch(&fail, 1u);  // the true path dies before symbol orig_size
+            }
+            run += tot;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            status[b] = (fail || run < osz) ? 1u : 0u;  // ran out of data before orig_size symbols
+        __syncthreads();
+    }
+}
+
+// Pass 4: decode each segment's true path into out[off, off + cnt), clipped at orig_size; the
+// segment holding symbol orig_size - 1 records where it ends.
+__global__ void k_hd_write(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
+                           const uint64_t* __restrict__ payload_off, const int32_t* __restrict__ child, const uint8_t* __restrict__ sym,
+                           const uint32_t* __restrict__ table, const uint32_t* __restrict__ status, const uint32_t* __restrict__ seg_base,
+                           uint32_t nseg, const HdSeg* __restrict__ seg, const uint32_t* __restrict__ off, uint8_t* __restrict__ out,
+                           const uint64_t* __restrict__ out_base, uint64_t* __restrict__ end_pos)
+{
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < nseg; g += gridDim.x * blockDim.x)
+    {
+        const uint32_t b = hd_seg_block(seg_base, nblocks, g);
+        if (status[b])
+            continue;
+        const HdSeg    S   = seg[g];
+        const uint32_t osz = meta[b].orig_size, o = off[g];
+        if (o >= osz || S.cnt == 0)
+            continue;
+        const HdBlock  B   = hd_block(meta, payload, payload_off, child, sym, table, b);
+        uint8_t*       dst = out + out_base[b];
+        uint64_t       pos = S.start;
+        const uint32_t n   = min(S.cnt, osz - o);
+        uint32_t       sy  = 0;
+        for (uint32_t i = 0; i < n; ++i)
+        {
+            (void) hd_step(B, pos, sy);
+            dst[o + i] = (uint8_t) sy;
+        }
+        if (o + n == osz)
+            end_pos[b] = pos;
+    }
+}
+
+// Pass 5: the reference's end-of-stream walk: it leaves the bit loop of the current byte and keeps
+// walking the remaining whole bytes; a completed symbol there would overrun its buffer (error), a
+// dead edge is an error, an unfinished walk is ignored.
+__global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
+                          const uint64_t* __restrict__ payload_off, const int32_t* __restrict__ child, const uint8_t* __restrict__ sym,
+                          const uint32_t* __restrict__ table, const uint64_t* __restrict__ end_pos, uint32_t* __restrict__ status)
 {
     for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
     {
-        if (tree_status[b])
-        {
-            out_status[b] = 1;
+        if (status[b])
             continue;
-        }
-        const HuffMetaRec& M     = meta[b];
-        const uint8_t*     src   = payload + payload_off[b];
-        const uint64_t     nbits = (uint64_t) M.encoded_size * 8;
-        const int32_t*     ch    = child + (size_t) b * TREE_CAP * 2;
-        const uint8_t*     sy    = sym + (size_t) b * TREE_CAP;
-        const uint32_t*    tb    = table + (size_t) b * (1u << PEEK);
-        uint8_t*           dst   = out + out_base[b];
-        uint64_t           pos   = 0;
-        uint32_t           k     = 0;
-        uint32_t           err   = 0;
-        // bit reader: 64-bit window starting at byte (pos >> 3)
-        auto peek = [&](uint64_t p, int n) -> uint32_t {
-            uint64_t w   = 0;
-            uint64_t byt = p >> 3;
-            for (int i = 0; i < 8; ++i)
-                w = (w << 8) | (byt + i < M.encoded_size ? src[byt + i] : 0);
-            return (uint32_t) ((w << (p & 7)) >> (64 - n));
-        };
-        while (k < M.orig_size)
+        const HdBlock B   = hd_block(meta, payload, payload_off, child, sym, table, b);
+        uint64_t      p2  = meta[b].orig_size ? ((end_pos[b] + 7) & ~7ull) : 0;
+        uint32_t      cur = 0, err = 0;
+        while (p2 < B.nbits)
         {
-            if (pos >= nbits)
-            {
-                err = 1;  // ran out of data (decoded_idx != orig_size)
-                break;
-            }
-            const uint32_t e    = tb[peek(pos, PEEK)];
-            const uint32_t kind = e >> 28, used = (e >> 24) & 15;
-            if (pos + used > nbits)
-            {
-                // the walk would read past the data: re-walk bit by bit to find where it stops
-                uint32_t cur = 0;
-                bool     leaf = false;
-                while (pos < nbits)
-                {
-                    const int nx = ch[2 * cur + (int) peek(pos, 1)];
-                    ++pos;
-                    if (nx < 0)
-                    {
-                        err = 1;
-                        break;
-                    }
-                    cur = (uint32_t) nx;
-                    if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
-                    {
-                        dst[k++] = sy[cur];
-                        leaf     = true;
-                        break;
-                    }
-                }
-                if (err || !leaf)
-                {
-                    err = 1;
-                    break;
-                }
-                continue;
-            }
-            if (kind == 0)
-            {
-                dst[k++] = (uint8_t) (e & 0xFFFFFF);
-                pos += used;
-            }
-            else if (kind == 2)
+            const int nx = B.ch[2 * cur + (int) hd_peek(B.src, B.nbytes, p2, 1)];
+            ++p2;
+            if (nx < 0)
             {
                 err = 1;
                 break;
             }
-            else
+            cur = (uint32_t) nx;
+            if (B.ch[2 * cur] < 0 && B.ch[2 * cur + 1] < 0)
             {
-                uint32_t cur = e & 0xFFFFFF;
-                pos += PEEK;
-                bool leaf = false;
-                while (pos < nbits)
-                {
-                    const int nx = ch[2 * cur + (int) peek(pos, 1)];
-                    ++pos;
-                    if (nx < 0)
-                        break;
-                    cur = (uint32_t) nx;
-                    if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
-                    {
-                        dst[k++] = sy[cur];
-                        leaf     = true;
-                        break;
-                    }
-                }
-                if (!leaf)
-                {
-                    err = 1;
-                    break;
-                }
+                err = 1;
+                break;
             }
         }
-        if (!err)
-        {
-            // the reference leaves the bit loop of the current byte and keeps walking the
-            // remaining whole bytes: a completed symbol there would overrun its buffer (error),
-            // a dead edge is an error, an unfinished walk is ignored.
-            uint64_t p2  = (pos + 7) & ~7ull;
-            uint32_t cur = 0;
-            while (p2 < nbits)
-            {
-                const int nx = ch[2 * cur + (int) peek(p2, 1)];
-                ++p2;
-                if (nx < 0)
-                {
-                    err = 1;
-                    break;
-                }
-                cur = (uint32_t) nx;
-                if (ch[2 * cur] < 0 && ch[2 * cur + 1] < 0)
-                {
-                    err = 1;
-                    break;
-                }
-            }
-        }
-        out_status[b] = err;
+        status[b] = err;
     }
 }
 
@@ -707,8 +872,41 @@ bool HuffWorkspace::reserve_tree(uint32_t nblocks)
     return true;
 }
 
+bool HuffWorkspace::reserve_segs(uint32_t nseg, uint32_t nblocks)
+{
+    if (nseg > cap_seg)
+    {
+        (void) hipFree(seg);
+        (void) hipFree(seg_off);
+        cap_seg = nseg + nseg / 4 + 256;
+        BRA_HIP_CHECK(hipMalloc(&seg, (size_t) cap_seg * 3 * sizeof(HdSeg)));
+        BRA_HIP_CHECK(hipMalloc(&seg_off, (size_t) cap_seg * 4));
+    }
+    if (nblocks + 1 > cap_segb)
+    {
+        (void) hipFree(seg_base);
+        (void) hipFree(end_pos);
+        (void) hipFree(flag);
+        cap_segb = nblocks + 64;
+        BRA_HIP_CHECK(hipMalloc(&seg_base, (size_t) cap_segb * 4));
+        BRA_HIP_CHECK(hipMalloc(&end_pos, (size_t) cap_segb * 8));
+        BRA_HIP_CHECK(hipMalloc(&flag, 4));
+        if (h_flag)
+            (void) hipHostFree(h_flag);
+        BRA_HIP_CHECK(hipHostMalloc(&h_flag, (size_t) (cap_segb + 1) * 4, hipHostMallocDefault));
+    }
+    return true;
+}
+
 void HuffWorkspace::release()
 {
+    (void) hipFree(seg);
+    (void) hipFree(seg_off);
+    (void) hipFree(seg_base);
+    (void) hipFree(end_pos);
+    (void) hipFree(flag);
+    if (h_flag)
+        (void) hipHostFree(h_flag);
     tiling.release();
     (void) hipFree(codes);
     (void) hipFree(tbits);
@@ -768,15 +966,65 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
     return true;
 }
 
-bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, uint32_t nblocks, const uint8_t* d_payload, const uint64_t* d_payload_off,
-                        uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s)
+bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint32_t* h_encoded_size, uint32_t nblocks, const uint8_t* d_payload,
+                        const uint64_t* d_payload_off, uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s)
 {
     if (!w.reserve(nblocks, 1) || !w.reserve_tree(nblocks))
         return false;
     hipLaunchKernelGGL(k_huff_tree, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, w.tree_child, w.tree_sym, w.status);
     hipLaunchKernelGGL(k_huff_table, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, w.tree_child, w.tree_sym, nblocks, w.table);
-    hipLaunchKernelGGL(k_huff_decode, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child,
-                       w.tree_sym, w.table, w.status, d_out, d_out_base, d_status);
+    // segments per block from the host-side encoded sizes
+    if (!w.reserve_segs(1, nblocks))
+        return false;
+    uint32_t* hb = w.h_flag + 1;  // pinned: segment bases, then one more entry for the total
+    uint32_t  ns = 0;
+    for (uint32_t b = 0; b < nblocks; ++b)
+    {
+        hb[b] = ns;
+        ns += (uint32_t) div_up((uint64_t) h_encoded_size[b] * 8, SEG_BITS);
+    }
+    hb[nblocks] = ns;
+    if (!w.reserve_segs(ns, nblocks))
+        return false;
+    hb = w.h_flag + 1;  // (reserve may have reallocated the pinned buffer before the copy below)
+    {
+        uint32_t n2 = 0;
+        for (uint32_t b = 0; b < nblocks; ++b)
+        {
+            hb[b] = n2;
+            n2 += (uint32_t) div_up((uint64_t) h_encoded_size[b] * 8, SEG_BITS);
+        }
+        hb[nblocks] = n2;
+    }
+    BRA_HIP_CHECK(hipMemcpyAsync(w.seg_base, hb, (size_t) (nblocks + 1) * 4, hipMemcpyHostToDevice, s));
+    HdSeg* spec = reinterpret_cast<HdSeg*>(w.seg);
+    HdSeg* cur  = spec + w.cap_seg;
+    HdSeg* nxt  = cur + w.cap_seg;
+    const uint32_t grid = std::min<uint32_t>(div_up(std::max(ns, 1u), 256), 16384);
+    if (ns)
+    {
+        hipLaunchKernelGGL(k_hd_spec, dim3(grid), dim3(256), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child, w.tree_sym, w.table,
+                           w.status, w.seg_base, ns, spec);
+        BRA_HIP_CHECK(hipMemcpyAsync(cur, spec, (size_t) ns * sizeof(HdSeg), hipMemcpyDeviceToDevice, s));
+        for (int it = 0; it < 64; ++it)
+        {
+            BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, 4, s));
+            hipLaunchKernelGGL(k_hd_sync, dim3(grid), dim3(256), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child, w.tree_sym,
+                               w.table, w.status, w.seg_base, ns, spec, cur, nxt, w.flag);
+            BRA_HIP_CHECK(hipMemcpyAsync(w.h_flag, w.flag, 4, hipMemcpyDeviceToHost, s));
+            BRA_HIP_CHECK(hipStreamSynchronize(s));
+            std::swap(cur, nxt);
+            if (!*w.h_flag)
+                break;
+        }
+    }
+    hipLaunchKernelGGL(k_hd_prefix, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_meta, nblocks, w.status, w.seg_base, cur,
+                       w.seg_off, d_status);
+    if (ns)
+        hipLaunchKernelGGL(k_hd_write, dim3(grid), dim3(256), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child, w.tree_sym, w.table,
+                           d_status, w.seg_base, ns, cur, w.seg_off, d_out, d_out_base, w.end_pos);
+    hipLaunchKernelGGL(k_hd_tail, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child, w.tree_sym,
+                       w.table, w.end_pos, d_status);
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }
