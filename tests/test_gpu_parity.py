@@ -202,3 +202,31 @@ def test_8mib_blocks_sym16(bra, codec, orc):
     total, bs = 4 * (8 << 20), 8 << 20
     data = bra.synth_fill(2, total, bs)
     _encode_check(bra, codec, orc, data, bs, check_blocks=[0, 3])
+
+
+@pytest.mark.gpu
+def test_huffman_decode_malformed(bra, orc):
+    """Truncated, bit-flipped and mis-sized streams: accept/reject and output as the oracle
+    (pinned to the reference on the same cases in test_oracle.py)."""
+    from test_oracle import _huffman_mutations
+
+    for lens, osz, esz, pay in _huffman_mutations(orc):
+        assert bra.huffman_decode(lens, osz, esz, pay) == orc.huffman_decode(lens, osz, esz, pay), (osz, esz)
+
+
+@pytest.mark.gpu
+def test_batch_decode_rejects_corruption(bra, codec):
+    """A corrupted payload in one block makes the batch decode fail (no silent garbage)."""
+    import torch
+
+    bs = 65536
+    data = bra.synth_fill(0, 8 * bs, bs)
+    d = torch.from_numpy(data).cuda()
+    hdr, off, pay = codec.encode(d, bs)
+    torch.cuda.synchronize()
+    h = hdr.cpu().numpy().copy()
+    esz3 = int.from_bytes(h[3, 264:268].tobytes(), "little")
+    h[3, 260:264] = np.frombuffer(np.uint32(int.from_bytes(h[3, 260:264].tobytes(), "little") + 5).tobytes(), np.uint8)
+    assert esz3 > 0
+    with pytest.raises(RuntimeError):
+        codec.decode(torch.from_numpy(h).cuda(), off, pay, data.size, bs)

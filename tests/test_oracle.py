@@ -116,3 +116,38 @@ def test_oracle_vs_reference(orc):
         a, b = orc.encode_block(d), R.encode_block(d)
         assert a == b, d[:32]
         assert R.decode_block(b) == d
+
+
+def _huffman_mutations(orc, seed=7, cases=40):
+    """Malformed and edge-case Huffman streams derived from valid ones (truncation, bit flips,
+    orig_size off by a few), as (lengths, orig_size, encoded_size, payload) tuples."""
+    import random
+
+    rnd = random.Random(seed)
+    out = []
+    for i in range(cases):
+        n = rnd.choice([1, 2, 5, 17, 300, 4000])
+        alpha = rnd.choice([2, 3, 16, 200])
+        data = bytes(rnd.randrange(alpha) for _ in range(n))
+        lens, osz, esz, pay = orc.huffman_encode(data)
+        out.append((lens, osz, esz, pay))
+        if esz > 1:
+            out.append((lens, osz, esz - 1, pay[:-1]))  # truncated
+        for _ in range(2):
+            if esz:
+                b = bytearray(pay)
+                k = rnd.randrange(esz)
+                b[k] ^= 1 << rnd.randrange(8)
+                out.append((lens, osz, esz, bytes(b)))  # bit flip
+        out.append((lens, osz + rnd.randrange(1, 4), esz, pay))  # asks for more symbols than coded
+        if osz > 1:
+            out.append((lens, osz - 1, esz, pay))  # stops one symbol early
+        out.append((lens, osz, esz + 2, pay + bytes([rnd.randrange(256), 0])))  # trailing bytes
+    return out
+
+
+@pytest.mark.skipif(not have_ref(), reason="reference build (oracle/_ref) not present")
+def test_huffman_decode_malformed_vs_reference(orc):
+    ref = Reference()
+    for lens, osz, esz, pay in _huffman_mutations(orc):
+        assert orc.huffman_decode(lens, osz, esz, pay) == ref.huffman_decode(lens, osz, esz, pay)
