@@ -34,7 +34,10 @@ ABI_SYMBOLS = (
     "bra_gpu_ctx_create", "bra_gpu_ctx_destroy", "bra_gpu_num_blocks", "bra_gpu_payload_bound",
     "bra_gpu_encode_blocks", "bra_gpu_decode_blocks", "bra_gpu_stage_ptr", "bra_gpu_version",
     "bra_gpu_prof_enable", "bra_gpu_prof_reset", "bra_gpu_prof_read",
+    "bra_gpu_crc32c", "bra_gpu_chunks_crc32c", "bra_gpu_crc32c_combine", "bra_gpu_entry_crc32c", "bra_gpu_chunks_bound",
+    "bra_gpu_frame_chunks", "bra_gpu_unframe_chunks", "bra_gpu_compress_chunks", "bra_gpu_decompress_chunks",
 )
+MAX_CHUNK_SIZE = 256 * 1024  # BRA_MAX_CHUNK_SIZE (src/lib_bra_defs.h:93): the .BRa chunk size
 
 SYNTH_TEXT, SYNTH_RANDOM, SYNTH_SYM16, SYNTH_TILED = 0, 1, 2, 3
 HEADER_BYTES = 268  # in-memory bra_io_chunk_header_t (pi u32 + packed bra_huffman_t)
@@ -119,6 +122,25 @@ def _load() -> C.CDLL:
     lib.bra_gpu_prof_read.restype = C.c_int
     lib.bra_gpu_version.argtypes = []
     lib.bra_gpu_version.restype = C.c_char_p
+    u64p = C.POINTER(C.c_uint64)
+    lib.bra_gpu_crc32c.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp]
+    lib.bra_gpu_crc32c.restype = C.c_int
+    lib.bra_gpu_chunks_crc32c.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint32, vp, vp]
+    lib.bra_gpu_chunks_crc32c.restype = C.c_int
+    lib.bra_gpu_crc32c_combine.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64]
+    lib.bra_gpu_crc32c_combine.restype = C.c_uint32
+    lib.bra_gpu_entry_crc32c.argtypes = [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32]
+    lib.bra_gpu_entry_crc32c.restype = C.c_uint32
+    lib.bra_gpu_chunks_bound.argtypes = [C.c_uint64, C.c_uint32]
+    lib.bra_gpu_chunks_bound.restype = C.c_uint64
+    lib.bra_gpu_frame_chunks.argtypes = [vp, vp, vp, vp, C.c_uint32, vp, C.c_uint64, u64p, vp]
+    lib.bra_gpu_frame_chunks.restype = C.c_int
+    lib.bra_gpu_unframe_chunks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp, u32p, vp]
+    lib.bra_gpu_unframe_chunks.restype = C.c_int
+    lib.bra_gpu_compress_chunks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, u64p, u32p, vp]
+    lib.bra_gpu_compress_chunks.restype = C.c_int
+    lib.bra_gpu_decompress_chunks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, u64p, C.c_uint32, u32p, vp]
+    lib.bra_gpu_decompress_chunks.restype = C.c_int
     return lib
 
 
@@ -133,6 +155,16 @@ def _buf(data: bytes):
 
 def version() -> str:
     return lib.bra_gpu_version().decode()
+
+
+def crc32c_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """bra_crc32c_combine with a 64-bit length (host arithmetic of the product library)."""
+    return lib.bra_gpu_crc32c_combine(crc_a, crc_b, len_b)
+
+
+def entry_crc32c(me_crc: int, chunks_size: int, chunks_crc: int, data_size: int, block_size: int = MAX_CHUNK_SIZE) -> int:
+    """me->crc32 after a compressed file (lib_bra_io_file_chunks.c:291-292)."""
+    return lib.bra_gpu_entry_crc32c(me_crc, chunks_size, chunks_crc, data_size, block_size)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -290,6 +322,89 @@ class BlockCodec:
             raise RuntimeError(f"bra_gpu_decode_blocks failed ({rc})")
         return out
 
+    # ---- the .BRa chunk stream (rows f1/f2) ----
+    def crc32c(self, data, prev: int = 0, stream=None) -> int:
+        """bra_crc32c(data, len, prev) of a uint8 CUDA tensor, computed on the device."""
+        import torch
+
+        out = torch.empty((1,), dtype=torch.int32, device=data.device)
+        s = stream.cuda_stream if stream is not None else None
+        if lib.bra_gpu_crc32c(self.ctx, data.data_ptr(), data.numel(), prev, out.data_ptr(), s) != 0:
+            raise RuntimeError("bra_gpu_crc32c failed")
+        return int(out.item()) & 0xFFFFFFFF
+
+    def chunks_crc32c(self, data, headers, block_size: int, prev: int = 0, stream=None) -> int:
+        """CRC32C of hdr0||chunk0||hdr1||... (the compress loop's crc32 for prev=0)."""
+        import torch
+
+        out = torch.empty((1,), dtype=torch.int32, device=data.device)
+        s = stream.cuda_stream if stream is not None else None
+        if lib.bra_gpu_chunks_crc32c(self.ctx, data.data_ptr(), data.numel(), block_size, headers.data_ptr(), prev, out.data_ptr(), s) != 0:
+            raise RuntimeError("bra_gpu_chunks_crc32c failed")
+        return int(out.item()) & 0xFFFFFFFF
+
+    def frame(self, headers, offsets, payload, out=None, stream=None):
+        """The chunk records of an encode() result, back to back (uint8 CUDA tensor)."""
+        import torch
+
+        nb = headers.shape[0]
+        need = int(offsets[nb].item()) + 267 * nb
+        if out is None:
+            out = torch.empty((max(need, 1),), dtype=torch.uint8, device=headers.device)
+        size = C.c_uint64()
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_frame_chunks(self.ctx, headers.data_ptr(), offsets.data_ptr(), payload.data_ptr(), nb, out.data_ptr(), out.numel(),
+                                      C.byref(size), s)
+        if rc != 0:
+            raise RuntimeError(f"bra_gpu_frame_chunks failed ({rc})")
+        return out[: size.value]
+
+    def unframe(self, stream_t, max_chunks: int | None = None, stream=None):
+        """(headers [n,268] u8, payload offsets [n+1] i64) of a chunk stream; raises on a malformed one."""
+        import torch
+
+        size = stream_t.numel()
+        cap = max_chunks if max_chunks is not None else size // 268 + 1
+        hdr = torch.empty((max(cap, 1), HEADER_BYTES), dtype=torch.uint8, device=stream_t.device)
+        off = torch.empty((cap + 1,), dtype=torch.int64, device=stream_t.device)
+        n = C.c_uint32()
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_unframe_chunks(self.ctx, stream_t.data_ptr(), size, cap, hdr.data_ptr(), off.data_ptr(), C.byref(n), s)
+        if rc != 0:
+            raise ValueError(f"bra_gpu_unframe_chunks rejected the stream ({rc}, {n.value} records)")
+        return hdr[: n.value], off[: n.value]
+
+    def compress_chunks(self, data, block_size: int = MAX_CHUNK_SIZE, out=None, stream=None):
+        """The reference compress loop on the device: (chunk stream tensor, crc32, compressed?)."""
+        import torch
+
+        total = data.numel()
+        cap = lib.bra_gpu_chunks_bound(total, block_size)
+        if out is None or out.numel() < cap:
+            out = torch.empty((cap,), dtype=torch.uint8, device=data.device)
+        size, crc = C.c_uint64(), C.c_uint32()
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_compress_chunks(self.ctx, data.data_ptr(), total, block_size, out.data_ptr(), out.numel(), C.byref(size), C.byref(crc), s)
+        if rc < 0:
+            raise RuntimeError(f"bra_gpu_compress_chunks failed ({rc})")
+        return out[: size.value], crc.value, rc == 1
+
+    def decompress_chunks(self, stream_t, block_size: int = MAX_CHUNK_SIZE, out_cap: int | None = None, prev_crc: int = 0, stream=None):
+        """The reference decode loop on the device: (decoded tensor, crc chained from prev_crc)."""
+        import torch
+
+        size = stream_t.numel()
+        if out_cap is None:
+            out_cap = (size // 268 + 1) * block_size
+        out = torch.empty((max(out_cap, 1),), dtype=torch.uint8, device=stream_t.device)
+        osz, crc = C.c_uint64(), C.c_uint32()
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_decompress_chunks(self.ctx, stream_t.data_ptr(), size, block_size, out.data_ptr(), out_cap, C.byref(osz), prev_crc,
+                                           C.byref(crc), s)
+        if rc != 0:
+            raise ValueError(f"bra_gpu_decompress_chunks rejected the stream ({rc})")
+        return out[: osz.value], crc.value
+
     def prof_enable(self, mask: int):
         """Time the selected kernel slots with HIP events (bit i = slot i, see csrc/prof.h)."""
         lib.bra_gpu_prof_enable(self.ctx, mask)
@@ -311,7 +426,8 @@ class BlockCodec:
              "bwt.l0_hist", "bwt.l0_scatter", "bwt.build_tiles", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.mjobs", "bwt.fallback",
              "mtf.lastocc", "mtf.scan", "mtf.encode",
              "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
-             "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack")
+             "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",
+             "chunks.frame", "chunks.crc")
 
     @classmethod
     def slot_mask(cls, *names) -> int:

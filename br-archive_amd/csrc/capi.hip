@@ -3,6 +3,7 @@
 #include "../../include/bra_hip.h"
 
 #include "bwt.h"
+#include "crc.h"
 #include "huffman.h"
 #include "ibwt.h"
 #include "mtf.h"
@@ -46,7 +47,8 @@ const char* prof_name(int slot)
         "bwt.l0_hist", "bwt.l0_scatter", "bwt.build_tiles", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.mjobs", "bwt.fallback",
         "mtf.lastocc", "mtf.scan", "mtf.encode",
         "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
-        "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack"};
+        "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",
+        "chunks.frame", "chunks.crc"};
     return (slot >= 0 && slot < P_NSLOT) ? names[slot] : "";
 }
 
@@ -182,6 +184,8 @@ struct bra_gpu_ctx_s
     bra_io_chunk_header_t* d_hdr = nullptr;
     uint64_t       cap_hdr = 0;
     uint32_t       last_nblocks = 0;
+    uint32_t*      d_word = nullptr;  // [0] CRC result, [1..2] unframe status
+    uint64_t       cap_word = 0;
     Prof           prof;
 };
 
@@ -204,7 +208,8 @@ static void ctx_free(bra_gpu_ctx_s* c)
     c->ib.release();
     c->hist_tiling.release();
     void* ptrs[] = {c->d_L,       c->d_mtf,   c->d_rle,  c->d_tmp,  c->d_blocks, c->d_pi,  c->d_rle_size, c->d_hist, c->d_status, c->d_rle_base,
-                    c->d_rle_cap, c->d_aux,   c->d_meta, c->d_recs, c->d_io,     c->d_off, c->d_pay,      c->d_hdr};
+                    c->d_rle_cap, c->d_aux,   c->d_meta, c->d_recs, c->d_io,     c->d_off, c->d_pay,      c->d_hdr,
+                    c->d_word};
     for (void* p : ptrs)
         (void) hipFree(p);
     if (c->stream)
@@ -304,9 +309,14 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     return 0;
 }
 
-// The whole decode chain.  d_out receives the blocks of geometry hb.
+// The whole decode chain.  d_out receives the blocks of geometry hb.  With `flex` (a .BRa chunk
+// stream, lib_bra_io_file_chunks.c:340-420) hb only gives capacities: every chunk may decode to
+// any size up to its hb[b].len, the primary index is checked against the decoded size (:383-387)
+// as the reference does, and the chunks land back to back in d_out (*out_size bytes, at most
+// out_cap).
 static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
-                       const std::vector<BlockDesc>& hb, uint8_t* d_out, hipStream_t s)
+                       const std::vector<BlockDesc>& hb, uint8_t* d_out, hipStream_t s, bool flex = false, uint64_t out_cap = 0,
+                       uint64_t* out_size = nullptr)
 {
     const uint32_t nb = (uint32_t) hb.size();
     if (nb == 0)
@@ -325,7 +335,7 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
     for (uint32_t b = 0; b < nb; ++b)
     {
         const uint32_t os = hh[b].huffman.orig_size;
-        if (hh[b].primary_index >= hb[b].len)
+        if (!flex && hh[b].primary_index >= hb[b].len)
         {
             bra_hip_report("invalid primary index (%u) for chunk size %u", hh[b].primary_index, hb[b].len);
             return -1;
@@ -373,16 +383,61 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
             bra_hip_report("huffman decode error in block %u", b);
             return -1;
         }
-        if (dsz[b] != hb[b].len)
+        if (!flex && dsz[b] != hb[b].len)
         {
             bra_hip_report("RLE decode of block %u gave %u bytes, expected %u", b, dsz[b], hb[b].len);
             return -1;
         }
     }
-    if (!mtf_decode_device(c->mtf, c->d_mtf, c->d_L, c->d_tmp, hb.data(), nb, s))
+    if (!flex)
+    {
+        if (!mtf_decode_device(c->mtf, c->d_mtf, c->d_L, c->d_tmp, hb.data(), nb, s) ||
+            !ibwt_device(c->ib, c->d_L, c->d_pi, c->d_blocks, hb.data(), nb, d_out, s))
+            return -1;
+        return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
+    }
+    // chunk stream: the decoded sizes define the geometry
+    std::vector<BlockDesc> g = hb;
+    uint64_t               total = 0;
+    bool                   packed = true;
+    for (uint32_t b = 0; b < nb; ++b)
+    {
+        if (dsz[b] == 0)
+        {
+            bra_hip_report("unable to decode RLE in chunk %u", b);
+            return -1;
+        }
+        if (hh[b].primary_index >= dsz[b])
+        {
+            bra_hip_report("invalid primary index (%u) for chunk size %u", hh[b].primary_index, dsz[b]);
+            return -1;
+        }
+        g[b].len = dsz[b];
+        packed   = packed && g[b].off == total;
+        total += dsz[b];
+    }
+    if (out_size)
+        *out_size = total;
+    if (total > out_cap)
+    {
+        bra_hip_report("decoded chunk stream needs %llu bytes, output holds %llu", (unsigned long long) total, (unsigned long long) out_cap);
+        return -2;
+    }
+    if (hipMemcpyAsync(c->d_blocks, g.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess)
         return -1;
-    if (!ibwt_device(c->ib, c->d_L, c->d_pi, c->d_blocks, hb.data(), nb, d_out, s))
+    if (!mtf_decode_device(c->mtf, c->d_mtf, c->d_L, c->d_tmp, g.data(), nb, s))
         return -1;
+    // a short chunk before the last leaves a gap in the capacity layout: decode to scratch, then pack
+    uint8_t* dst = packed ? d_out : c->d_tmp;
+    if (!ibwt_device(c->ib, c->d_L, c->d_pi, c->d_blocks, g.data(), nb, dst, s))
+        return -1;
+    if (!packed)
+    {
+        uint64_t o = 0;
+        for (uint32_t b = 0; b < nb; o += g[b].len, ++b)
+            if (hipMemcpyAsync(d_out + o, c->d_tmp + g[b].off, g[b].len, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return -1;
+    }
     return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
 }
 
@@ -444,6 +499,176 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_heade
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     return decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
+}
+
+int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t prev, uint32_t* d_crc, void* stream)
+{
+    if (!c || !d_crc || (len && !d_data) || hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    if (!crc_stream_device(static_cast<const uint8_t*>(d_data), len, 0, nullptr, prev, d_crc, s))
+        return -1;
+    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;  // NULL stream: complete on return
+}
+
+int bra_gpu_chunks_crc32c(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_t total, uint32_t block_size, const bra_io_chunk_header_t* d_headers,
+                          uint32_t prev, uint32_t* d_crc, void* stream)
+{
+    if (!c || !d_crc || !block_size || (total && (!d_data || !d_headers)) || hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    if (!crc_stream_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), prev, d_crc, s))
+        return -1;
+    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
+}
+
+uint32_t bra_gpu_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return crc32c_combine_host(crc_a, crc_b, len_b); }
+
+uint32_t bra_gpu_entry_crc32c(uint32_t me_crc, uint64_t chunks_size, uint32_t chunks_crc, uint64_t data_size, uint32_t block_size)
+{
+    const uint64_t num_chunks = block_size ? (data_size + block_size - 1) / block_size : 0;
+    const int64_t  tsz        = (int64_t) chunks_size;
+    me_crc                    = crc32c_host(&tsz, sizeof tsz, me_crc);
+    // bra_crc32c_combine takes a uint32_t length: keep its truncation for parity
+    return crc32c_combine_host(me_crc, chunks_crc, (uint32_t) (data_size + num_chunks * sizeof(bra_io_chunk_header_t)));
+}
+
+uint64_t bra_gpu_chunks_bound(uint64_t total, uint32_t block_size)
+{
+    return bra_gpu_payload_bound(total, block_size) + (uint64_t) CHUNK_HDR_DISK * bra_gpu_num_blocks(total, block_size);
+}
+
+int bra_gpu_frame_chunks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
+                         uint32_t nblocks, uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* stream)
+{
+    if (!c || !d_headers || !d_payload_off || !d_payload || !d_out || hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    uint64_t    P = 0;
+    if (hipMemcpyAsync(&P, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    const uint64_t need = P + (uint64_t) CHUNK_HDR_DISK * nblocks;
+    if (out_size)
+        *out_size = need;
+    if (need > out_cap)
+        return -2;
+    if (!frame_chunks_device(reinterpret_cast<const uint8_t*>(d_headers), d_payload_off, d_payload, nblocks, d_out, s))
+        return -1;
+    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
+}
+
+int bra_gpu_unframe_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t max_chunks, bra_io_chunk_header_t* d_headers,
+                           uint64_t* d_payload_off, uint32_t* n_chunks, void* stream)
+{
+    if (!c || !d_stream || !d_headers || !d_payload_off || hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    if (!grow(c->d_word, c->cap_word, 4))
+        return -1;
+    uint32_t st[2] = {0, 0};
+    if (!unframe_chunks_device(d_stream, stream_size, max_chunks, BRA_MAX_CHUNK, reinterpret_cast<uint8_t*>(d_headers), d_payload_off,
+                               c->d_word + 1, s) ||
+        hipMemcpyAsync(st, c->d_word + 1, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    if (n_chunks)
+        *n_chunks = st[0];
+    if (st[1])
+    {
+        bra_hip_report(st[1] & 2 ? "chunk header not valid" : "truncated chunk stream (%u records)", st[0]);
+        return -1;
+    }
+    return 0;
+}
+
+int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data_size, uint32_t block_size, uint8_t* d_out, uint64_t out_cap,
+                            uint64_t* out_size, uint32_t* chunks_crc, void* stream)
+{
+    if (!c || !d_in || !data_size || !block_size || block_size >= (1u << 24) || !d_out || hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t    s  = stream ? (hipStream_t) stream : c->stream;
+    const auto     hb = geometry(data_size, block_size);
+    const uint32_t nb = (uint32_t) hb.size();
+    const uint64_t pb = bra_gpu_payload_bound(data_size, block_size);
+    if (!grow(c->d_hdr, c->cap_hdr, nb) || !grow(c->d_off, c->cap_off, nb + 1) || !grow(c->d_pay, c->cap_pay, pb) || !grow(c->d_word, c->cap_word, 4))
+        return -1;
+    g_prof        = c->prof.mask ? &c->prof : nullptr;
+    uint64_t P    = 0;
+    int      rc   = encode_impl(c, d_in, hb, c->d_hdr, c->d_off, c->d_pay, c->cap_pay, s, &P);
+    uint32_t crc  = 0;
+    uint64_t need = P + (uint64_t) CHUNK_HDR_DISK * nb;
+    if (rc == 0)
+    {
+        if (out_size)
+            *out_size = need;
+        if (need > out_cap)
+            rc = -2;
+    }
+    if (rc == 0)
+    {
+        bool ok;
+        {
+            BRA_PROF(P_FRAME, s);
+            ok = frame_chunks_device(reinterpret_cast<const uint8_t*>(c->d_hdr), c->d_off, c->d_pay, nb, d_out, s);
+        }
+        if (ok)
+        {
+            BRA_PROF(P_CRC, s);
+            ok = crc_stream_device(d_in, data_size, block_size, reinterpret_cast<const uint8_t*>(c->d_hdr), 0, c->d_word, s);
+        }
+        if (g_prof)
+        {
+            prof_bytes(P_FRAME, 2.0 * (double) need);
+            prof_bytes(P_CRC, (double) data_size + 268.0 * nb);
+        }
+        if (!ok || hipMemcpyAsync(&crc, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            rc = -1;
+    }
+    g_prof = nullptr;
+    if (rc != 0)
+        return rc;
+    if (chunks_crc)
+        *chunks_crc = crc;
+    return need < data_size ? 1 : 0;  // 0: not smaller than the input -> STORED (lib_bra_io_file_chunks.c:274-278)
+}
+
+int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
+                              uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream)
+{
+    if (!c || !d_stream || !block_size || block_size >= (1u << 24) || !d_out || hipSetDevice(c->device) != hipSuccess)
+        return -1;
+    hipStream_t    s        = stream ? (hipStream_t) stream : c->stream;
+    const uint32_t max_recs = (uint32_t) std::min<uint64_t>(stream_size / (CHUNK_HDR_DISK + 1) + 1, 1u << 26);
+    if (!grow(c->d_hdr, c->cap_hdr, max_recs) || !grow(c->d_off, c->cap_off, max_recs + 1) || !grow(c->d_word, c->cap_word, 4))
+        return -1;
+    uint32_t nb = 0;
+    if (bra_gpu_unframe_chunks(c, d_stream, stream_size, max_recs, c->d_hdr, c->d_off, &nb, s) != 0)
+        return -1;
+    if (nb == 0)
+    {
+        bra_hip_report("corrupted file entry: empty chunk stream");
+        return -1;
+    }
+    std::vector<BlockDesc> caps(nb);
+    for (uint32_t b = 0; b < nb; ++b)
+        caps[b] = BlockDesc{(uint64_t) b * block_size, block_size, 0};
+    uint64_t total = 0;
+    int      rc    = decode_impl(c, c->d_hdr, c->d_off, d_stream, caps, d_out, s, true, out_cap, &total);
+    if (out_size)
+        *out_size = total;
+    if (rc != 0)
+        return rc;
+    if (total <= stream_size)  // the reference's safety check (:423-427)
+    {
+        bra_hip_report("corrupted file entry: %llu decoded bytes from %llu", (unsigned long long) total, (unsigned long long) stream_size);
+        return -1;
+    }
+    if (crc_out)
+    {
+        if (!crc_stream_device(d_out, total, block_size, reinterpret_cast<const uint8_t*>(c->d_hdr), prev_crc, c->d_word, s) ||
+            hipMemcpyAsync(crc_out, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return -1;
+    }
+    return 0;
 }
 
 const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)

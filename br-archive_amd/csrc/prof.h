@@ -17,6 +17,7 @@ enum ProfSlot : int
     P_MTF_LASTOCC, P_MTF_SCAN, P_MTF_ENCODE,
     P_RLE_RUNS, P_RLE_LINK, P_RLE_SIZES, P_RLE_OFFSETS, P_RLE_WRITE,
     P_HUF_BUILD, P_HUF_OFFSETS, P_HUF_TILEBITS, P_HUF_TILESCAN, P_HUF_ZERO, P_HUF_PACK,
+    P_FRAME, P_CRC,
     P_NSLOT
 };
 

@@ -115,6 +115,80 @@ int bra_gpu_encode_blocks(bra_gpu_ctx_t* ctx, const uint8_t* d_in, uint64_t tota
 int bra_gpu_decode_blocks(bra_gpu_ctx_t* ctx, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off,
                           const uint8_t* d_payload, uint64_t total, uint32_t block_size, uint8_t* d_out, void* stream);
 
+/* ---- Part 3: the .BRa chunk stream on the device --------------------- */
+/* Streams: a NULL stream means the context's stream and the call has completed when it returns;
+ * with an explicit stream the device results are ordered on that stream. */
+
+/*
+ * CRC32C of d_data[0, len) (device memory) chained from prev, i.e. bra_crc32c(data, len, prev)
+ * (replaces src/utils/lib_bra_crc32c.h bra_crc32c, lib_bra_crc32c.c:102-117 / :133-179 for
+ * device-resident data).  The result is written to *d_crc (device memory) on the stream.
+ */
+int bra_gpu_crc32c(bra_gpu_ctx_t* ctx, const void* d_data, uint64_t len, uint32_t prev, uint32_t* d_crc, void* stream);
+
+/*
+ * CRC32C of the chunk stream hdr[0] || chunk 0 || hdr[1] || chunk 1 || ... chained from prev, where
+ * hdr[b] is the 268-byte in-memory header d_headers[b] and chunk b is d_data[b*block_size, ...)
+ * (last one ragged).  prev = 0 (BRA_CRC32C_INIT) gives the `crc32` of the reference compress loop
+ * (lib_bra_io_file_chunks.c:214,248-249); prev = me->crc32 over decoded chunks gives the decode
+ * loop's update (:396-397).  Result in *d_crc (device memory).
+ */
+int bra_gpu_chunks_crc32c(bra_gpu_ctx_t* ctx, const uint8_t* d_data, uint64_t total, uint32_t block_size,
+                          const bra_io_chunk_header_t* d_headers, uint32_t prev, uint32_t* d_crc, void* stream);
+
+/* Host: bra_crc32c_combine (lib_bra_crc32c.c:181-231) with a 64-bit length; used to merge the
+ * per-rank chunk-stream CRCs of a sharded encode in block order. */
+uint32_t bra_gpu_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* Host: me->crc32 after a compressed file (lib_bra_io_file_chunks.c:291-292) from the meta entry's
+ * CRC so far, the chunk stream size (tmpfile size), its CRC and the input size.  The combine
+ * length is truncated to 32 bits exactly as in the reference. */
+uint32_t bra_gpu_entry_crc32c(uint32_t me_crc, uint64_t chunks_size, uint32_t chunks_crc, uint64_t data_size, uint32_t block_size);
+
+/* Output capacity for bra_gpu_compress_chunks: payload bound + 267 bytes per chunk. */
+uint64_t bra_gpu_chunks_bound(uint64_t total, uint32_t block_size);
+
+/*
+ * Write the .BRa chunk records of nblocks encoded blocks (bra_gpu_encode_blocks output) back to
+ * back into d_out: 3 low bytes of pi + the packed 264-byte bra_huffman_t + payload
+ * (bra_io_file_chunks_write_header, lib_bra_io_file_chunks.c:76-95, then :260).  *out_size =
+ * payload_off[nblocks] + 267 * nblocks; -2 when that exceeds out_cap.
+ */
+int bra_gpu_frame_chunks(bra_gpu_ctx_t* ctx, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
+                         uint32_t nblocks, uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* stream);
+
+/*
+ * Parse a chunk stream d_stream[0, stream_size) (the read loop of bra_io_file_chunks_decompress_file,
+ * lib_bra_io_file_chunks.c:340-420): headers to d_headers, payload b at d_stream + d_payload_off[b].
+ * Fails (< 0) on a truncated stream, more than max_chunks records, or a header that
+ * bra_io_file_chunks_header_validate (:31-49) rejects.  *n_chunks = records found.
+ */
+int bra_gpu_unframe_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_stream, uint64_t stream_size, uint32_t max_chunks,
+                           bra_io_chunk_header_t* d_headers, uint64_t* d_payload_off, uint32_t* n_chunks, void* stream);
+
+/*
+ * The compress chunk loop (bra_io_file_chunks_compress_file, lib_bra_io_file_chunks.c:199-278) over
+ * device data: every block_size chunk of d_in[0, data_size) encoded, framed into d_out (the exact
+ * bytes the reference writes to its tmpfile, *out_size of them) and the loop's running CRC32C in
+ * *chunks_crc (host).  block_size = 262144 (BRA_MAX_CHUNK_SIZE) reproduces the reference format.
+ * Returns 1 when the chunk stream is smaller than the input, 0 when it is not (the reference then
+ * stores the file: BRA_ATTR_COMP_STORED, :274-278), -2 when out_cap is too small (*out_size holds
+ * the need), other < 0 on error.  Pair with bra_gpu_entry_crc32c for me->crc32.
+ */
+int bra_gpu_compress_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_in, uint64_t data_size, uint32_t block_size, uint8_t* d_out,
+                            uint64_t out_cap, uint64_t* out_size, uint32_t* chunks_crc, void* stream);
+
+/*
+ * The decode loop (bra_io_file_chunks_decompress_file, lib_bra_io_file_chunks.c:340-427) over a
+ * device-resident chunk stream: the decoded bytes back to back in d_out (*out_size of them, at
+ * most out_cap; -2 if larger) and, when crc_out is non-NULL, me->crc32 updated from prev_crc as the
+ * reference does (:396-397).  Every reference rejection is an error here too (invalid header,
+ * Huffman / RLE failure, pi >= chunk size, decoded size not above the stream size).  block_size
+ * bounds every chunk's decoded size.
+ */
+int bra_gpu_decompress_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
+                              uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream);
+
 /*
  * Device pointers to the intermediate stage outputs of the last bra_gpu_encode_blocks call (for
  * parity tests): 0 = BWT last column (total bytes), 1 = MTF (total bytes), 2 = RLE output (block b

@@ -4,7 +4,10 @@ ctypes bindings to
   * ``liboracle.so``        -- the CPU restatement of the reference chain (``bra_oracle.c``);
   * ``_ref/libbraref.so``   -- the reference's own ``src/encoders`` compiled from /root/reference
                                by ``oracle/Makefile`` (absent when the reference tree was never
-                               available; then only the restatement + committed golden vectors).
+                               available; then only the restatement + committed golden vectors);
+  * ``_ref/libbralib.so``   -- the whole reference ``lib_bra`` plus ``oracle/ref_chunks.c``, a
+                               driver of its chunk loop (``bra_io_file_chunks_compress_file``)
+                               and CRC32C, for the chunk-stream and framing parity (rows f1/f2).
 
 Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import this
 package, and only as the checker.  The product library (``br-archive_amd/``) never links it.
@@ -80,6 +83,16 @@ class Oracle:
         L.orc_huffman_encode.argtypes = [u8p, C.c_uint32, C.POINTER(HuffMeta), C.POINTER(C.c_void_p)]
         L.orc_huffman_decode.argtypes = [C.POINTER(HuffMeta), u8p, u8p]
         L.orc_free.argtypes = [C.c_void_p]
+        L.orc_crc32c.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
+        L.orc_crc32c.restype = C.c_uint32
+        L.orc_crc32c_combine.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_crc32c_combine.restype = C.c_uint32
+        L.orc_chunks_crc32c.argtypes = [u8p, u8p, C.c_uint64, C.c_uint32, C.c_uint32]
+        L.orc_chunks_crc32c.restype = C.c_uint32
+        L.orc_entry_crc32c.argtypes = [C.c_uint32, C.c_int64, C.c_uint32, C.c_uint64]
+        L.orc_entry_crc32c.restype = C.c_uint32
+        L.orc_frame_record.argtypes = [u8p, u8p, C.c_uint32, u8p]
+        L.orc_frame_record.restype = C.c_size_t
 
     def bwt_encode(self, data: bytes, want_sa: bool = False):
         n = len(data)
@@ -159,6 +172,37 @@ class Oracle:
         m = self.rle_decode(r)
         b = self.mtf_decode(m)
         return self.bwt_decode(b, ch.primary_index)
+
+    # ---- CRC32C and the chunk stream (rows f1/f2) ----
+    def crc32c(self, data: bytes, prev: int = 0) -> int:
+        return self.lib.orc_crc32c(_buf(data), len(data), prev)
+
+    def crc32c_combine(self, a: int, b: int, len_b: int) -> int:
+        return self.lib.orc_crc32c_combine(a, b, len_b & 0xFFFFFFFF)
+
+    def chunks_crc32c(self, headers: bytes, data: bytes, chunk_size: int, prev: int = 0) -> int:
+        """crc32 of the compress loop (lib_bra_io_file_chunks.c:248-249): headers = n x 268 B."""
+        return self.lib.orc_chunks_crc32c(_buf(headers), _buf(data), len(data), chunk_size, prev)
+
+    def entry_crc32c(self, me_crc: int, tmpfile_size: int, chunks_crc: int, data_size: int) -> int:
+        """me->crc32 after a compressed file (lib_bra_io_file_chunks.c:291-292)."""
+        return self.lib.orc_entry_crc32c(me_crc, tmpfile_size, chunks_crc, data_size)
+
+    def frame(self, chunks: list) -> bytes:
+        """The tmpfile of the compress loop: every chunk as 3-B pi + 264-B meta + payload."""
+        out = []
+        for ch in chunks:
+            rec = (C.c_uint8 * (267 + ch.encoded_size))()
+            hdr = ch.primary_index.to_bytes(4, "little") + ch.lengths + ch.orig_size.to_bytes(4, "little") + ch.encoded_size.to_bytes(4, "little")
+            n = self.lib.orc_frame_record(_buf(hdr), _buf(ch.payload), ch.encoded_size, rec)
+            out.append(bytes(rec)[:n])
+        return b"".join(out)
+
+    def compress_chunks(self, data: bytes, chunk_size: int = 256 * 1024):
+        """(tmpfile bytes, crc32, chunks) as bra_io_file_chunks_compress_file builds them."""
+        chunks = [self.encode_block(data[i : i + chunk_size]) for i in range(0, len(data), chunk_size)]
+        hdrs = b"".join(ch.primary_index.to_bytes(4, "little") + ch.lengths + ch.orig_size.to_bytes(4, "little") + ch.encoded_size.to_bytes(4, "little") for ch in chunks)
+        return self.frame(chunks), self.chunks_crc32c(hdrs, data, chunk_size), chunks
 
 
 # --------------------------------------------------------------------------------------------
@@ -274,3 +318,47 @@ class Reference:
         m = self.rle_decode(r)
         b = self.mtf_decode(m)
         return self.bwt_decode(b, ch.primary_index)
+
+
+# --------------------------------------------------------------------------------------------
+# The whole reference lib_bra (oracle/_ref/libbralib.so): CRC32C and the chunk loop
+# --------------------------------------------------------------------------------------------
+LIB_PATH = os.path.join(_HERE, "_ref", "libbralib.so")
+
+
+def have_reflib() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+class ReferenceLib:
+    """bra_crc32c / bra_crc32c_combine (lib_bra_crc32c.h) and the reference chunk loop driven by
+    oracle/ref_chunks.c on real files."""
+
+    def __init__(self, path: str = LIB_PATH):
+        self.lib = L = C.CDLL(path)
+        L.bra_crc32c.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
+        L.bra_crc32c.restype = C.c_uint32
+        L.bra_crc32c_combine.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        L.bra_crc32c_combine.restype = C.c_uint32
+        L.ref_compress_file.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ref_compress_file.restype = C.c_int
+
+    def crc32c(self, data: bytes, prev: int = 0) -> int:
+        return self.lib.bra_crc32c(_buf(data), len(data), prev)
+
+    def crc32c_combine(self, a: int, b: int, len_b: int) -> int:
+        return self.lib.bra_crc32c_combine(a, b, len_b & 0xFFFFFFFF)
+
+    def compress_file(self, data: bytes, workdir: str):
+        """Run bra_io_file_chunks_compress_file on `data`.  Returns (ok, dst bytes, me->crc32
+        before, me->crc32 after, attributes after).  dst holds the meta entry (when compressed)
+        followed by the chunk records."""
+        src = os.path.join(workdir, "src.bin")
+        dst = os.path.join(workdir, "dst.bin")
+        with open(src, "wb") as f:
+            f.write(data)
+        cb, ca, at = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        ok = self.lib.ref_compress_file(src.encode(), dst.encode(), len(data), C.byref(cb), C.byref(ca), C.byref(at))
+        with open(dst, "rb") as f:
+            out = f.read()
+        return bool(ok), out, cb.value, ca.value, at.value

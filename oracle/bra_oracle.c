@@ -557,4 +557,122 @@ int orc_encode_block(const uint8_t* in, uint32_t n, uint32_t* primary_index, orc
     return ok;
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* CRC32C and the chunk stream  (restates src/utils/lib_bra_crc32c.c:102-231 and the CRC        */
+/* sequence of src/io/lib_bra_io_file_chunks.c:214,248-249,291-292)                             */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Reflected Castagnoli polynomial (lib_bra_crc32c.c:27). */
+#define ORC_CRC_POLY 0x82F63B78u
+
+static uint32_t orc_crc_tab[256];
+static int      orc_crc_ready;
+
+static void orc_crc_init(void)
+{
+    if (orc_crc_ready)
+        return;
+    for (uint32_t v = 0; v < 256; ++v)
+    {
+        uint32_t c = v;
+        for (int k = 0; k < 8; ++k)
+            c = (c & 1) ? (c >> 1) ^ ORC_CRC_POLY : c >> 1;
+        orc_crc_tab[v] = c;
+    }
+    orc_crc_ready = 1;
+}
+
+/* bra_crc32c(data, length, previous_crc) (lib_bra_crc32c.c:102-117): the public value is the
+ * complemented register, so chaining passes the previous result straight back in. */
+uint32_t orc_crc32c(const void* data, uint64_t length, uint32_t previous_crc)
+{
+    orc_crc_init();
+    const uint8_t* p = (const uint8_t*) data;
+    uint32_t       c = ~previous_crc;
+    for (uint64_t i = 0; i < length; ++i)
+        c = orc_crc_tab[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return ~c;
+}
+
+/* GF(2) 32x32 operator helpers: column n of `mat` is the image of bit n. */
+static uint32_t orc_gf2_times(const uint32_t* mat, uint32_t vec)
+{
+    uint32_t sum = 0;
+    for (int n = 0; vec; ++n, vec >>= 1)
+        if (vec & 1)
+            sum ^= mat[n];
+    return sum;
+}
+
+static void orc_gf2_square(uint32_t* sq, const uint32_t* mat)
+{
+    for (int n = 0; n < 32; ++n)
+        sq[n] = orc_gf2_times(mat, mat[n]);
+}
+
+/* bra_crc32c_combine(a, b, len_b) (lib_bra_crc32c.c:181-231): the CRC of A||B from crc(A),
+ * crc(B) and |B|.  Appending |B| zero bytes to A is applied as repeated squarings of the
+ * one-zero-bit operator (1 -> 2 -> 4 -> 8 bits, then one squaring per bit of len_b). */
+uint32_t orc_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint32_t len_b)
+{
+    if (len_b == 0)
+        return crc_a;
+    uint32_t op1[32], op2[32];
+    op1[0] = ORC_CRC_POLY; /* one zero bit */
+    for (int n = 1; n < 32; ++n)
+        op1[n] = 1u << (n - 1);
+    orc_gf2_square(op2, op1); /* two zero bits  */
+    orc_gf2_square(op1, op2); /* four zero bits */
+    uint32_t* cur = op1;
+    uint32_t* nxt = op2;
+    while (len_b)
+    {
+        orc_gf2_square(nxt, cur); /* 8, 16, 32 ... zero bits */
+        if (len_b & 1)
+            crc_a = orc_gf2_times(nxt, crc_a);
+        len_b >>= 1;
+        uint32_t* t = cur;
+        cur         = nxt;
+        nxt         = t;
+    }
+    return crc_a ^ crc_b;
+}
+
+/* The `crc32` variable of bra_io_file_chunks_compress_file after its loop (:186,214,248-249):
+ * per chunk the 268-byte in-memory header, then the source chunk, folded in by combine.
+ * headers: nchunks x 268 bytes; data: the source (or, on decode, the decoded) chunks back to back
+ * with every chunk chunk_size bytes except a ragged last one. */
+uint32_t orc_chunks_crc32c(const uint8_t* headers, const uint8_t* data, uint64_t total, uint32_t chunk_size, uint32_t crc)
+{
+    uint64_t b = 0;
+    for (uint64_t i = 0; i < total; i += chunk_size, ++b)
+    {
+        const uint32_t s   = (uint32_t) ((total - i) < chunk_size ? (total - i) : chunk_size);
+        const uint32_t src = orc_crc32c(data + i, s, 0);
+        crc                = orc_crc32c(headers + 268 * b, 268, crc);
+        crc                = orc_crc32c_combine(crc, src, s);
+    }
+    return crc;
+}
+
+/* The meta entry CRC after a compressed file (:291-292): the 8-byte tmpfile size, then the chunk
+ * stream CRC combined over data_size + num_chunks * 268 bytes (len_b is uint32_t there). */
+uint32_t orc_entry_crc32c(uint32_t me_crc, int64_t tmpfile_size, uint32_t chunks_crc, uint64_t data_size)
+{
+    uint64_t num_chunks = data_size / (256 * 1024) + (data_size % (256 * 1024) ? 1 : 0);
+    me_crc              = orc_crc32c(&tmpfile_size, sizeof tmpfile_size, me_crc);
+    return orc_crc32c_combine(me_crc, chunks_crc, (uint32_t) (data_size + num_chunks * 268));
+}
+
+/* One .BRa chunk record (lib_bra_io_file_chunks.c:76-95 + :260): 3 low bytes of the primary
+ * index, the packed 264-byte bra_huffman_t, the payload.  Returns the record size. */
+size_t orc_frame_record(const uint8_t header268[268], const uint8_t* payload, uint32_t encoded_size, uint8_t* out)
+{
+    memcpy(out, header268, 3);
+    memcpy(out + 3, header268 + 4, 264);
+    if (encoded_size)
+        memcpy(out + 267, payload, encoded_size);
+    return 267 + (size_t) encoded_size;
+}
+
 void orc_free(void* p) { free(p); }

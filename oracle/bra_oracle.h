@@ -35,6 +35,11 @@ int    orc_huffman_encode(const uint8_t* in, uint32_t n, orc_huffman_meta_t* met
 int    orc_huffman_decode(const orc_huffman_meta_t* meta, const uint8_t* data, uint8_t* out);
 int    orc_encode_block(const uint8_t* in, uint32_t n, uint32_t* primary_index, orc_huffman_meta_t* meta, uint8_t** payload,
                         uint8_t* bwt_out, uint8_t* mtf_out, uint8_t** rle_out, size_t* rle_size);
+uint32_t orc_crc32c(const void* data, uint64_t length, uint32_t previous_crc);
+uint32_t orc_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint32_t len_b);
+uint32_t orc_chunks_crc32c(const uint8_t* headers, const uint8_t* data, uint64_t total, uint32_t chunk_size, uint32_t crc);
+uint32_t orc_entry_crc32c(uint32_t me_crc, int64_t tmpfile_size, uint32_t chunks_crc, uint64_t data_size);
+size_t   orc_frame_record(const uint8_t header268[268], const uint8_t* payload, uint32_t encoded_size, uint8_t* out);
 void   orc_free(void* p);
 
 #ifdef __cplusplus

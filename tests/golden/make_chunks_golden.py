@@ -1,0 +1,79 @@
+"""Generate tests/golden/chunks.json from the REFERENCE chunk loop (rows f1/f2).
+
+Run in the build container (where /root/reference exists):
+    make -C oracle ref && python tests/golden/make_chunks_golden.py
+
+For every case the input is a deterministic synthetic buffer (br-archive_amd/csrc/bra_synth.c,
+bra_synth_fill(kind, 0, ..., total, 262144)), and the expected values come from
+oracle/_ref/libbralib.so, i.e. the reference's own bra_io_file_chunks_compress_file
+(src/io/lib_bra_io_file_chunks.c:169-312) run on a real file by oracle/ref_chunks.c:
+  * compressed   -- the call succeeded (False: the reference switched the entry to STORED);
+  * stream_size / stream_sha256 -- the chunk records the reference writes after the 8-byte
+    data_size of the meta entry (what bra_gpu_compress_chunks must produce byte for byte);
+  * entry_crc    -- me->crc32 after the call (lib_bra_io_file_chunks.c:291-292), from a fresh
+    entry whose CRC is BRA_CRC32C_INIT;
+  * chunk_crcs   -- the CRC32C of every 268-byte in-memory header + chunk (parsed back from the
+    stream with the reference's bra_crc32c, so the fixture also pins the header layout).
+The fixture stores digests and CRCs only (JSON data, no code).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+from oracle import ReferenceLib, have_reflib  # noqa: E402
+
+CASES = [  # (name, synth kind, total bytes)
+    ("text_600000", 0, 600000),
+    ("text_262144", 0, 262144),
+    ("text_262145", 0, 262145),
+    ("sym16_524288", 2, 524288),
+    ("random_100000", 1, 100000),
+]
+
+
+def synth(kind: int, total: int) -> bytes:
+    import numpy as np
+
+    bra = __import__("importlib").import_module("br-archive_amd")
+    a = np.empty(total, dtype=np.uint8)
+    bra.synth_lib().bra_synth_fill(kind, 0, a.ctypes.data, total, 262144)
+    return a.tobytes()
+
+
+def main():
+    if not have_reflib():
+        sys.exit("oracle/_ref/libbralib.so missing: run `make -C oracle ref` where /root/reference exists")
+    R = ReferenceLib()
+    out = {}
+    for name, kind, total in CASES:
+        data = synth(kind, total)
+        with tempfile.TemporaryDirectory() as d:
+            ok, dst, cb, ca, attr = R.compress_file(data, d)
+        rec = dict(kind=kind, total=total, compressed=ok, attr=attr, entry_crc_before=cb, entry_crc=ca)
+        if ok:
+            tsz = int.from_bytes(dst[:8], "little")
+            stream = dst[8:]
+            assert len(stream) == tsz, (name, len(stream), tsz)
+            crcs, pos, b = [], 0, 0
+            while pos < len(stream):
+                esz = int.from_bytes(stream[pos + 263: pos + 267], "little")
+                hdr = stream[pos: pos + 3] + b"\0" + stream[pos + 3: pos + 267]
+                chunk = data[b * 262144: (b + 1) * 262144]
+                crcs.append(R.crc32c(chunk, R.crc32c(hdr)))
+                pos += 267 + esz
+                b += 1
+            rec.update(stream_size=tsz, stream_sha256=hashlib.sha256(stream).hexdigest(), chunk_crcs=crcs)
+        out[name] = rec
+        print(name, {k: v for k, v in rec.items() if k != "chunk_crcs"}, flush=True)
+    with open(os.path.join(ROOT, "tests", "golden", "chunks.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,212 @@
+"""Device CRC32C, chunk framing and the chunk loops against the oracle and
+the reference's own chunk-loop output (tests/golden/chunks.json).  Bar: bit-exact bytes and CRCs.
+"""
+import hashlib
+import importlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CS = 256 * 1024
+
+
+@pytest.fixture(scope="module")
+def bra():
+    return importlib.import_module("br-archive_amd")
+
+
+@pytest.fixture(scope="module")
+def codec(bra):
+    c = bra.BlockCodec(0)
+    yield c
+    c.close()
+
+
+def _dev(a: np.ndarray, pad: int = 0):
+    """CUDA copy of a, starting `pad` bytes into its allocation (misaligned views)."""
+    import torch
+
+    t = torch.zeros(a.size + pad + 16, dtype=torch.uint8, device="cuda")
+    t[pad: pad + a.size] = torch.from_numpy(a).cuda()
+    return t[pad: pad + a.size]
+
+
+def _hdr_bytes(ch):
+    return ch.primary_index.to_bytes(4, "little") + ch.lengths + ch.orig_size.to_bytes(4, "little") + ch.encoded_size.to_bytes(4, "little")
+
+
+def test_crc32c_device_vs_oracle(codec, orc):
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 3, 15, 16, 17, 255, 4096, 65535, 65536, 65537, 200003, (1 << 20) + 5, 3 << 20):
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        for pad in (0, 1, 7, 13):
+            prev = int(rng.integers(0, 1 << 32))
+            assert codec.crc32c(_dev(a, pad), prev) == orc.crc32c(a.tobytes(), prev), (n, pad)
+
+
+def test_crc32c_device_full_size_split(bra, codec):
+    """256 MiB: crc(A || B) == combine(crc(A), crc(B), |B|) for splits at awkward offsets."""
+    import torch
+
+    total = 256 << 20
+    d = torch.from_numpy(bra.synth_fill(0, total, 1 << 20)).cuda()
+    full = codec.crc32c(d)
+    for cut in (1, 65536 * 3 + 5, total // 2 - 1, total - 3):
+        a, b = codec.crc32c(d[:cut]), codec.crc32c(d[cut:])
+        assert bra.crc32c_combine(a, b, total - cut) == full, cut
+    assert codec.crc32c(d[5:], codec.crc32c(d[:5])) == full
+
+
+@pytest.mark.parametrize("bs,total,pad", [(CS, 3 * CS + 100, 0), (1 << 20, 5 << 20, 3), (65536, 65536 * 7 - 1, 9), (4096, 4096, 0)])
+def test_chunks_crc_device_vs_oracle(codec, orc, bs, total, pad):
+    import torch
+
+    rng = np.random.default_rng(total)
+    data = rng.integers(0, 256, total, dtype=np.uint8)
+    nb = (total + bs - 1) // bs
+    hdr = rng.integers(0, 256, (nb, 268), dtype=np.uint8)
+    prev = int(rng.integers(0, 1 << 32))
+    want = orc.chunks_crc32c(hdr.tobytes(), data.tobytes(), bs, prev)
+    h = _dev(hdr.reshape(-1), 5).view(nb, 268) if pad else torch.from_numpy(hdr).cuda()
+    assert codec.chunks_crc32c(_dev(data, pad), h, bs, prev) == want
+
+
+def _golden():
+    with open(os.path.join(ROOT, "tests", "golden", "chunks.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", sorted(_golden()))
+def test_compress_chunks_vs_reference_golden(bra, codec, name):
+    """The device chunk loop reproduces the reference's tmpfile bytes and CRCs."""
+    import torch
+
+    g = _golden()[name]
+    data = bra.synth_fill(g["kind"], g["total"], CS)
+    stream, crc, compressed = codec.compress_chunks(torch.from_numpy(data).cuda(), CS)
+    assert compressed == g["compressed"]
+    if not compressed:
+        # the reference then stores the file; its CRC is bra_crc32c over the raw bytes
+        return
+    s = stream.cpu().numpy().tobytes()
+    assert len(s) == g["stream_size"]
+    assert hashlib.sha256(s).hexdigest() == g["stream_sha256"]
+    assert bra.entry_crc32c(g["entry_crc_before"], len(s), crc, g["total"]) == g["entry_crc"]
+    # decode side: the same stream CRC folded over the decoded chunks
+    out, dcrc = codec.decompress_chunks(stream, CS, prev_crc=0)
+    assert torch.equal(out.cpu(), torch.from_numpy(data))
+    assert dcrc == crc
+
+
+@pytest.mark.parametrize("kind,total,bs", [(0, 8 << 20, 1 << 20), (2, 3 * CS + 1, CS), (1, 2 * CS, CS), (0, 1, CS)])
+def test_compress_chunks_vs_oracle(bra, codec, orc, kind, total, bs):
+    import torch
+
+    data = bra.synth_fill(kind, total, bs)
+    stream, crc, compressed = codec.compress_chunks(torch.from_numpy(data).cuda(), bs)
+    want, wcrc, _ = orc.compress_chunks(data.tobytes(), bs)
+    assert stream.cpu().numpy().tobytes() == want
+    assert crc == wcrc
+    assert compressed == (len(want) < total)
+
+
+def test_frame_unframe_roundtrip(bra, codec, orc):
+    """encode() + frame() == oracle framing; unframe() gives back the headers and offsets."""
+    import torch
+
+    bs = 65536
+    data = bra.synth_fill(0, 9 * bs + 333, bs)
+    hdr, off, pay = codec.encode(torch.from_numpy(data).cuda(), bs)
+    st = codec.frame(hdr, off, pay)
+    want = orc.frame([orc.encode_block(data[i: i + bs].tobytes()) for i in range(0, data.size, bs)])
+    assert st.cpu().numpy().tobytes() == want
+    h2, o2 = codec.unframe(st)
+    nb = hdr.shape[0]
+    assert torch.equal(h2.cpu(), hdr.cpu())
+    offs = off.cpu().numpy()[:nb] + 267 * (np.arange(nb) + 1)
+    assert np.array_equal(o2.cpu().numpy()[:nb], offs)
+
+
+def test_decompress_chunks_prev_crc(bra, codec, orc):
+    """me->crc32 update of the decode loop (:396-397) chained from a non-zero entry CRC."""
+    import torch
+
+    data = bra.synth_fill(2, 2 * CS + 5, CS)
+    stream, _, _ = codec.compress_chunks(torch.from_numpy(data).cuda(), CS)
+    st = stream.cpu().numpy().tobytes()
+    hdrs, pos = b"", 0
+    while pos < len(st):
+        hdrs += st[pos: pos + 3] + b"\0" + st[pos + 3: pos + 267]
+        pos += 267 + int.from_bytes(st[pos + 263: pos + 267], "little")
+    out, crc = codec.decompress_chunks(stream, CS, prev_crc=0x1234ABCD)
+    assert out.cpu().numpy().tobytes() == data.tobytes()
+    assert crc == orc.chunks_crc32c(hdrs, data.tobytes(), CS, 0x1234ABCD)
+
+
+def test_decompress_chunks_rejects(bra, codec):
+    """Every case the reference decode loop rejects (lib_bra_io_file_chunks.c:31-49,340-427)."""
+    import torch
+
+    data = bra.synth_fill(0, 2 * CS + 9, CS)
+    stream, _, _ = codec.compress_chunks(torch.from_numpy(data).cuda(), CS)
+    good = stream.cpu().numpy()
+
+    def bad(mut):
+        a = good.copy()
+        a = mut(a)
+        with pytest.raises(ValueError):
+            codec.decompress_chunks(torch.from_numpy(a).cuda(), CS)
+
+    bad(lambda a: a[:-1])                                    # truncated payload
+    bad(lambda a: np.concatenate([a, np.zeros(5, np.uint8)]))  # trailing partial header
+    bad(lambda a: _set(a, 0, (CS + 1).to_bytes(4, "little")[:3]))  # pi >= 256 KiB
+    bad(lambda a: _set(a, 263, b"\0\0\0\0"))                 # encoded_size 0
+    bad(lambda a: _set(a, 259, (CS + 1).to_bytes(4, "little")))  # orig_size > 256 KiB
+    # a stored-size stream (decoded size not above the stream size) is "corrupted"
+    rnd = np.random.default_rng(1).integers(0, 256, 1000, dtype=np.uint8)
+    st2, _, compressed = codec.compress_chunks(torch.from_numpy(rnd).cuda(), CS)
+    assert not compressed
+    with pytest.raises(ValueError):
+        codec.decompress_chunks(st2, CS)
+    # the untouched stream still decodes
+    out, _ = codec.decompress_chunks(torch.from_numpy(good).cuda(), CS)
+    assert out.cpu().numpy().tobytes() == data.tobytes()
+
+
+def _set(a, pos, b):
+    a[pos: pos + len(b)] = np.frombuffer(b, np.uint8)
+    return a
+
+
+def test_sharded_stream_crc_merge(bra, codec):
+    """Two ranks' chunk streams (split at a chunk boundary) merge to the single-GPU stream and CRC."""
+    import torch
+
+    data = bra.synth_fill(0, 6 * CS + 77, CS)
+    d = torch.from_numpy(data).cuda()
+    s_all, c_all, _ = codec.compress_chunks(d, CS)
+    cut = 4 * CS
+    s_a, c_a, _ = codec.compress_chunks(d[:cut], CS)
+    s_b, c_b, _ = codec.compress_chunks(d[cut:], CS)
+    assert torch.equal(torch.cat([s_a, s_b]).cpu(), s_all.cpu())
+    nb_b = (data.size - cut + CS - 1) // CS
+    assert bra.crc32c_combine(c_a, c_b, data.size - cut + 268 * nb_b) == c_all
+
+
+def test_full_size_chunk_stream(bra, codec):
+    """256 MiB of text as 1024 reference-size chunks: stream round trip, encode CRC == decode CRC."""
+    import torch
+
+    total = 256 << 20
+    d = torch.from_numpy(bra.synth_fill(0, total, CS)).cuda()
+    stream, crc, compressed = codec.compress_chunks(d, CS)
+    assert compressed
+    out, dcrc = codec.decompress_chunks(stream, CS, out_cap=total)
+    assert torch.equal(out, d)
+    assert dcrc == crc
