@@ -88,23 +88,61 @@ struct Group
     uint32_t start, len, depth, block;
 };
 
+// Every counter that many workgroups hit with device-scope atomics sits on its own 128-byte line:
+// same-line atomics serialise at the memory side (about 11 ns each), which made the per-bucket
+// scan cost ~58 ns per workgroup while all counters shared one line.
 struct Counters
 {
-    uint32_t n_big;         // buckets appended to the next level      } one 64-bit atomic
-    uint32_t n_tiles_next;  // tiles reserved for the next level        }
-    uint32_t n_jobs;        // wave jobs (<= JOB_MAX elements)
-    uint32_t n_mjobs;       // workgroup jobs (<= mjob_max elements)
-    uint32_t n_groups;      // fallback groups appended (next round)
-    uint32_t pad0;
-    uint32_t overflow;      // a work list overflowed (fatal)
-    uint32_t g_members;     // members of appended fallback groups
-    uint32_t hmin;          // min depth of appended fallback groups
-    uint32_t pad1;
-    uint32_t n_moved;       // elements the level's scatter moves (byte accounting)
-    uint32_t n_elems_next;
-    uint32_t n_melems;      // elements in workgroup jobs (byte accounting)
-    uint32_t pad;
+    alignas(128) uint32_t n_big;         // buckets appended to the next level      } one 64-bit atomic
+    uint32_t n_tiles_next;               // tiles reserved for the next level        }
+    alignas(128) uint32_t n_jobs;        // wave jobs (<= JOB_MAX elements)         } one 64-bit atomic
+    uint32_t n_mjobs;                    // workgroup jobs (<= mjob_max elements)   }
+    alignas(128) uint32_t n_groups;      // fallback groups appended (next round)
+    uint32_t g_members;                  // members of appended fallback groups
+    uint32_t hmin;                       // min depth of appended fallback groups
+    alignas(128) uint32_t overflow;      // a work list overflowed (fatal)
+    alignas(128) uint32_t n_moved;       // elements the level's scatter moves (byte accounting)
+    alignas(128) uint32_t n_elems_next;
+    alignas(128) uint32_t n_melems;      // elements in workgroup jobs (byte accounting)
 };
+
+// A STRING-mode MSD tile as the hist and scatter kernels need it (built with the tile order, so a
+// workgroup reaches its tile's data with one dependent load).
+struct TileDesc
+{
+    uint32_t t;       // tile index (tile_hist / tile_off row)
+    uint32_t bi;      // bucket
+    uint32_t s0;      // slot of the tile's first element
+    uint32_t cnt;     // elements in the tile
+    uint32_t d;       // bucket depth (digit = byte d, carried in the payloads)
+    uint32_t bstart;  // bucket slots [bstart, bstart + blen)
+    uint32_t blen;
+    uint32_t buf;     // KV buffer holding the bucket
+    uint32_t boff;    // block offset in the batch / block length
+    uint32_t nlen;
+    uint32_t pad[2];
+};
+
+// Ordered tile list of a level: XCD x's part is [xseg[x], xseg[x + 1]) (workgroup w works on
+// XCD w % 8's part).  desc == nullptr: natural order (tile i, RANK mode).
+struct TileOrder
+{
+    const TileDesc* desc;
+    const uint32_t* xseg;
+};
+
+// List position of a workgroup's i-th tile, or ~0u when its XCD's part is exhausted.
+__device__ __forceinline__ uint32_t tile_pos(const TileOrder& o, uint32_t i, uint32_t ntiles)
+{
+    if (!o.desc)
+    {
+        const uint32_t t = blockIdx.x + i * gridDim.x;
+        return t < ntiles ? t : ~0u;
+    }
+    const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, g = gridDim.x >> 3;
+    const uint32_t p = o.xseg[x] + l + i * g;
+    return p < o.xseg[x + 1] ? p : ~0u;
+}
 
 // Start of an MSD level.
 // Counters a level's kernels accumulate from zero.  Nothing reads a counter on the device in a
@@ -168,44 +206,50 @@ __device__ __forceinline__ uint32_t key_digit(uint64_t key, uint32_t d, uint32_t
     return (uint32_t) (key >> (56 - 8 * (d - kd))) & 0xFFu;
 }
 
+// STRING mode: the element's payload carries the digit (byte B.d of its rotation) in its top byte,
+// written by the scatter that put it into this bucket; nothing else is read.  RANK mode: the digit
+// comes from the 32-bit rank key.
 template <uint32_t MODE>
-__global__ void __launch_bounds__(TPB) k_hist(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
-                                              const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
-                                              const Counters* __restrict__ ctr, uint64_t* __restrict__ key0, uint64_t* __restrict__ key1,
+__global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
+                                              const uint64_t* __restrict__ key0, const uint64_t* __restrict__ key1,
                                               const uint32_t* __restrict__ pay0, const uint32_t* __restrict__ pay1,
-                                              uint32_t* __restrict__ tile_hist, uint32_t ntiles)
+                                              uint32_t* __restrict__ tile_hist, uint32_t ntiles, TileOrder to)
 {
     __shared__ uint32_t h[256];
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    for (uint32_t it = 0;; ++it)
     {
+        const uint32_t p = tile_pos(to, it, ntiles);
+        if (p == ~0u)
+            break;
         h[threadIdx.x] = 0;
         __syncthreads();
-        const Bucket    B     = buckets[tile_bucket[t]];
-        const uint32_t  first = (t - B.tile0) * TILE;
-        const uint32_t  cnt   = min((uint32_t) TILE, B.len - first);
-        uint64_t*       key   = B.buf ? key1 : key0;
-        const uint32_t* pay   = B.buf ? pay1 : pay0;
-        const uint32_t  kd    = eff_kd(B, MODE);
-        const bool      rekey = (MODE == MODE_STRING) && kd != B.kd;
-        const BlockDesc BD    = blocks[B.block];
-        for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
+        uint32_t t;
+        if (MODE == MODE_STRING)
         {
-            const size_t s = (size_t) B.start + first + i;
-            uint64_t     k;
-            if (rekey)
+            const TileDesc  D   = to.desc[p];
+            const uint32_t* pay = (D.buf ? pay1 : pay0) + D.s0;
+            uint32_t        v[PER_THREAD];
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
             {
-                uint32_t idx = pay[s] & 0xFFFFFFu;
-                if (!BRA_DCHECK(idx < BD.len && s >= BD.off && s < BD.off + BD.len, "hist idx %u n %u slot %llu", idx, BD.len, (unsigned long long) s))
-                    idx = 0;
-                uint32_t st = idx + (B.d % BD.len);
-                if (st >= BD.len)
-                    st -= BD.len;
-                k      = load_key8(in + BD.off, BD.len, st);
-                key[s] = k;
+                const uint32_t e = threadIdx.x + i * TPB;
+                v[i]             = e < D.cnt ? pay[e] : 0u;
             }
-            else
-                k = key[s];
-            atomicAdd(&h[key_digit(k, B.d, kd)], 1u);
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+                if (threadIdx.x + i * TPB < D.cnt)
+                    atomicAdd(&h[v[i] >> 24], 1u);
+            t = D.t;
+        }
+        else
+        {
+            t                    = p;
+            const Bucket   B     = buckets[tile_bucket[t]];
+            const uint32_t first = (t - B.tile0) * TILE;
+            const uint32_t cnt   = min((uint32_t) TILE, B.len - first);
+            const uint64_t* key  = (B.buf ? key1 : key0) + (size_t) B.start + first;
+            for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
+                atomicAdd(&h[key_digit(key[i], B.d, B.kd)], 1u);
         }
         __syncthreads();
         tile_hist[(size_t) t * 256 + threadIdx.x] = h[threadIdx.x];
@@ -243,13 +287,13 @@ struct ScanArgs
 constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into one wave job
 
 
-// One wave per bucket (4 buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
+// One wave per bucket (SCAN_WAVES buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
 // per tile; the sub-buckets become wave jobs (<= JOB_MAX; consecutive ones of <= SMALL_MAX share
 // a job: digits of one run between larger sub-buckets are grouped by floor(prefix / SMALL_MAX),
 // so every job holds < JOB_MAX elements), workgroup jobs (<= mjob_max), next-level buckets (with
 // their tiles) or fallback groups.  The four waves' list slots are reserved with one atomic per
 // list per workgroup (jobs and workgroup jobs share a 64-bit atomic, so do buckets and tiles).
-constexpr int SCAN_WAVES = 4;
+constexpr int SCAN_WAVES = 16;
 
 struct ScanWaveCounts
 {
@@ -311,12 +355,21 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         uint32_t base[4];
         wave_excl_sum4(tot, base);
         {
+            // bit 31 (STRING mode): the sub-bucket is a next-level bucket, so the scatter loads the
+            // next digit of its elements (slots are < 2^31)
+            uint32_t flag[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const bool nb = (MODE == MODE_STRING) && tot[r] > a.mjob_max && B.d + 1 < a.dcap;
+                flag[r]       = nb ? 0x80000000u : 0u;
+            }
             uint4*   to     = reinterpret_cast<uint4*>(a.tile_off + (size_t) B.tile0 * 256) + lane;
             uint32_t run[4] = {B.start + base[0], B.start + base[1], B.start + base[2], B.start + base[3]};
             for (uint32_t t = 0; t < ntiles; ++t)
             {
                 const uint4 h        = th[(size_t) t * 64];
-                to[(size_t) t * 64] = make_uint4(run[0], run[1], run[2], run[3]);
+                to[(size_t) t * 64] = make_uint4(run[0] | flag[0], run[1] | flag[1], run[2] | flag[2], run[3] | flag[3]);
                 run[0] += h.x;
                 run[1] += h.y;
                 run[2] += h.z;
@@ -324,11 +377,21 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
             }
         }
         const bool     nomove = active && __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
+        // STRING mode: a bucket that does not move but continues as a next-level bucket still needs
+        // its elements' next digit (nomove code 2: the scatter updates the payloads in place)
+        bool nm_next = false;
+        if (MODE == MODE_STRING && nomove)
+        {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                nm_next |= (tot[r] == B.len) && tot[r] > a.mjob_max && B.d + 1 < a.dcap;
+            nm_next = __any(nm_next);
+        }
         const uint32_t kd     = eff_kd(B, MODE);
         const uint32_t nd     = B.d + 1;
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
         if (active && lane == 0)
-            a.nomove[bi] = nomove ? 1 : 0;
+            a.nomove[bi] = nomove ? (nm_next ? 2 : 1) : 0;
         bool big[4], med[4], mid[4], small[4], fin[4], nbn[4];
         uint32_t xs[4], xb[4], xp[4];
 #pragma unroll
@@ -542,6 +605,43 @@ struct TileStage
     uint32_t tmp[8];
 };
 
+// STRING-mode tile staging: payloads only (the digit is in the payload's top byte).
+struct TileStageP
+{
+    uint32_t pay[TILE];
+    uint32_t cnt[256];
+    uint32_t base[256];
+    uint32_t goff[256];  // sub-bucket slot of the tile's first element per digit (bit 31: next-level bucket)
+    uint32_t tmp[8];
+};
+constexpr uint32_t NEXT_FLAG = 0x80000000u;
+
+// Ranks the tile's elements by digit in LDS and stages them in digit order; returns nothing, the
+// caller reads S.pay[q] back in order (coalesced output runs per digit).
+__device__ __forceinline__ void stage_p(TileStageP& S, const uint32_t (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
+{
+    uint32_t rank[PER_THREAD];
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i)
+    {
+        const uint32_t e = threadIdx.x + i * TPB;
+        if (e < cnt)
+            rank[i] = atomicAdd(&S.cnt[dgt[i]], 1u);
+    }
+    __syncthreads();
+    const uint32_t c    = S.cnt[threadIdx.x];
+    S.base[threadIdx.x] = block256_exclusive_sum(c, S.tmp);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER_THREAD; ++i)
+    {
+        const uint32_t e = threadIdx.x + i * TPB;
+        if (e < cnt)
+            S.pay[S.base[dgt[i]] + rank[i]] = v[i];
+    }
+    __syncthreads();
+}
+
 // Writes the staged tile (already in TileStage.key/pay, count `cnt`, digit base `base`) to global.
 __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k)[PER_THREAD], const uint32_t (&v)[PER_THREAD],
                                                 const uint32_t (&dgt)[PER_THREAD], uint32_t cnt, uint32_t d, uint32_t kd,
@@ -590,14 +690,14 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
     }
 }
 
+// Level 0: every element gets payload (byte 1 << 24 | index): its next digit.
 __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
                                                     const L0Tile* __restrict__ tiles, uint32_t ntiles,
-                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ okey,
-                                                    uint32_t* __restrict__ opay)
+                                                    const uint32_t* __restrict__ tile_off, uint32_t* __restrict__ opay)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStage& S   = *reinterpret_cast<TileStage*>(smem);
-    uint8_t*   win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStage));  // TILE + 32 bytes, 16-aligned
+    TileStageP& S   = *reinterpret_cast<TileStageP*>(smem);
+    uint8_t*    win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageP));  // TILE + 32 bytes, 16-aligned
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile    T   = tiles[t];
@@ -623,32 +723,137 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
             }
         }
         S.cnt[threadIdx.x]  = 0;
-        S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x];
+        S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x] & ~NEXT_FLAG;
         __syncthreads();
-        uint64_t k[PER_THREAD];
         uint32_t v[PER_THREAD], dg[PER_THREAD];
 #pragma unroll
         for (int i = 0; i < PER_THREAD; ++i)
         {
             const uint32_t e = threadIdx.x + i * TPB;
-            if (e < cnt)
+            dg[i]            = win[e + 16];  // rotation byte 0 (e < cnt; unused otherwise)
+            v[i]             = (dg[i] << 24) | e;
+        }
+        stage_p(S, v, dg, cnt);
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i)
+        {
+            const uint32_t q = threadIdx.x + i * TPB;
+            if (q < cnt)
             {
-                // bytes [e + 16, e + 24) of the window = rotation bytes 0..7; win[e + 15] = previous byte
-                const uint32_t  o  = e + 16;
-                const uint32_t* w4 = reinterpret_cast<const uint32_t*>(win) + (o >> 2);
-                const uint32_t  a0 = w4[0], a1 = w4[1], a2 = w4[2], sh = o & 3;
-                const uint32_t  lo = __builtin_amdgcn_alignbyte(a1, a0, sh), hi = __builtin_amdgcn_alignbyte(a2, a1, sh);
-                const uint64_t  kk = __builtin_bswap64(((uint64_t) hi << 32) | lo);
-                k[i]               = kk;
-                v[i]               = ((uint32_t) win[e + 15] << 24) | (T.start + e);
-                dg[i]              = (uint32_t) (kk >> 56);
+                const uint32_t vv   = S.pay[q];
+                const uint32_t dd   = vv >> 24, e = vv & 0xFFFFFFu;
+                const uint32_t slot = S.goff[dd] + (q - S.base[dd]);
+                if (BRA_DCHECK(slot >= B.off && slot < B.off + B.len, "l0 scatter slot %u outside block %u", slot, T.block))
+                    opay[slot] = ((uint32_t) win[e + 17] << 24) | (T.start + e);
             }
         }
-        stage_and_write(S, k, v, dg, cnt, 0, 0, okey, opay, B.off, B.off + B.len);
         __syncthreads();
     }
 }
 
+// STRING-mode MSD scatter: payloads only.  An element whose sub-bucket continues as a next-level
+// bucket (tile_off bit 31) gets its next digit, byte d + 1 of its rotation, gathered from the
+// input (the block is in the XCD's L2 or the Infinity Cache); others keep their payload (jobs only
+// use the index).  nomove 1: the bucket stays as it is; 2: it stays in place but continues, so
+// only the digits are updated.
+__global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
+                                                   const uint32_t* __restrict__ tile_off, uint32_t* __restrict__ pay0,
+                                                   uint32_t* __restrict__ pay1, uint32_t ntiles, TileOrder to)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    TileStageP& S = *reinterpret_cast<TileStageP*>(smem);
+    for (uint32_t it = 0;; ++it)
+    {
+        const uint32_t p = tile_pos(to, it, ntiles);
+        if (p == ~0u)
+            break;
+        const TileDesc D  = to.desc[p];
+        const uint32_t nm = nomove[D.bi];
+        if (nm == 1)
+            continue;  // uniform per workgroup
+        const uint32_t t   = D.t;
+        const uint8_t* blk = in + D.boff;
+        const uint32_t cnt = D.cnt;
+        struct
+        {
+            uint32_t off, len;
+        } BD{D.boff, D.nlen};
+        struct
+        {
+            uint32_t start, len, d, buf;
+        } B{D.bstart, D.blen, D.d, D.buf};
+        const uint32_t  dn = (B.d + 1) % BD.len;  // next digit's depth
+        const size_t    s0 = D.s0;
+        uint32_t*       ip = (B.buf ? pay1 : pay0) + s0;
+        if (nm == 2)
+        {
+            uint32_t v[PER_THREAD];
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+            {
+                const uint32_t e = threadIdx.x + i * TPB;
+                if (e < cnt)
+                    v[i] = ip[e];
+            }
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+            {
+                const uint32_t e = threadIdx.x + i * TPB;
+                if (e < cnt)
+                {
+                    const uint32_t idx = v[i] & 0xFFFFFFu;
+                    uint32_t       st  = idx + dn;
+                    if (st >= BD.len)
+                        st -= BD.len;
+                    ip[e] = ((uint32_t) blk[st] << 24) | idx;
+                }
+            }
+            continue;
+        }
+        uint32_t* op        = B.buf ? pay0 : pay1;
+        S.cnt[threadIdx.x]  = 0;
+        S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x];
+        __syncthreads();
+        uint32_t v[PER_THREAD], dg[PER_THREAD];
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i)
+        {
+            const uint32_t e = threadIdx.x + i * TPB;
+            v[i]             = (e < cnt) ? ip[e] : 0u;
+            dg[i]            = v[i] >> 24;
+        }
+        stage_p(S, v, dg, cnt);
+        uint32_t slot[PER_THREAD], nv[PER_THREAD];
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i)
+        {
+            const uint32_t q = threadIdx.x + i * TPB;
+            slot[i]          = 0xFFFFFFFFu;
+            if (q < cnt)
+            {
+                const uint32_t vv = S.pay[q];
+                const uint32_t dd = vv >> 24, g = S.goff[dd];
+                slot[i]           = (g & ~NEXT_FLAG) + (q - S.base[dd]);
+                nv[i]             = vv;
+                if (g & NEXT_FLAG)
+                {
+                    const uint32_t idx = vv & 0xFFFFFFu;
+                    uint32_t       st  = idx + dn;
+                    if (st >= BD.len)
+                        st -= BD.len;
+                    nv[i] = ((uint32_t) blk[st] << 24) | idx;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < PER_THREAD; ++i)
+            if (slot[i] != 0xFFFFFFFFu && BRA_DCHECK(slot[i] >= B.start && slot[i] < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot[i], B.start, B.len))
+                op[slot[i]] = nv[i];
+        __syncthreads();
+    }
+}
+
+// RANK-mode MSD scatter (fallback rounds): 8-byte keys + payloads.
 __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buckets, const uint8_t* __restrict__ nomove,
                                                  const uint32_t* __restrict__ tile_bucket, const Counters* __restrict__ ctr,
                                                  const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ key0,
@@ -673,7 +878,7 @@ __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buck
         uint64_t*       ok    = B.buf ? key0 : key1;
         uint32_t*       op    = B.buf ? pay0 : pay1;
         S.cnt[threadIdx.x]    = 0;
-        S.goff[threadIdx.x]   = tile_off[(size_t) t * 256 + threadIdx.x];
+        S.goff[threadIdx.x]   = tile_off[(size_t) t * 256 + threadIdx.x] & ~NEXT_FLAG;
         __syncthreads();
         uint64_t k[PER_THREAD];
         uint32_t v[PER_THREAD], dg[PER_THREAD];
@@ -1123,12 +1328,17 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             }
             else
             {
-                uint32_t st = (v[r] & 0xFFFFFFu) + ((depth - 1) % BD.len);
+                // STRING payloads carry an MSD digit in the top byte: replace it by the rotation's
+                // previous byte (its BWT output byte), gathered together with the key
+                const uint32_t idx = v[r] & 0xFFFFFFu;
+                uint32_t       st  = idx + ((depth - 1) % BD.len);
                 if (st >= BD.len)
                     st -= BD.len;
-                uint64_t w0, w1;
+                const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
+                uint64_t      w0, w1;
                 load_key16(blk, BD.len, st, w0, w1);
                 make_key1<W>(c, w0, w1, kh[r], kl[r]);
+                v[r] = ((uint32_t) lb << 24) | idx;
             }
         }
         S.v[c] = v[r];
@@ -1296,25 +1506,176 @@ __global__ void __launch_bounds__(64 * W, JOB_MIN_WAVES) k_mjobs(JobArgs a)
 
 // Block-major, XCD-major job order: key(b) = (b % 8) * kb + b / 8.
 // Size class first (jobs longer than split_len after the others; split_len 0 = one class).
-__device__ __forceinline__ uint32_t job_key(const Job& J, uint32_t kb, uint32_t split_len)
+// With many blocks, q consecutive blocks of one XCD share a key (q = 1 up to 8192 blocks), so the
+// keys of a list fit the LDS counters of the ordering kernels.
+__device__ __forceinline__ uint32_t job_key(const Job& J, uint32_t kb, uint32_t q, uint32_t split_len)
 {
     const uint32_t sc = (split_len && J.len > split_len) ? 1u : 0u;
-    return sc * 8 * kb + (J.block & 7u) * kb + (J.block >> 3);
+    return sc * 8 * kb + (J.block & 7u) * kb + (J.block >> 3) / q;
 }
 
-__global__ void k_job_count(const Job* __restrict__ jobs, uint32_t n, uint32_t kb, uint32_t split_len, uint32_t* __restrict__ cnt)
-{
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
-        atomicAdd(&cnt[job_key(jobs[j], kb, split_len)], 1u);
-}
+constexpr uint32_t JOB_CHUNK = 4096;  // jobs per workgroup of the ordering kernels (256 threads x 16)
 
-__global__ void k_job_scatter(const Job* __restrict__ in, uint32_t n, uint32_t kb, uint32_t split_len, uint32_t* __restrict__ cursor,
-                              Job* __restrict__ out)
+// Per-key job counts.  Each workgroup counts a chunk of the list in LDS and adds its nonzero counts
+// to the global ones (one atomic per key and workgroup instead of one per job: thousands of jobs of
+// one block share a key, and same-address device atomics serialise).  nkeys <= lds capacity.
+__global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs, uint32_t n, uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys,
+                                                   uint32_t* __restrict__ cnt)
 {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x)
+    extern __shared__ uint32_t h[];
+    for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
-        const Job J = in[j];
-        out[atomicAdd(&cursor[job_key(J, kb, split_len)], 1u)] = J;
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            h[k] = 0;
+        __syncthreads();
+        const uint32_t c1 = min(n, c0 + JOB_CHUNK);
+        for (uint32_t j = c0 + threadIdx.x; j < c1; j += 256)
+            atomicAdd(&h[job_key(jobs[j], kb, q, split_len)], 1u);
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            if (h[k])
+                atomicAdd(&cnt[k], h[k]);
+        __syncthreads();
+    }
+}
+
+// Scatter into key order: per chunk, local ranks from LDS atomics, one global cursor reservation per
+// nonzero key and workgroup.  (Job order within a key only affects speed.)
+__global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in, uint32_t n, uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys,
+                                                     uint32_t* __restrict__ cursor, Job* __restrict__ out)
+{
+    extern __shared__ uint32_t h[];
+    constexpr int PT = JOB_CHUNK / 256;
+    for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
+    {
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            h[k] = 0;
+        __syncthreads();
+        uint32_t key[PT], rank[PT];
+#pragma unroll
+        for (int i = 0; i < PT; ++i)
+        {
+            const uint32_t j = c0 + threadIdx.x + i * 256;
+            if (j < n)
+            {
+                key[i]  = job_key(in[j], kb, q, split_len);
+                rank[i] = atomicAdd(&h[key[i]], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            if (h[k])
+                h[k] = atomicAdd(&cursor[k], h[k]);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PT; ++i)
+        {
+            const uint32_t j = c0 + threadIdx.x + i * 256;
+            if (j < n)
+                out[h[key[i]] + rank[i]] = in[j];
+        }
+        __syncthreads();
+    }
+}
+
+// MSD tile order.  A level's tiles (tile_bucket, in the order the scan reserved them) are listed
+// XCD-major and block-major: the key of a tile is that of its block (job_key without size class).
+// Workgroup w then works on XCD w % 8's part of the list, tiles of the blocks b = x (mod 8) in block
+// order, so the digit gathers of the scatter hit the one or two blocks its XCD's L2 holds.
+__device__ __forceinline__ uint32_t tile_key(uint32_t block, uint32_t kb, uint32_t q) { return (block & 7u) * kb + (block >> 3) / q; }
+
+__global__ void __launch_bounds__(256) k_tile_count(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket, uint32_t n,
+                                                    uint32_t kb, uint32_t q, uint32_t nkeys, uint32_t* __restrict__ cnt)
+{
+    extern __shared__ uint32_t h[];
+    for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
+    {
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            h[k] = 0;
+        __syncthreads();
+        const uint32_t c1 = min(n, c0 + JOB_CHUNK);
+        for (uint32_t j = c0 + threadIdx.x; j < c1; j += 256)
+            atomicAdd(&h[tile_key(buckets[tile_bucket[j]].block, kb, q)], 1u);
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            if (h[k])
+                atomicAdd(&cnt[k], h[k]);
+        __syncthreads();
+    }
+}
+
+// One workgroup: exclusive prefix of the key counts into cursors, per-XCD list ranges into xseg[0..8].
+__global__ void __launch_bounds__(256) k_tile_prefix(const uint32_t* __restrict__ cnt, uint32_t nkeys, uint32_t kb, uint32_t* __restrict__ cursor,
+                                                     uint32_t* __restrict__ xseg)
+{
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0)
+        carry = 0;
+    __syncthreads();
+    for (uint32_t k0 = 0; k0 < nkeys; k0 += 256)
+    {
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t c = k < nkeys ? cnt[k] : 0u;
+        uint32_t       tot;
+        const uint32_t ex = block256_exclusive_sum(c, tmp, &tot) + carry;
+        if (k < nkeys)
+        {
+            cursor[k] = ex;
+            if (k % kb == 0)
+                xseg[k / kb] = ex;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        xseg[8] = carry;
+}
+
+__global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket, uint32_t n,
+                                                      uint32_t kb, uint32_t q, uint32_t nkeys, uint32_t* __restrict__ cursor,
+                                                      const BlockDesc* __restrict__ blocks, TileDesc* __restrict__ order)
+{
+    extern __shared__ uint32_t h[];
+    constexpr int PT = JOB_CHUNK / 256;
+    for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
+    {
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            h[k] = 0;
+        __syncthreads();
+        uint32_t key[PT], rank[PT];
+#pragma unroll
+        for (int i = 0; i < PT; ++i)
+        {
+            const uint32_t j = c0 + threadIdx.x + i * 256;
+            if (j < n)
+            {
+                key[i]  = tile_key(buckets[tile_bucket[j]].block, kb, q);
+                rank[i] = atomicAdd(&h[key[i]], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
+            if (h[k])
+                h[k] = atomicAdd(&cursor[k], h[k]);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PT; ++i)
+        {
+            const uint32_t j = c0 + threadIdx.x + i * 256;
+            if (j < n)
+            {
+                const uint32_t  bi = tile_bucket[j];
+                const Bucket    B  = buckets[bi];
+                const BlockDesc BD = blocks[B.block];
+                const uint32_t  f  = (j - B.tile0) * TILE;
+                order[h[key[i]] + rank[i]] =
+                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, (uint32_t) BD.off, BD.len, {0, 0}};
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -1506,6 +1867,8 @@ struct BwtWorkspace
     Job*      mjobs_sorted   = nullptr;
     uint32_t* job_cnt        = nullptr;  // 2 lists x 2 size classes x 8 * ceil(blocks / 8) keys, then the cursors
     uint32_t* h_job_cnt      = nullptr;  // pinned: counts back, cursors out
+    uint32_t* tile_cnt       = nullptr;  // MSD tile order: key counts, cursors, xseg[9]
+    TileDesc* tile_order     = nullptr;
     Group*    groups[2]      = {nullptr, nullptr};
     Counters* ctr            = nullptr;
     Counters* h_ctr          = nullptr;  // pinned
@@ -1514,6 +1877,7 @@ struct BwtWorkspace
     int       grid = 2048;
     int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
     uint32_t  jobs_grid = 8192;         // workgroups of the wave-job launch (env BRA_JOBS_GRID)
+    uint32_t  nblocks   = 0;            // blocks of the current call
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
@@ -1523,7 +1887,8 @@ struct BwtWorkspace
 // out[0] wave jobs, out[1] small workgroup jobs, out[2] large ones.
 static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[3], hipStream_t s)
 {
-    const uint32_t kb = div_up(nblocks, 8), nk = 8 * kb;  // keys per size class
+    const uint32_t kb0 = div_up(nblocks, 8), q = div_up(kb0, 1024u);
+    const uint32_t kb = div_up(kb0, q), nk = 8 * kb;  // keys per size class (<= 8192)
     const uint32_t n[2]     = {ja.njobs, jm.njobs};
     const uint32_t split[2] = {0, w.mjob_max() / 2};
     const Job*     src[2]   = {w.jobs, w.mjobs};
@@ -1534,8 +1899,8 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, con
     for (int l = 0; l < 2; ++l)
         if (n[l])
         {
-            hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb, split[l],
-                               dcnt + (size_t) l * 2 * nk);
+            hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], JOB_CHUNK), 2048u)), dim3(256), 2 * nk * 4, s, src[l], n[l], kb,
+                               q, split[l], 2 * nk, dcnt + (size_t) l * 2 * nk);
             BRA_DSYNC(s);
         }
     BRA_HIP_CHECK(hipMemcpyAsync(w.h_job_cnt, dcnt, 4 * (size_t) nk * 4, hipMemcpyDeviceToHost, s));
@@ -1573,8 +1938,8 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, con
     for (int l = 0; l < 2; ++l)
         if (n[l])
         {
-            hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], 256), 1024u)), dim3(256), 0, s, src[l], n[l], kb, split[l],
-                               dcur + (size_t) l * 2 * nk, dst[l]);
+            hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], JOB_CHUNK), 2048u)), dim3(256), 2 * nk * 4, s, src[l], n[l], kb,
+                               q, split[l], 2 * nk, dcur + (size_t) l * 2 * nk, dst[l]);
             BRA_DSYNC(s);
         }
     BRA_HIP_CHECK(hipGetLastError());
@@ -1623,6 +1988,8 @@ static void ws_free(BwtWorkspace& w)
     (void) hipFree(w.jobs_sorted);
     (void) hipFree(w.mjobs_sorted);
     (void) hipFree(w.job_cnt);
+    (void) hipFree(w.tile_cnt);
+    (void) hipFree(w.tile_order);
     (void) hipHostFree(w.h_job_cnt);
     (void) hipFree(w.mjobs);
     (void) hipFree(w.ctr);
@@ -1687,6 +2054,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     BRA_HIP_CHECK(hipMalloc(&w.mjobs_sorted, (size_t) w.cap_mjobs * sizeof(Job)));
     const size_t nkeys = 8 * (size_t) div_up(B, 8);
     BRA_HIP_CHECK(hipMalloc(&w.job_cnt, 8 * nkeys * 4));
+    BRA_HIP_CHECK(hipMalloc(&w.tile_cnt, (2 * nkeys + 16) * 4));
+    BRA_HIP_CHECK(hipMalloc(&w.tile_order, (size_t) w.cap_tiles * sizeof(TileDesc)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
     BRA_HIP_CHECK(hipMalloc(&w.l0tiles, (size_t) w.cap_l0 * sizeof(L0Tile)));
@@ -1729,10 +2098,25 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
     while (nbig > 0)
     {
         hipLaunchKernelGGL(k_level_start, dim3(1), dim3(1), 0, s, w.ctr); BRA_DSYNC(s);
+        TileOrder to{nullptr, nullptr};
+        if (MODE == MODE_STRING)
+        {
+            // XCD-major, block-major tile list (the scatter's digit gathers stay in the XCD's L2)
+            const uint32_t kb0 = div_up(w.nblocks, 8), q = div_up(kb0, 1024u), kb = div_up(kb0, q), nk = 8 * kb;
+            uint32_t*      cnt = w.tile_cnt, *cur_ = w.tile_cnt + nk, *xs = w.tile_cnt + 2 * nk;
+            const dim3     g(std::min<uint32_t>(div_up(ntiles, JOB_CHUNK), 1024u));
+            BRA_HIP_CHECK(hipMemsetAsync(cnt, 0, nk * 4, s));
+            hipLaunchKernelGGL(k_tile_count, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cnt); BRA_DSYNC(s);
+            hipLaunchKernelGGL(k_tile_prefix, dim3(1), dim3(256), 0, s, cnt, nk, kb, cur_, xs); BRA_DSYNC(s);
+            hipLaunchKernelGGL(k_tile_scatter, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cur_, d_blocks,
+                               w.tile_order);
+            BRA_DSYNC(s);
+            to = TileOrder{w.tile_order, xs};
+        }
         {
             BRA_PROF(P_BWT_HIST, s);
-            hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, d_in, d_blocks, w.big[cur], w.tile_bucket[cur], w.ctr, w.key[0],
-                               w.key[1], w.pay[0], w.pay[1], w.tile_hist, ntiles); BRA_DSYNC(s);
+            hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
+                               w.pay[1], w.tile_hist, ntiles, to); BRA_DSYNC(s);
         }
         ScanArgs a{d_blocks, w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
                    w.cap_big,   w.tile_bucket[cur ^ 1],   w.cap_tiles, w.jobs,       w.cap_jobs,
@@ -1744,8 +2128,13 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         }
         {
             BRA_PROF(P_BWT_SCATTER, s);
-            hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
-                               w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles); BRA_DSYNC(s);
+            if (MODE == MODE_STRING)
+                hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageP), s, d_in, w.nomove, w.tile_off, w.pay[0], w.pay[1],
+                                   ntiles, to);
+            else
+                hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
+                                   w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles);
+            BRA_DSYNC(s);
         }
         BRA_HIP_CHECK(hipGetLastError());
         if (!read_ctr(w, s))
@@ -1753,9 +2142,11 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         // algorithmic bytes: keys read by the histogram, tile histograms, KV moved by the scatter
         const double nt = ntiles, ne = nelems, nm = w.h_ctr->n_moved;
         nelems          = w.h_ctr->n_elems_next;
-        prof_bytes(P_BWT_HIST, 8.0 * ne + 1024.0 * nt);
+        // STRING: 4-byte payloads (+ the next digit gathered for elements that stay in big buckets)
+        const double eb = (MODE == MODE_STRING) ? 4.0 : 8.0, mb = (MODE == MODE_STRING) ? 9.0 : 24.0;
+        prof_bytes(P_BWT_HIST, eb * ne + 1024.0 * nt);
         prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * nbig);
-        prof_bytes(P_BWT_SCATTER, 24.0 * nm + 1024.0 * nt);
+        prof_bytes(P_BWT_SCATTER, mb * nm + 1024.0 * nt);
         nbig   = w.h_ctr->n_big;
         ntiles = w.h_ctr->n_tiles_next;
         cur ^= 1;
@@ -1784,6 +2175,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     if (!ws_reserve(w, N, nblocks))
         return false;
+    w.nblocks = nblocks;
 #ifdef BRA_DEBUG
     // poison every work buffer so that a read of anything this call did not write shows up
     for (int i = 0; i < 2; ++i)
@@ -1808,7 +2200,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (lds + TILE + 48)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageP) + TILE + 48)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>)));
@@ -1845,15 +2237,15 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
-        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), tile_stage_bytes() + TILE + 48, s, d_in, d_blocks,
-                           w.l0tiles, nt0, w.tile_off, w.key[0], w.pay[0]); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageP) + TILE + 48, s, d_in, d_blocks,
+                           w.l0tiles, nt0, w.tile_off, w.pay[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
         return false;
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
-    prof_bytes(P_BWT_L0SCATTER, 13.0 * N + 1024.0 * nt0);
+    prof_bytes(P_BWT_L0SCATTER, 5.0 * N + 1024.0 * nt0);  // window in, payload out
     // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]
     if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, w.h_ctr->n_tiles_next, 0, w.groups[0], s))
         return false;
@@ -1899,9 +2291,10 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof ph));
     }
 #endif
-    // read key+payload, write SA entry + L byte (split by the elements each kind of job covers)
-    prof_bytes(P_BWT_JOBS, 17.0 * ((double) N - (double) w.h_ctr->n_melems));
-    prof_bytes(P_BWT_MJOBS, 17.0 * (double) w.h_ctr->n_melems);
+    // payload in, SA entry + L byte out, 16 key bytes + the previous byte gathered (split by the
+    // elements each kind of job covers)
+    prof_bytes(P_BWT_JOBS, 26.0 * ((double) N - (double) w.h_ctr->n_melems));
+    prof_bytes(P_BWT_MJOBS, 26.0 * (double) w.h_ctr->n_melems);
 
     // ---- fallback: prefix doubling on the groups still tied ----
     uint32_t ng = w.h_ctr->n_groups;
