@@ -22,7 +22,9 @@ import os
 from dataclasses import dataclass
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbra_hip.so")
+# BRA_HIP_LIB: an alternative build of the same library (measurement variants built by
+# scripts/build_variants.sh); the default is the in-tree product library.
+LIB_PATH = os.environ.get("BRA_HIP_LIB") or os.path.join(HERE, "libbra_hip.so")
 SYNTH_PATH = os.path.join(HERE, "libbra_synth.so")
 
 # Exported symbols of include/bra_hip.h (checked by tests/test_abi.py against the header).

@@ -158,22 +158,23 @@ __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
 }
 
 // Value of x held by lane (lane ^ LM), LM in {1, 2, 4, 8, 16, 32}, without going through LDS:
-// DPP quad permutes / row rotate / row shifts inside a row of 16, permlane swaps across rows.
+// DPP quad permutes / row rotate inside a row of 16 (one instruction each), xor 4 as two row shifts
+// writing complementary bank masks (lanes with bit 2 clear take lane + 4, the others lane - 4), and
+// permlane swaps across rows.
 template <int LM>
 __device__ __forceinline__ uint32_t xlane(uint32_t x)
 {
     if constexpr (LM == 1)
-        return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        return (uint32_t) __builtin_amdgcn_mov_dpp((int) x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
     else if constexpr (LM == 2)
-        return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        return (uint32_t) __builtin_amdgcn_mov_dpp((int) x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
     else if constexpr (LM == 4)
     {
-        const uint32_t up = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x104, 0xF, 0xF, false);  // row_shl:4, lane i <- i+4
-        const uint32_t dn = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x114, 0xF, 0xF, false);  // row_shr:4, lane i <- i-4
-        return (lane_id() & 4) ? dn : up;
+        const int up = __builtin_amdgcn_mov_dpp((int) x, 0x104, 0xF, 0x5, false);             // row_shl:4 into banks 0, 2
+        return (uint32_t) __builtin_amdgcn_update_dpp(up, (int) x, 0x114, 0xF, 0xA, false);  // row_shr:4 into banks 1, 3
     }
     else if constexpr (LM == 8)
-        return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x128, 0xF, 0xF, false);  // row_ror:8
+        return (uint32_t) __builtin_amdgcn_mov_dpp((int) x, 0x128, 0xF, 0xF, true);  // row_ror:8
     else if constexpr (LM == 16)
     {
         const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
@@ -185,6 +186,59 @@ __device__ __forceinline__ uint32_t xlane(uint32_t x)
         const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);
         return (lane_id() & 32) ? p[0] : p[1];
     }
+}
+
+// 128-bit keys as four dwords (k0 lowest).  k > o is the borrow out of the 128-bit subtraction
+// o - k: four chained VALU subtractions into VCC, so a compare-exchange is 4 subtractions, one SALU
+// xnor with a lane mask and 4 selects (the C++ form compiles to three 64-bit compares, SALU
+// and/or and the selects).  Dword operands keep the compiler from pairing registers.
+// Compare-exchange with the partner's key o: the lanes whose (k > o) equals their bit of
+// `keep_min` take o.
+__device__ __forceinline__ void cx128(uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t& k3, uint32_t o0, uint32_t o1, uint32_t o2,
+                                      uint32_t o3, uint64_t keep_min)
+{
+    uint32_t t;
+    asm volatile(
+        "v_sub_co_u32 %[t], vcc, %[o0], %[k0]\n\t"
+        "v_subb_co_u32 %[t], vcc, %[o1], %[k1], vcc\n\t"
+        "v_subb_co_u32 %[t], vcc, %[o2], %[k2], vcc\n\t"
+        "v_subb_co_u32 %[t], vcc, %[o3], %[k3], vcc\n\t"
+        "s_xnor_b64 vcc, vcc, %[km]\n\t"
+        "v_cndmask_b32 %[k0], %[k0], %[o0], vcc\n\t"
+        "v_cndmask_b32 %[k1], %[k1], %[o1], vcc\n\t"
+        "v_cndmask_b32 %[k2], %[k2], %[o2], vcc\n\t"
+        "v_cndmask_b32 %[k3], %[k3], %[o3], vcc"
+        : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1), [k2] "+v"(k2), [k3] "+v"(k3)
+        : [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2), [o3] "v"(o3), [km] "s"(keep_min)
+        : "vcc");
+}
+
+// In-lane compare-exchange of keys a and b: afterwards a < b in the lanes set in `asc`, a > b in
+// the others (the selects write fresh registers, so no copies).
+__device__ __forceinline__ void cx128_pair(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& a3, uint32_t& b0, uint32_t& b1, uint32_t& b2,
+                                           uint32_t& b3, uint64_t asc)
+{
+    uint32_t t, n0, n1, n2, n3, m0, m1, m2, m3;
+    asm volatile(
+        "v_sub_co_u32 %[t], vcc, %[b0], %[a0]\n\t"
+        "v_subb_co_u32 %[t], vcc, %[b1], %[a1], vcc\n\t"
+        "v_subb_co_u32 %[t], vcc, %[b2], %[a2], vcc\n\t"
+        "v_subb_co_u32 %[t], vcc, %[b3], %[a3], vcc\n\t"
+        "s_xnor_b64 vcc, vcc, %[asc]\n\t"
+        "v_cndmask_b32 %[n0], %[a0], %[b0], vcc\n\t"
+        "v_cndmask_b32 %[m0], %[b0], %[a0], vcc\n\t"
+        "v_cndmask_b32 %[n1], %[a1], %[b1], vcc\n\t"
+        "v_cndmask_b32 %[m1], %[b1], %[a1], vcc\n\t"
+        "v_cndmask_b32 %[n2], %[a2], %[b2], vcc\n\t"
+        "v_cndmask_b32 %[m2], %[b2], %[a2], vcc\n\t"
+        "v_cndmask_b32 %[n3], %[a3], %[b3], vcc\n\t"
+        "v_cndmask_b32 %[m3], %[b3], %[a3], vcc"
+        : [t] "=&v"(t), [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2),
+          [m3] "=&v"(m3)
+        : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [b3] "v"(b3), [asc] "s"(asc)
+        : "vcc");
+    a0 = n0, a1 = n1, a2 = n2, a3 = n3;
+    b0 = m0, b1 = m1, b2 = m2, b3 = m3;
 }
 
 template <int LM>

@@ -1070,26 +1070,18 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
     total = wtot;
 }
 
-// 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian.  Non-wrapping reads
-// take one or two aligned 16-byte loads (the second only for an unaligned start: then both hold
-// in-range bytes, so the read never leaves the buffer's pages) and a funnel shift.
+// 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian.  A non-wrapping read is
+// one 16-byte load at the byte address (gfx950 global loads need no alignment; one L2 request
+// unless it straddles a line, where two aligned loads always made two).
+typedef uint4 __attribute__((aligned(1))) uint4_u;
+
 __device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint32_t n, uint32_t start, uint64_t& w0, uint64_t& w1)
 {
     if (start + 16u <= n)
     {
-        const uintptr_t a  = (uintptr_t) (blk + start);
-        const uint4*    p  = (const uint4*) (a & ~(uintptr_t) 15);
-        const uint4     q0 = p[0];
-        const uint4     q1 = (a & 15) ? p[1] : make_uint4(0, 0, 0, 0);  // an aligned start needs 16 bytes only
-        const uint64_t  u0 = ((uint64_t) q0.y << 32) | q0.x, u1 = ((uint64_t) q0.w << 32) | q0.z;
-        const uint64_t  u2 = ((uint64_t) q1.y << 32) | q1.x, u3 = ((uint64_t) q1.w << 32) | q1.z;
-        const bool      hi = (a & 8) != 0;
-        const uint64_t  A = hi ? u1 : u0, B = hi ? u2 : u1, C = hi ? u3 : u2;
-        const uint32_t  sh = (uint32_t) (a & 7) * 8;
-        const uint64_t  r0 = sh ? (A >> sh) | (B << (64 - sh)) : A;
-        const uint64_t  r1 = sh ? (B >> sh) | (C << (64 - sh)) : B;
-        w0                 = __builtin_bswap64(r0);
-        w1                 = __builtin_bswap64(r1);
+        const uint4 q = *reinterpret_cast<const uint4_u*>(blk + start);
+        w0            = __builtin_bswap64(((uint64_t) q.y << 32) | q.x);
+        w1            = __builtin_bswap64(((uint64_t) q.w << 32) | q.z);
         return;
     }
     w0          = load_key8(blk, n, start);
@@ -1103,30 +1095,38 @@ __device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint
 // 128-bit key (kh, kl) "greater than"; keys are unique (the slot is in the low bits of kl).
 __device__ __forceinline__ bool k2_gt(uint64_t ha, uint64_t la, uint64_t hb, uint64_t lb) { return ha > hb || (ha == hb && la > lb); }
 
-// One bitonic stage whose partners sit LM lanes away (same register r): exchanged with DPP /
-// permlane swaps.  keep_min: this lane keeps the smaller key of each pair.
+// One bitonic stage whose partners sit LM lanes away (same element r): exchanged with DPP /
+// permlane swaps.  k[i][r] = dword i of element r's key.
 template <int LM>
-__device__ __forceinline__ void net_stage_lanes(uint64_t (&kh)[4], uint64_t (&kl)[4], bool keep_min)
+__device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[4][4], uint64_t keep_min)
 {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        const uint64_t oh = xlane64<LM>(kh[r]), ol = xlane64<LM>(kl[r]);
-        if (k2_gt(kh[r], kl[r], oh, ol) == keep_min)
-        {
-            kh[r] = oh;
-            kl[r] = ol;
-        }
+        const uint32_t o0 = xlane<LM>(k[0][r]), o1 = xlane<LM>(k[1][r]), o2 = xlane<LM>(k[2][r]), o3 = xlane<LM>(k[3][r]);
+        cx128(k[0][r], k[1][r], k[2][r], k[3][r], o0, o1, o2, o3, keep_min);
     }
 }
 
 // Bitonic sort of the job's 256*W slots (4 consecutive per lane, slot e = wj*256 + lane*4 + r)
-// over the first P (power of two) slots.
+// over the first P (power of two) slots.  Keys are unique (the slot is in the low bits).  The
+// network runs on dwords (no 64-bit register pairs to keep together); cross-wave stages exchange
+// whole keys through LDS as 16-byte words.
 template <int W>
 __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], int P, JobLds<W>& S, int wj)
 {
     const int      lane = lane_id();
     const uint32_t e0   = wj * 256 + lane * 4;
+    uint32_t       k[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        k[0][r] = (uint32_t) kl[r];
+        k[1][r] = (uint32_t) (kl[r] >> 32);
+        k[2][r] = (uint32_t) kh[r];
+        k[3][r] = (uint32_t) (kh[r] >> 32);
+    }
+    uint4* X = reinterpret_cast<uint4*>(S.kh);  // S.kh and S.kl back to back: 256*W 16-byte words
     for (int size = 2; size <= P; size <<= 1)
     {
         for (int j = size >> 1; j > 0; j >>= 1)
@@ -1136,57 +1136,50 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
                 job_sync<W>();
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                {
-                    S.kh[e0 + r] = kh[r];
-                    S.kl[e0 + r] = kl[r];
-                }
+                    X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], k[3][r]);
                 job_sync<W>();
-                const bool keep_min = ((e0 & size) == 0) == ((e0 & j) == 0);
+                const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & size) == 0) == ((e0 & j) == 0));
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                 {
-                    const uint64_t oh = S.kh[(e0 + r) ^ j], ol = S.kl[(e0 + r) ^ j];
-                    if (k2_gt(kh[r], kl[r], oh, ol) == keep_min)
-                    {
-                        kh[r] = oh;
-                        kl[r] = ol;
-                    }
+                    const uint4 o = X[(e0 + r) ^ j];
+                    cx128(k[0][r], k[1][r], k[2][r], k[3][r], o.x, o.y, o.z, o.w, keep_min);
                 }
             }
             else if (j >= 4)
             {
-                const bool keep_min = ((e0 & size) == 0) == ((e0 & j) == 0);
+                const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & size) == 0) == ((e0 & j) == 0));
                 switch (j >> 2)
                 {
-                case 1: net_stage_lanes<1>(kh, kl, keep_min); break;
-                case 2: net_stage_lanes<2>(kh, kl, keep_min); break;
-                case 4: net_stage_lanes<4>(kh, kl, keep_min); break;
-                case 8: net_stage_lanes<8>(kh, kl, keep_min); break;
-                case 16: net_stage_lanes<16>(kh, kl, keep_min); break;
-                default: net_stage_lanes<32>(kh, kl, keep_min); break;
+                case 1: net_stage_lanes<1>(k, keep_min); break;
+                case 2: net_stage_lanes<2>(k, keep_min); break;
+                case 4: net_stage_lanes<4>(k, keep_min); break;
+                case 8: net_stage_lanes<8>(k, keep_min); break;
+                case 16: net_stage_lanes<16>(k, keep_min); break;
+                default: net_stage_lanes<32>(k, keep_min); break;
                 }
             }
             else
             {
+                // partners in the same lane: r and r ^ j; ascending where (slot & size) == 0
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                 {
                     const int q = r ^ j;
                     if (q > r)
                     {
-                        const bool up = ((e0 + r) & size) == 0;
-                        if (k2_gt(kh[r], kl[r], kh[q], kl[q]) == up)
-                        {
-                            const uint64_t th = kh[r], tl = kl[r];
-                            kh[r]             = kh[q];
-                            kl[r]             = kl[q];
-                            kh[q]             = th;
-                            kl[q]             = tl;
-                        }
+                        const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & size) == 0);
+                        cx128_pair(k[0][r], k[1][r], k[2][r], k[3][r], k[0][q], k[1][q], k[2][q], k[3][q], asc);
                     }
                 }
             }
         }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        kl[r] = ((uint64_t) k[1][r] << 32) | k[0][r];
+        kh[r] = ((uint64_t) k[3][r] << 32) | k[2][r];
     }
     job_sync<W>();
 }
@@ -1334,9 +1327,14 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 uint32_t       st  = idx + ((depth - 1) % BD.len);
                 if (st >= BD.len)
                     st -= BD.len;
+#ifdef BRA_EXP_NOGATHER
+                const uint8_t lb = 0;  // measurement variant: no gathers (results are wrong)
+                uint64_t      w0 = 0, w1 = ((uint64_t) idx << 20) ^ st;
+#else
                 const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
                 uint64_t      w0, w1;
                 load_key16(blk, BD.len, st, w0, w1);
+#endif
                 make_key1<W>(c, w0, w1, kh[r], kl[r]);
                 v[r] = ((uint32_t) lb << 24) | idx;
             }
@@ -1351,6 +1349,9 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     int P = 4;
     while ((uint32_t) P < T)
         P <<= 1;
+#ifdef BRA_EXP_NOSORT
+    P = 1;  // measurement variant: no sort network (results are wrong)
+#endif
     PH_T(t_g1);
 #ifdef BRA_PHASES
     if (MODE == MODE_STRING)
@@ -1391,8 +1392,10 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 continue;
             const uint32_t slot = J.start + pos[r];
             const uint32_t idx  = v[r] & 0xFFFFFFu;
+#ifndef BRA_EXP_NOOUT
             a.fsa[slot]         = idx;
             a.L[slot]           = (uint8_t) (v[r] >> 24);
+#endif
             const uint32_t gst  = J.start + S.pos[g[r]] - boff;  // block-local start of the group
             if (MODE == MODE_RANK)
                 a.isa[BD.off + idx] = gst;
