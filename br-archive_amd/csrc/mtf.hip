@@ -37,8 +37,24 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
         __syncthreads();
         const Piece    P = segs[s];
         const uint8_t* p = in + P.off;
-        for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
-            atomicMax(&lo[p[i]], (int32_t) i);
+        if (P.len == MTF_SEG && (P.off & 7) == 0)
+        {
+            // 8 consecutive bytes per thread: only the last byte of each equal run inside them
+            // updates LDS (post-BWT input is run-heavy, and same-address LDS atomics serialise)
+            const uint2    q    = reinterpret_cast<const uint2*>(p)[threadIdx.x];
+            const uint64_t w    = ((uint64_t) q.y << 32) | q.x;
+            const int32_t  base = (int32_t) threadIdx.x * 8;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+            {
+                const uint32_t c = (uint32_t) (w >> (8 * i)) & 0xFF;
+                if (i == 7 || c != ((uint32_t) (w >> (8 * i + 8)) & 0xFF))
+                    atomicMax(&lo[c], base + i);
+            }
+        }
+        else
+            for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
+                atomicMax(&lo[p[i]], (int32_t) i);
         __syncthreads();
         state[(size_t) s * 256 + threadIdx.x] = lo[threadIdx.x] >= 0 ? (int32_t) P.start + lo[threadIdx.x] : -1;
         __syncthreads();
