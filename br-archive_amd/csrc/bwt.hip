@@ -120,7 +120,8 @@ struct TileDesc
     uint32_t buf;     // KV buffer holding the bucket
     uint32_t boff;    // block offset in the batch / block length
     uint32_t nlen;
-    uint32_t pad[2];
+    uint32_t kd;      // the payloads carry digits [kd, kd + CARRY)
+    uint32_t pad;
 };
 
 // Ordered tile list of a level: XCD x's part is [xseg[x], xseg[x + 1]) (workgroup w works on
@@ -142,6 +143,34 @@ __device__ __forceinline__ uint32_t tile_pos(const TileOrder& o, uint32_t i, uin
     const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, g = gridDim.x >> 3;
     const uint32_t p = o.xseg[x] + l + i * g;
     return p < o.xseg[x + 1] ? p : ~0u;
+}
+
+// STRING-mode payload (64 bits): the rotation index in bits 0-23 and CARRY digits, bytes
+// [kd, kd + CARRY) of the rotation, big-endian in bits 24-63.  A bucket at depth d reads digit
+// d - kd; the scatter that moves an element into a bucket at depth kd + CARRY gathers the next
+// CARRY bytes (one unaligned 8-byte load), so an element costs one gather per CARRY MSD levels.
+constexpr uint32_t CARRY = 5;
+__device__ __forceinline__ uint32_t p_idx(uint64_t P) { return (uint32_t) P & 0xFFFFFFu; }
+__device__ __forceinline__ uint32_t p_digit(uint64_t P, uint32_t j) { return (uint32_t) (P >> (56 - 8 * j)) & 0xFFu; }
+typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
+// payload carrying bytes [st, st + CARRY) (cyclic) of a block of n bytes
+__device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ blk, uint32_t n, uint32_t st, uint32_t idx)
+{
+    uint64_t k;
+    if (st + 8u <= n)
+        k = __builtin_bswap64(*reinterpret_cast<const u64_unaligned*>(blk + st));
+    else
+    {
+        k          = 0;
+        uint32_t q = st;
+        for (uint32_t i = 0; i < CARRY; ++i)
+        {
+            k = (k << 8) | blk[q];
+            q = (q + 1 == n) ? 0 : q + 1;
+        }
+        k <<= 64 - 8 * CARRY;
+    }
+    return (k & 0xFFFFFFFFFF000000ull) | idx;
 }
 
 // Start of an MSD level.
@@ -206,8 +235,8 @@ __device__ __forceinline__ uint32_t key_digit(uint64_t key, uint32_t d, uint32_t
     return (uint32_t) (key >> (56 - 8 * (d - kd))) & 0xFFu;
 }
 
-// STRING mode: the element's payload carries the digit (byte B.d of its rotation) in its top byte,
-// written by the scatter that put it into this bucket; nothing else is read.  RANK mode: the digit
+// STRING mode: the element's payload carries the digit (byte B.d of its rotation, see p_digit);
+// nothing else is read.  RANK mode: the digit
 // comes from the 32-bit rank key.
 template <uint32_t MODE>
 __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
@@ -227,18 +256,19 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
         if (MODE == MODE_STRING)
         {
             const TileDesc  D   = to.desc[p];
-            const uint32_t* pay = (D.buf ? pay1 : pay0) + D.s0;
+            const uint64_t* pay = (D.buf ? key1 : key0) + D.s0;  // STRING payloads live in the key buffers
+            const uint32_t  j   = D.d - D.kd;
             uint32_t        v[PER_THREAD];
 #pragma unroll
             for (int i = 0; i < PER_THREAD; ++i)
             {
                 const uint32_t e = threadIdx.x + i * TPB;
-                v[i]             = e < D.cnt ? pay[e] : 0u;
+                v[i]             = e < D.cnt ? p_digit(pay[e], j) : 0u;
             }
 #pragma unroll
             for (int i = 0; i < PER_THREAD; ++i)
                 if (threadIdx.x + i * TPB < D.cnt)
-                    atomicAdd(&h[v[i] >> 24], 1u);
+                    atomicAdd(&h[v[i]], 1u);
             t = D.t;
         }
         else
@@ -355,8 +385,8 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         uint32_t base[4];
         wave_excl_sum4(tot, base);
         {
-            // bit 31 (STRING mode): the sub-bucket is a next-level bucket, so the scatter loads the
-            // next digit of its elements (slots are < 2^31)
+            // bit 31 (STRING mode): the sub-bucket is a next-level bucket (the scatter re-gathers its
+            // payload digits when the carried ones run out; slots are < 2^31)
             uint32_t flag[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -377,17 +407,19 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
             }
         }
         const bool     nomove = active && __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
-        // STRING mode: a bucket that does not move but continues as a next-level bucket still needs
-        // its elements' next digit (nomove code 2: the scatter updates the payloads in place)
+        // STRING mode: the next bucket's payloads carry digits [kd, kd + CARRY); a bucket that does
+        // not move but continues needs its payloads re-gathered in place when they run out (nomove
+        // code 2), otherwise it is left alone (code 1)
+        const bool     regather = (MODE == MODE_STRING) && (B.buf == 2u || B.d + 1 - B.kd >= CARRY);
+        const uint32_t kd       = (MODE == MODE_STRING) ? (B.buf == 2u ? 1u : (regather ? B.d + 1 : B.kd)) : eff_kd(B, MODE);
         bool nm_next = false;
-        if (MODE == MODE_STRING && nomove)
+        if (MODE == MODE_STRING && nomove && regather)
         {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 nm_next |= (tot[r] == B.len) && tot[r] > a.mjob_max && B.d + 1 < a.dcap;
             nm_next = __any(nm_next);
         }
-        const uint32_t kd     = eff_kd(B, MODE);
         const uint32_t nd     = B.d + 1;
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
         if (active && lane == 0)
@@ -605,10 +637,10 @@ struct TileStage
     uint32_t tmp[8];
 };
 
-// STRING-mode tile staging: payloads only (the digit is in the payload's top byte).
+// STRING-mode tile staging: 64-bit payloads (index + carried digits).
 struct TileStageP
 {
-    uint32_t pay[TILE];
+    uint64_t pay[TILE];
     uint32_t cnt[256];
     uint32_t base[256];
     uint32_t goff[256];  // sub-bucket slot of the tile's first element per digit (bit 31: next-level bucket)
@@ -618,7 +650,8 @@ constexpr uint32_t NEXT_FLAG = 0x80000000u;
 
 // Ranks the tile's elements by digit in LDS and stages them in digit order; returns nothing, the
 // caller reads S.pay[q] back in order (coalesced output runs per digit).
-__device__ __forceinline__ void stage_p(TileStageP& S, const uint32_t (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
+template <typename V>
+__device__ __forceinline__ void stage_p(TileStageP& S, const V (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
 {
     uint32_t rank[PER_THREAD];
 #pragma unroll
@@ -690,10 +723,10 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
     }
 }
 
-// Level 0: every element gets payload (byte 1 << 24 | index): its next digit.
+// Level 0: every element gets its payload carrying rotation bytes 1..CARRY (the next digits).
 __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
                                                     const L0Tile* __restrict__ tiles, uint32_t ntiles,
-                                                    const uint32_t* __restrict__ tile_off, uint32_t* __restrict__ opay)
+                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageP& S   = *reinterpret_cast<TileStageP*>(smem);
@@ -740,25 +773,31 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
             const uint32_t q = threadIdx.x + i * TPB;
             if (q < cnt)
             {
-                const uint32_t vv   = S.pay[q];
+                const uint32_t vv   = (uint32_t) S.pay[q];
                 const uint32_t dd   = vv >> 24, e = vv & 0xFFFFFFu;
                 const uint32_t slot = S.goff[dd] + (q - S.base[dd]);
+                // window bytes [e + 16, e + 24) = rotation bytes 0..7: keep bytes 1..CARRY
+                const uint32_t  o  = e + 16;
+                const uint32_t* w4 = reinterpret_cast<const uint32_t*>(win) + (o >> 2);
+                const uint32_t  a0 = w4[0], a1 = w4[1], a2 = w4[2], sh = o & 3;
+                const uint32_t  lo = __builtin_amdgcn_alignbyte(a1, a0, sh), hi = __builtin_amdgcn_alignbyte(a2, a1, sh);
+                const uint64_t  kk = __builtin_bswap64(((uint64_t) hi << 32) | lo);
                 if (BRA_DCHECK(slot >= B.off && slot < B.off + B.len, "l0 scatter slot %u outside block %u", slot, T.block))
-                    opay[slot] = ((uint32_t) win[e + 17] << 24) | (T.start + e);
+                    opay[slot] = ((kk << 8) & 0xFFFFFFFFFF000000ull) | (T.start + e);
             }
         }
         __syncthreads();
     }
 }
 
-// STRING-mode MSD scatter: payloads only.  An element whose sub-bucket continues as a next-level
-// bucket (tile_off bit 31) gets its next digit, byte d + 1 of its rotation, gathered from the
-// input (the block is in the XCD's L2 or the Infinity Cache); others keep their payload (jobs only
-// use the index).  nomove 1: the bucket stays as it is; 2: it stays in place but continues, so
-// only the digits are updated.
+// STRING-mode MSD scatter of 64-bit payloads.  An element whose sub-bucket continues as a
+// next-level bucket (tile_off bit 31) at depth kd + CARRY gets the next CARRY digits gathered from
+// the input (the block is in the XCD's L2); all others keep their payload (jobs only use the
+// index).  nomove 1: the bucket stays as it is; 2: it stays in place but continues and its
+// payloads are re-gathered in place.
 __global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
-                                                   const uint32_t* __restrict__ tile_off, uint32_t* __restrict__ pay0,
-                                                   uint32_t* __restrict__ pay1, uint32_t ntiles, TileOrder to)
+                                                   const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ pay0,
+                                                   uint64_t* __restrict__ pay1, uint32_t ntiles, TileOrder to)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageP& S = *reinterpret_cast<TileStageP*>(smem);
@@ -782,12 +821,14 @@ __global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ i
         {
             uint32_t start, len, d, buf;
         } B{D.bstart, D.blen, D.d, D.buf};
-        const uint32_t  dn = (B.d + 1) % BD.len;  // next digit's depth
+        const uint32_t  j  = B.d - D.kd;              // this level's digit in the payload
+        const bool      rg = j + 1 >= CARRY;          // next-level buckets start a new carry
+        const uint32_t  dn = (B.d + 1) % BD.len;      // their first digit's depth
         const size_t    s0 = D.s0;
-        uint32_t*       ip = (B.buf ? pay1 : pay0) + s0;
+        uint64_t*       ip = (B.buf ? pay1 : pay0) + s0;
         if (nm == 2)
         {
-            uint32_t v[PER_THREAD];
+            uint64_t v[PER_THREAD];
 #pragma unroll
             for (int i = 0; i < PER_THREAD; ++i)
             {
@@ -801,29 +842,31 @@ __global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ i
                 const uint32_t e = threadIdx.x + i * TPB;
                 if (e < cnt)
                 {
-                    const uint32_t idx = v[i] & 0xFFFFFFu;
+                    const uint32_t idx = p_idx(v[i]);
                     uint32_t       st  = idx + dn;
                     if (st >= BD.len)
                         st -= BD.len;
-                    ip[e] = ((uint32_t) blk[st] << 24) | idx;
+                    ip[e] = p_make(blk, BD.len, st, idx);
                 }
             }
             continue;
         }
-        uint32_t* op        = B.buf ? pay0 : pay1;
+        uint64_t* op        = B.buf ? pay0 : pay1;
         S.cnt[threadIdx.x]  = 0;
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x];
         __syncthreads();
-        uint32_t v[PER_THREAD], dg[PER_THREAD];
+        uint64_t v[PER_THREAD];
+        uint32_t dg[PER_THREAD];
 #pragma unroll
         for (int i = 0; i < PER_THREAD; ++i)
         {
             const uint32_t e = threadIdx.x + i * TPB;
-            v[i]             = (e < cnt) ? ip[e] : 0u;
-            dg[i]            = v[i] >> 24;
+            v[i]             = (e < cnt) ? ip[e] : 0ull;
+            dg[i]            = p_digit(v[i], j);
         }
         stage_p(S, v, dg, cnt);
-        uint32_t slot[PER_THREAD], nv[PER_THREAD];
+        uint32_t slot[PER_THREAD];
+        uint64_t nv[PER_THREAD];
 #pragma unroll
         for (int i = 0; i < PER_THREAD; ++i)
         {
@@ -831,17 +874,17 @@ __global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ i
             slot[i]          = 0xFFFFFFFFu;
             if (q < cnt)
             {
-                const uint32_t vv = S.pay[q];
-                const uint32_t dd = vv >> 24, g = S.goff[dd];
+                const uint64_t vv = S.pay[q];
+                const uint32_t dd = p_digit(vv, j), g = S.goff[dd];
                 slot[i]           = (g & ~NEXT_FLAG) + (q - S.base[dd]);
                 nv[i]             = vv;
-                if (g & NEXT_FLAG)
+                if (rg && (g & NEXT_FLAG))
                 {
-                    const uint32_t idx = vv & 0xFFFFFFu;
+                    const uint32_t idx = p_idx(vv);
                     uint32_t       st  = idx + dn;
                     if (st >= BD.len)
                         st -= BD.len;
-                    nv[i] = ((uint32_t) blk[st] << 24) | idx;
+                    nv[i] = p_make(blk, BD.len, st, idx);
                 }
             }
         }
@@ -1310,7 +1353,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         kh[r] = kl[r] = ~0ull;
         if (c < T)
         {
-            v[r] = V[J.start + c];
+            // STRING payloads are the 64-bit MSD payloads in the key buffers (index in the low bits)
+            v[r] = (MODE == MODE_RANK) ? V[J.start + c] : (uint32_t) K[J.start + c] & 0xFFFFFFu;
             if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (mode %u buf %u slot %u)", v[r] & 0xFFFFFFu, BD.len, MODE, J.buf,
                             J.start + c))
                 v[r] = 0;
@@ -1675,7 +1719,7 @@ __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__
                 const BlockDesc BD = blocks[B.block];
                 const uint32_t  f  = (j - B.tile0) * TILE;
                 order[h[key[i]] + rank[i]] =
-                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, (uint32_t) BD.off, BD.len, {0, 0}};
+                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, (uint32_t) BD.off, BD.len, B.kd, 0};
             }
         }
         __syncthreads();
@@ -1686,17 +1730,17 @@ __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__
 // fallback (prefix doubling on ranks) helpers
 // -------------------------------------------------------------------------------------------------
 // Copy the members of fallback groups that still live in a KV buffer into fsa.
-__global__ void k_group_flush(const Group* __restrict__ groups, uint32_t ng, const uint32_t* __restrict__ pay0,
-                              const uint32_t* __restrict__ pay1, uint32_t* __restrict__ fsa)
+__global__ void k_group_flush(const Group* __restrict__ groups, uint32_t ng, const uint64_t* __restrict__ pay0,
+                              const uint64_t* __restrict__ pay1, uint32_t* __restrict__ fsa)
 {
     for (uint32_t gi = blockIdx.x; gi < ng; gi += gridDim.x)
     {
         const Group G = groups[gi];
         if (G.block & (1u << 30))
             continue;
-        const uint32_t* p = (G.block >> 31) ? pay1 : pay0;
+        const uint64_t* p = (G.block >> 31) ? pay1 : pay0;
         for (uint32_t i = threadIdx.x; i < G.len; i += blockDim.x)
-            fsa[G.start + i] = p[G.start + i] & 0xFFFFFFu;
+            fsa[G.start + i] = (uint32_t) p[G.start + i] & 0xFFFFFFu;
     }
 }
 
@@ -2132,7 +2176,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         {
             BRA_PROF(P_BWT_SCATTER, s);
             if (MODE == MODE_STRING)
-                hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageP), s, d_in, w.nomove, w.tile_off, w.pay[0], w.pay[1],
+                hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageP), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
                                    ntiles, to);
             else
                 hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
@@ -2146,7 +2190,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         const double nt = ntiles, ne = nelems, nm = w.h_ctr->n_moved;
         nelems          = w.h_ctr->n_elems_next;
         // STRING: 4-byte payloads (+ the next digit gathered for elements that stay in big buckets)
-        const double eb = (MODE == MODE_STRING) ? 4.0 : 8.0, mb = (MODE == MODE_STRING) ? 9.0 : 24.0;
+        const double eb = 8.0, mb = (MODE == MODE_STRING) ? 16.0 + 8.0 / CARRY : 24.0;
         prof_bytes(P_BWT_HIST, eb * ne + 1024.0 * nt);
         prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * nbig);
         prof_bytes(P_BWT_SCATTER, mb * nm + 1024.0 * nt);
@@ -2241,14 +2285,14 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
         hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageP) + TILE + 48, s, d_in, d_blocks,
-                           w.l0tiles, nt0, w.tile_off, w.pay[0]); BRA_DSYNC(s);
+                           w.l0tiles, nt0, w.tile_off, w.key[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
         return false;
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
-    prof_bytes(P_BWT_L0SCATTER, 5.0 * N + 1024.0 * nt0);  // window in, payload out
+    prof_bytes(P_BWT_L0SCATTER, 9.0 * N + 1024.0 * nt0);  // window in, payload out
     // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]
     if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, w.h_ctr->n_tiles_next, 0, w.groups[0], s))
         return false;
@@ -2305,7 +2349,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return true;
     BRA_PROF(P_BWT_FALLBACK, s);
     int gcur = 0;
-    hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pay[0], w.pay[1], w.fsa); BRA_DSYNC(s);
+    hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.key[0], w.key[1], w.fsa); BRA_DSYNC(s);
     // mark blocks, build ranks: singletons rank = own slot, group members = group start
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
                        w.flag); BRA_DSYNC(s);  // sets the flags (its rank writes are redone below)
