@@ -1151,6 +1151,60 @@ __device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[4][4], uint64_t ke
     }
 }
 
+// Stage (SIZE, J) of the bitonic network and, recursively, the rest of its merge phase.  All
+// stage parameters are compile-time, so a phase is straight-line code with the keys in fixed
+// registers (a runtime stage loop made the compiler copy every key between register sets at each
+// stage join).
+template <int W, int SIZE, int J>
+__device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uint32_t e0)
+{
+    if constexpr (J >= 256)
+    {
+        static_assert(W > 1, "cross-wave stage");
+        uint4* X = reinterpret_cast<uint4*>(S.kh);  // S.kh and S.kl back to back: 256*W 16-byte words
+        job_sync<W>();
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], k[3][r]);
+        job_sync<W>();
+        const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint4 o = X[(e0 + r) ^ J];
+            cx128(k[0][r], k[1][r], k[2][r], k[3][r], o.x, o.y, o.z, o.w, keep_min);
+        }
+    }
+    else if constexpr (J >= 4)
+    {
+        const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
+        net_stage_lanes<J / 4>(k, keep_min);
+    }
+    else
+    {
+        // partners in the same lane: r and r ^ J; ascending where (slot & SIZE) == 0
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const int q = r ^ J;
+            if (q > r)
+            {
+                const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & SIZE) == 0);
+                cx128_pair(k[0][r], k[1][r], k[2][r], k[3][r], k[0][q], k[1][q], k[2][q], k[3][q], asc);
+            }
+        }
+    }
+    if constexpr (J > 1)
+        net_stage<W, SIZE, J / 2>(k, S, e0);
+}
+
+template <int W, int SIZE>
+__device__ __forceinline__ void net_phase(uint32_t (&k)[4][4], JobLds<W>& S, uint32_t e0)
+{
+    if constexpr (SIZE <= 256 * W)
+        net_stage<W, SIZE, SIZE / 2>(k, S, e0);
+}
+
 // Bitonic sort of the job's 256*W slots (4 consecutive per lane, slot e = wj*256 + lane*4 + r)
 // over the first P (power of two) slots.  Keys are unique (the slot is in the low bits).  The
 // network runs on dwords (no 64-bit register pairs to keep together); cross-wave stages exchange
@@ -1169,53 +1223,22 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
         k[2][r] = (uint32_t) kh[r];
         k[3][r] = (uint32_t) (kh[r] >> 32);
     }
-    uint4* X = reinterpret_cast<uint4*>(S.kh);  // S.kh and S.kl back to back: 256*W 16-byte words
     for (int size = 2; size <= P; size <<= 1)
     {
-        for (int j = size >> 1; j > 0; j >>= 1)
+        switch (size)
         {
-            if (W > 1 && j >= 256)
-            {
-                job_sync<W>();
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], k[3][r]);
-                job_sync<W>();
-                const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & size) == 0) == ((e0 & j) == 0));
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const uint4 o = X[(e0 + r) ^ j];
-                    cx128(k[0][r], k[1][r], k[2][r], k[3][r], o.x, o.y, o.z, o.w, keep_min);
-                }
-            }
-            else if (j >= 4)
-            {
-                const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & size) == 0) == ((e0 & j) == 0));
-                switch (j >> 2)
-                {
-                case 1: net_stage_lanes<1>(k, keep_min); break;
-                case 2: net_stage_lanes<2>(k, keep_min); break;
-                case 4: net_stage_lanes<4>(k, keep_min); break;
-                case 8: net_stage_lanes<8>(k, keep_min); break;
-                case 16: net_stage_lanes<16>(k, keep_min); break;
-                default: net_stage_lanes<32>(k, keep_min); break;
-                }
-            }
-            else
-            {
-                // partners in the same lane: r and r ^ j; ascending where (slot & size) == 0
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const int q = r ^ j;
-                    if (q > r)
-                    {
-                        const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & size) == 0);
-                        cx128_pair(k[0][r], k[1][r], k[2][r], k[3][r], k[0][q], k[1][q], k[2][q], k[3][q], asc);
-                    }
-                }
-            }
+        case 2: net_phase<W, 2>(k, S, e0); break;
+        case 4: net_phase<W, 4>(k, S, e0); break;
+        case 8: net_phase<W, 8>(k, S, e0); break;
+        case 16: net_phase<W, 16>(k, S, e0); break;
+        case 32: net_phase<W, 32>(k, S, e0); break;
+        case 64: net_phase<W, 64>(k, S, e0); break;
+        case 128: net_phase<W, 128>(k, S, e0); break;
+        case 256: net_phase<W, 256>(k, S, e0); break;
+        case 512: net_phase<W, 512>(k, S, e0); break;
+        case 1024: net_phase<W, 1024>(k, S, e0); break;
+        case 2048: net_phase<W, 2048>(k, S, e0); break;
+        default: net_phase<W, 4096>(k, S, e0); break;
         }
     }
 #pragma unroll
