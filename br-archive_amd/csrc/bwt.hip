@@ -975,7 +975,50 @@ struct JobArgs
     uint32_t         hstep;    // RANK mode: depth added to a subgroup (min depth of the round)
     uint32_t         xcd_major;  // jobs ordered by job_order(): XCD x works on jobs [xseg[x], xseg[x+1])
     uint32_t         xseg[9];
+    uint32_t*        jq;       // dynamic order (xcd_major only): per-XCD claim counters, 32 dwords apart; null = static ranges
+    uint32_t         jq_chunk; // jobs a wave claims at once
 };
+
+// Hardware id (0-7) of the XCD the calling wave runs on.  Speed only: the job queues below stay
+// correct whatever it returns, since every wave drains all eight queues before it exits.
+__device__ __forceinline__ uint32_t xcc_id()
+{
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x & 7u;
+}
+
+// Dynamic job order: the waves of XCD x claim chunks of XCD x's part of the block-major list with
+// an atomic counter, so all waves of an XCD work on the same one or two blocks at any time (the
+// static stride let late-starting workgroups begin at the head of the list while early ones were
+// at its tail, spreading an XCD's gathers over all its blocks).  A wave whose own part is
+// exhausted helps the other XCDs' parts, so the launch drains every job whatever the placement.
+// Returns the first job of the claimed chunk and its end, or false when all parts are drained.
+struct JobClaim
+{
+    uint32_t x0, t;
+};
+
+// Called by a whole wave (wave-uniform control flow; lane 0 performs the atomic).
+__device__ __forceinline__ bool job_claim(const JobArgs& a, JobClaim& c, uint32_t chunk, uint32_t& first, uint32_t& end)
+{
+    while (c.t < 8)
+    {
+        const uint32_t x = (c.x0 + c.t) & 7u, lo = a.xseg[x], hi = a.xseg[x + 1];
+        uint32_t       b = 0;
+        if (lane_id() == 0)
+            b = atomicAdd(&a.jq[x * 32], chunk);
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (b < hi - lo)
+        {
+            first = lo + b;
+            end   = min(hi, first + chunk);
+            return true;
+        }
+        ++c.t;
+    }
+    return false;
+}
 
 // Job index ranges per workgroup.  With xcd_major, workgroup w runs on XCD w % 8 (the dispatcher's
 // round-robin; only speed depends on it) and walks that XCD's list, where the jobs of the blocks
@@ -1555,22 +1598,62 @@ template <uint32_t MODE>
 __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
 {
     __shared__ JobLds<1> lds[4];
-    const int      wl = threadIdx.x >> 6;
-    const JobRange R  = job_range(a, wl, 4);
-    for (uint32_t j = R.first; j < R.end; j += R.step)
+    const int      wl  = threadIdx.x >> 6;
+    const bool     dyn = a.xcd_major && a.jq;
+    const JobRange R   = job_range(a, wl, 4);
+    JobClaim       c{xcc_id(), 0};
+    uint32_t       end = 0;
+    // one call site of job_run, in a plain while loop (other loop shapes raised the register
+    // allocation of the inlined job by up to 2x)
+    const auto next = [&](uint32_t j) -> uint32_t {
+        if (!dyn)
+            return j + R.step < R.end ? j + R.step : ~0u;
+        if (j + 1 < end)
+            return j + 1;
+        uint32_t first = 0;
+        return job_claim(a, c, a.jq_chunk, first, end) ? first : ~0u;
+    };
+    uint32_t j = dyn ? next(~0u) : (R.first < R.end ? R.first : ~0u);
+    while (j != ~0u)
+    {
         job_run<MODE, 1>(a, a.jobs[j], lds[wl], 0);
+        j = next(j);
+    }
 }
 
 template <uint32_t MODE, int W>
 __global__ void __launch_bounds__(64 * W, JOB_MIN_WAVES) k_mjobs(JobArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    JobLds<W>&     S = *reinterpret_cast<JobLds<W>*>(smem);
-    const JobRange R = job_range(a, 0, 1);
-    for (uint32_t j = R.first; j < R.end; j += R.step)
+    JobLds<W>&     S   = *reinterpret_cast<JobLds<W>*>(smem);
+    uint32_t*      claim = reinterpret_cast<uint32_t*>(smem + sizeof(JobLds<W>));  // 2 own LDS words (launch adds 16 bytes)
+    const bool     dyn   = a.xcd_major && a.jq;
+    const JobRange R     = job_range(a, 0, 1);
+    JobClaim       c{xcc_id(), 0};
+    uint32_t       k = 0;
+    // Dynamic order: wave 0 claims the next job into claim[k & 1] and one barrier publishes it (the
+    // two slots alternate, so a slot is rewritten only after every wave passed the next barrier).
+    const auto next = [&](uint32_t j) -> uint32_t {
+        if (!dyn)
+        {
+            __syncthreads();  // the LDS of the finished job is reused
+            return j + R.step < R.end ? j + R.step : ~0u;
+        }
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) == 0)  // wave 0
+        {
+            uint32_t first = 0, end = 0;
+            const bool ok = job_claim(a, c, 1, first, end);
+            if (lane_id() == 0)
+                claim[k & 1] = ok ? first : ~0u;
+        }
+        __syncthreads();
+        return __builtin_amdgcn_readfirstlane(claim[(k++) & 1]);
+    };
+    uint32_t j = dyn ? next(0) : (R.first < R.end ? R.first : ~0u);
+    while (j != ~0u)
     {
         job_run<MODE, W>(a, a.jobs[j], S, threadIdx.x >> 6);
-        __syncthreads();
+        j = next(j);
     }
 }
 
@@ -1947,6 +2030,9 @@ struct BwtWorkspace
     int       grid = 2048;
     int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
     uint32_t  jobs_grid = 8192;         // workgroups of the wave-job launch (env BRA_JOBS_GRID)
+    uint32_t* jobq      = nullptr;      // per-XCD claim counters of the three job launches (3 x 8 x 32 dwords)
+    int       jobq_on   = 1;            // dynamic job order (env BRA_JOBQ=0: static strides)
+    uint32_t  jobq_chunk = 2;           // wave jobs claimed at once (env BRA_JOBQ_CH)
     uint32_t  nblocks   = 0;            // blocks of the current call
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -2025,13 +2111,13 @@ static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
 {
     const dim3 g(round8(std::min<uint32_t>(n, g_mjobs_grid)));
     if (waves == 16)
-        hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>), s, a);
+        hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>) + 16, s, a);
     else if (waves == 8)
-        hipLaunchKernelGGL((k_mjobs<MODE, 8>), g, dim3(64 * 8), sizeof(JobLds<8>), s, a);
+        hipLaunchKernelGGL((k_mjobs<MODE, 8>), g, dim3(64 * 8), sizeof(JobLds<8>) + 16, s, a);
     else if (waves == 4)
-        hipLaunchKernelGGL((k_mjobs<MODE, 4>), g, dim3(64 * 4), sizeof(JobLds<4>), s, a);
+        hipLaunchKernelGGL((k_mjobs<MODE, 4>), g, dim3(64 * 4), sizeof(JobLds<4>) + 16, s, a);
     else
-        hipLaunchKernelGGL((k_mjobs<MODE, 2>), g, dim3(64 * 2), sizeof(JobLds<2>), s, a);
+        hipLaunchKernelGGL((k_mjobs<MODE, 2>), g, dim3(64 * 2), sizeof(JobLds<2>) + 16, s, a);
 #ifdef BRA_DEBUG
     if (hipStreamSynchronize(s) != hipSuccess)
         fprintf(stderr, "[bra dsync] k_mjobs mode %u waves %d n %u xcd_major %u failed\n", MODE, waves, n, a.xcd_major);
@@ -2063,6 +2149,7 @@ static void ws_free(BwtWorkspace& w)
     (void) hipHostFree(w.h_job_cnt);
     (void) hipFree(w.mjobs);
     (void) hipFree(w.ctr);
+    (void) hipFree(w.jobq);
     (void) hipFree(w.l0tiles);
     if (w.h_ctr)
         (void) hipHostFree(w.h_ctr);
@@ -2079,7 +2166,8 @@ void          bwt_workspace_destroy(BwtWorkspace* w)
     }
 }
 
-static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
+// Tuning knobs from the environment (ws_free resets the workspace, so they are applied after it).
+static void ws_env(BwtWorkspace& w)
 {
     if (const char* e = getenv("BRA_MJ_WAVES"))  // tuning knob: 0 (off), 2, 4, 8 or 16 waves per workgroup job
     {
@@ -2090,9 +2178,19 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
         w.jobs_grid = std::max(8, atoi(e));
     if (const char* e = getenv("BRA_MJOBS_GRID"))
         g_mjobs_grid = std::max(8, atoi(e));
+    if (const char* e = getenv("BRA_JOBQ"))
+        w.jobq_on = atoi(e) != 0;
+    if (const char* e = getenv("BRA_JOBQ_CH"))
+        w.jobq_chunk = (uint32_t) std::max(1, atoi(e));
+}
+
+static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
+{
+    ws_env(w);
     if (n <= w.cap_n && nblocks <= w.cap_blocks)
         return true;
     ws_free(w);
+    ws_env(w);
     const uint64_t N = std::max<uint64_t>(n, 1 << 16);
     const uint32_t B = std::max<uint32_t>(nblocks, 64);
     w.cap_n      = N;
@@ -2128,6 +2226,7 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     BRA_HIP_CHECK(hipMalloc(&w.tile_order, (size_t) w.cap_tiles * sizeof(TileDesc)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
+    BRA_HIP_CHECK(hipMalloc(&w.jobq, 3 * 8 * 32 * 4));
     BRA_HIP_CHECK(hipMalloc(&w.l0tiles, (size_t) w.cap_l0 * sizeof(L0Tile)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault));
     return true;
@@ -2271,10 +2370,10 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageP) + TILE + 48)));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>)));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>)));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
         attr_set = true;
     }
     const int grid = w.grid;
@@ -2331,6 +2430,15 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     JobArgs ord[3];
     if (!order_jobs(w, nblocks, ja, jm, ord, s))
         return false;
+    if (w.jobq_on)
+    {
+        BRA_HIP_CHECK(hipMemsetAsync(w.jobq, 0, 3 * 8 * 32 * 4, s));
+        for (int k = 0; k < 3; ++k)
+        {
+            ord[k].jq       = w.jobq + k * 8 * 32;
+            ord[k].jq_chunk = w.jobq_chunk;
+        }
+    }
     if (njobs)
     {
         BRA_PROF(P_BWT_JOBS, s);
