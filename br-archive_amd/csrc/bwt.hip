@@ -61,6 +61,9 @@ constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket go
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
 #ifndef JOB_MIN_WAVES
+#ifndef BRA_HIST_PIPE
+#define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
+#endif
 #define JOB_MIN_WAVES 1                  // min waves per SIMD the job kernels are compiled for (1 = compiler choice; 6 and 8 measured slower)
 #endif
 
@@ -245,6 +248,53 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
                                               uint32_t* __restrict__ tile_hist, uint32_t ntiles, TileOrder to)
 {
     __shared__ uint32_t h[256];
+    if (MODE == MODE_STRING && BRA_HIST_PIPE)
+    {
+        // software-pipelined over the workgroup's tiles: the next tile's descriptor and payloads
+        // are loaded before the current tile's LDS histogram is built
+        // Only the payload dword holding the digit is loaded (p_digit: digits 0-3 in the high
+        // dword, digit 4 in bits 24-31 of the low one).
+        uint32_t p = tile_pos(to, 0, ntiles);
+        TileDesc D{};
+        uint32_t w[PER_THREAD];
+        const auto load = [&](uint32_t pp, TileDesc& DD, uint32_t (&ww)[PER_THREAD]) {
+            if (pp == ~0u)
+                return;
+            DD                  = to.desc[pp];
+            const uint32_t  jj  = DD.d - DD.kd;
+            const uint32_t* pay = reinterpret_cast<const uint32_t*>((DD.buf ? key1 : key0) + DD.s0) + (jj < 4 ? 1 : 0);
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+            {
+                const uint32_t e = threadIdx.x + i * TPB;
+                ww[i]            = e < DD.cnt ? pay[2 * e] : 0u;
+            }
+        };
+        load(p, D, w);
+        for (uint32_t it = 1; p != ~0u; ++it)
+        {
+            const uint32_t pn = tile_pos(to, it, ntiles);
+            TileDesc       Dn{};
+            uint32_t       wn[PER_THREAD];
+            load(pn, Dn, wn);
+            h[threadIdx.x] = 0;
+            __syncthreads();
+            const uint32_t j  = D.d - D.kd;
+            const uint32_t sh = j < 4 ? 24 - 8 * j : 24;
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+                if (threadIdx.x + i * TPB < D.cnt)
+                    atomicAdd(&h[(w[i] >> sh) & 0xFFu], 1u);
+            __syncthreads();
+            tile_hist[(size_t) D.t * 256 + threadIdx.x] = h[threadIdx.x];
+            p = pn;
+            D = Dn;
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+                w[i] = wn[i];
+        }
+        return;
+    }
     for (uint32_t it = 0;; ++it)
     {
         const uint32_t p = tile_pos(to, it, ntiles);
@@ -256,7 +306,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
         if (MODE == MODE_STRING)
         {
             const TileDesc  D   = to.desc[p];
-            const uint64_t* pay = (D.buf ? key1 : key0) + D.s0;  // STRING payloads live in the key buffers
+            const uint64_t* pay = (D.buf ? key1 : key0) + D.s0;
             const uint32_t  j   = D.d - D.kd;
             uint32_t        v[PER_THREAD];
 #pragma unroll
@@ -273,11 +323,11 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
         }
         else
         {
-            t                    = p;
-            const Bucket   B     = buckets[tile_bucket[t]];
-            const uint32_t first = (t - B.tile0) * TILE;
-            const uint32_t cnt   = min((uint32_t) TILE, B.len - first);
-            const uint64_t* key  = (B.buf ? key1 : key0) + (size_t) B.start + first;
+            t                     = p;
+            const Bucket    B     = buckets[tile_bucket[t]];
+            const uint32_t  first = (t - B.tile0) * TILE;
+            const uint32_t  cnt   = min((uint32_t) TILE, B.len - first);
+            const uint64_t* key   = (B.buf ? key1 : key0) + (size_t) B.start + first;
             for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
                 atomicAdd(&h[key_digit(key[i], B.d, B.kd)], 1u);
         }
@@ -795,7 +845,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
 // the input (the block is in the XCD's L2); all others keep their payload (jobs only use the
 // index).  nomove 1: the bucket stays as it is; 2: it stays in place but continues and its
 // payloads are re-gathered in place.
-__global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
+__global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ pay0,
                                                    uint64_t* __restrict__ pay1, uint32_t ntiles, TileOrder to)
 {
@@ -865,33 +915,30 @@ __global__ void __launch_bounds__(TPB) k_scatter_p(const uint8_t* __restrict__ i
             dg[i]            = p_digit(v[i], j);
         }
         stage_p(S, v, dg, cnt);
-        uint32_t slot[PER_THREAD];
-        uint64_t nv[PER_THREAD];
+        // slot and (re-gathered) payload of each staged element, stored at once (keeping all 16
+        // in registers until a separate store loop cost 2x the VGPRs: 2 waves per SIMD)
 #pragma unroll
         for (int i = 0; i < PER_THREAD; ++i)
         {
             const uint32_t q = threadIdx.x + i * TPB;
-            slot[i]          = 0xFFFFFFFFu;
             if (q < cnt)
             {
-                const uint64_t vv = S.pay[q];
-                const uint32_t dd = p_digit(vv, j), g = S.goff[dd];
-                slot[i]           = (g & ~NEXT_FLAG) + (q - S.base[dd]);
-                nv[i]             = vv;
+                const uint64_t vv   = S.pay[q];
+                const uint32_t dd   = p_digit(vv, j), g = S.goff[dd];
+                const uint32_t slot = (g & ~NEXT_FLAG) + (q - S.base[dd]);
+                uint64_t       nv   = vv;
                 if (rg && (g & NEXT_FLAG))
                 {
                     const uint32_t idx = p_idx(vv);
                     uint32_t       st  = idx + dn;
                     if (st >= BD.len)
                         st -= BD.len;
-                    nv[i] = p_make(blk, BD.len, st, idx);
+                    nv = p_make(blk, BD.len, st, idx);
                 }
+                if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
+                    op[slot] = nv;
             }
         }
-#pragma unroll
-        for (int i = 0; i < PER_THREAD; ++i)
-            if (slot[i] != 0xFFFFFFFFu && BRA_DCHECK(slot[i] >= B.start && slot[i] < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot[i], B.start, B.len))
-                op[slot[i]] = nv[i];
         __syncthreads();
     }
 }
