@@ -130,6 +130,46 @@ __device__ __forceinline__ uint32_t shift_upto(uint32_t cur, uint32_t below_top,
     return (cur & keep) | (((cur << 8) | below_top) & ~keep);
 }
 
+// One 16-entry LDS chunk d of the table during a search for c (cc = c in every byte): if c is in
+// it, shift the entries below it up by one (the entry `top` enters at 0), store, set r to c's
+// position in the chunk and return true; otherwise shift the whole chunk, store, and carry its top
+// entry out in `top`.
+__device__ __forceinline__ bool mtf_chunk(const uint4& v, uint32_t cc, uint32_t c, uint32_t& top, uint32_t* dst, uint32_t& r)
+{
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    uint32_t       zc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        zc[k] = haszero8(d[k] ^ cc);
+    uint32_t o[4];
+    if (zc[0] | zc[1] | zc[2] | zc[3])
+    {
+        const uint32_t k  = zc[0] ? 0 : zc[1] ? 1 : zc[2] ? 2 : 3;
+        const uint32_t zz = zc[0] ? zc[0] : zc[1] ? zc[1] : zc[2] ? zc[2] : zc[3];
+        const uint32_t b  = (uint32_t) __builtin_ctz(zz) >> 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            const uint32_t ntop = d[q] >> 24;
+            o[q]                = ((uint32_t) q < k) ? shift1(d[q], top) : ((uint32_t) q == k) ? shift_upto(d[q], top, b) : d[q];
+            top                 = ntop;
+        }
+        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+        r                              = k * 4 + b;
+        return true;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t ntop = d[q] >> 24;
+        o[q]                = shift1(d[q], top);
+        top                 = ntop;
+    }
+    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+    (void) c;
+    return false;
+}
+
 // One MTF step.  Entries 0..15 live in registers R; entries 16..255 in this thread's LDS table,
 // read, checked and written back shifted 16 entries at a time (one ds_read_b128 / ds_write_b128
 // pair per chunk) until the chunk holding the symbol.  Returns the symbol's position.
@@ -167,38 +207,18 @@ __device__ __forceinline__ uint32_t mtf_step(uint32_t (&R)[4], uint32_t* tbl, ui
         R[q]                = shift1(cur, top);
         top                 = ntop;
     }
-    for (uint32_t ch = 1; ch < 16; ++ch)
+    // Chunks are visited two at a time: both 16-byte reads are issued together, so a deep search
+    // waits for one LDS round trip per 32 entries.  (Chunk 16 is the row's pad: it is read with
+    // chunk 15 but never examined, since the symbol is found by chunk 15 at the latest.)
+    for (uint32_t ch = 1; ch < 16; ch += 2)
     {
-        uint4          v = *reinterpret_cast<const uint4*>(tbl + ch * 4);
-        const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-        uint32_t       zc[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            zc[k] = haszero8(d[k] ^ cc);
-        uint32_t o[4];
-        if (zc[0] | zc[1] | zc[2] | zc[3])
-        {
-            const uint32_t k  = zc[0] ? 0 : zc[1] ? 1 : zc[2] ? 2 : 3;
-            const uint32_t zz = zc[0] ? zc[0] : zc[1] ? zc[1] : zc[2] ? zc[2] : zc[3];
-            const uint32_t b  = (uint32_t) __builtin_ctz(zz) >> 3;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-            {
-                const uint32_t ntop = d[q] >> 24;
-                o[q]                = ((uint32_t) q < k) ? shift1(d[q], top) : ((uint32_t) q == k) ? shift_upto(d[q], top, b) : d[q];
-                top                 = ntop;
-            }
-            *reinterpret_cast<uint4*>(tbl + ch * 4) = make_uint4(o[0], o[1], o[2], o[3]);
-            return ch * 16 + k * 4 + b;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            const uint32_t ntop = d[q] >> 24;
-            o[q]                = shift1(d[q], top);
-            top                 = ntop;
-        }
-        *reinterpret_cast<uint4*>(tbl + ch * 4) = make_uint4(o[0], o[1], o[2], o[3]);
+        const uint4 va = *reinterpret_cast<const uint4*>(tbl + ch * 4);
+        const uint4 vb = *reinterpret_cast<const uint4*>(tbl + ch * 4 + 4);
+        uint32_t    r;
+        if (mtf_chunk(va, cc, c, top, tbl + ch * 4, r))
+            return ch * 16 + r;
+        if (mtf_chunk(vb, cc, c, top, tbl + ch * 4 + 4, r))
+            return ch * 16 + 16 + r;
     }
     return 255;  // unreachable: the table is a permutation of 0..255
 }

@@ -26,110 +26,6 @@ namespace {
 constexpr int TPB = 256;
 constexpr int PT  = RLE_TILE / TPB;  // 16 bytes per thread
 
-struct RunSum
-{
-    uint32_t len, pre, suf;
-    uint8_t  first, last, all, pad;
-};
-
-__device__ __forceinline__ RunSum run_combine(const RunSum& A, const RunSum& B)
-{
-    if (A.len == 0)
-        return B;
-    if (B.len == 0)
-        return A;
-    RunSum R;
-    R.len   = A.len + B.len;
-    R.first = A.first;
-    R.pre   = (A.all && A.first == B.first) ? A.len + B.pre : A.pre;
-    R.last  = B.last;
-    R.suf   = (B.all && B.last == A.last) ? B.len + A.suf : B.suf;
-    R.all   = A.all && B.all && A.last == B.first;
-    R.pad   = 0;
-    return R;
-}
-
-struct GapSum
-{
-    uint32_t len, lead, trail, has;  // has = contains a non-literal position
-};
-
-__device__ __forceinline__ GapSum gap_combine(const GapSum& A, const GapSum& B)
-{
-    GapSum R;
-    R.len   = A.len + B.len;
-    R.has   = A.has | B.has;
-    R.lead  = A.has ? A.lead : A.len + B.lead;
-    R.trail = B.has ? B.trail : B.len + A.trail;
-    return R;
-}
-
-__device__ __forceinline__ RunSum shfl_run(const RunSum& x, int src)
-{
-    RunSum r;
-    r.len             = __shfl(x.len, src, 64);
-    r.pre             = __shfl(x.pre, src, 64);
-    r.suf             = __shfl(x.suf, src, 64);
-    const uint32_t pk = __shfl((uint32_t) x.first | ((uint32_t) x.last << 8) | ((uint32_t) x.all << 16), src, 64);
-    r.first           = pk & 0xFF;
-    r.last            = (pk >> 8) & 0xFF;
-    r.all             = (pk >> 16) & 1;
-    r.pad             = 0;
-    return r;
-}
-
-__device__ __forceinline__ GapSum shfl_gap(const GapSum& x, int src)
-{
-    return GapSum{(uint32_t) __shfl(x.len, src, 64), (uint32_t) __shfl(x.lead, src, 64), (uint32_t) __shfl(x.trail, src, 64),
-                  (uint32_t) __shfl(x.has, src, 64)};
-}
-
-// Block-wide EXCLUSIVE scans over 256 threads (forward: combine(prefix, x); backward: combine(x, suffix)).
-template <typename T, typename Comb, typename Shfl>
-__device__ __forceinline__ T block_scan_fwd(const T& v, const T& seed, const T& ident, T* lds, Comb comb, Shfl shfl)
-{
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    T         x    = v;
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        T o = shfl(x, max(lane - d, 0));
-        if (lane >= d)
-            x = comb(o, x);
-    }
-    if (lane == 63)
-        lds[w] = x;
-    T ex = shfl(x, max(lane - 1, 0));
-    __syncthreads();
-    T pre = seed;
-    for (int i = 0; i < w; ++i)
-        pre = comb(pre, lds[i]);
-    __syncthreads();
-    return lane == 0 ? pre : comb(pre, ex);
-    (void) ident;
-}
-
-template <typename T, typename Comb, typename Shfl>
-__device__ __forceinline__ T block_scan_bwd(const T& v, const T& seed, T* lds, Comb comb, Shfl shfl)
-{
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    T         x    = v;
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        T o = shfl(x, min(lane + d, 63));
-        if (lane + d < 64)
-            x = comb(x, o);
-    }
-    if (lane == 0)
-        lds[w] = x;
-    T ex = shfl(x, min(lane + 1, 63));
-    __syncthreads();
-    T suf = seed;
-    for (int i = 3; i > w; --i)
-        suf = comb(lds[i], suf);
-    __syncthreads();
-    return lane == 63 ? suf : comb(ex, suf);
-}
-
 struct TileRun
 {
     uint32_t len, pre, suf, flags;  // flags: first | last << 8 | all << 16
@@ -150,160 +46,247 @@ struct TileOff
     uint32_t g_in, out_off, rem_after, pad;
 };
 
-__device__ __forceinline__ void load16(const uint8_t* p, uint32_t cnt, uint32_t base, uint8_t (&x)[PT])
+// ---- wave / workgroup scans on one dword per thread (DPP inside rows of 16, row totals by
+// readlane; no LDS inside a wave) ----
+struct OpMax
 {
-    // base = first tile byte of this thread; bytes beyond cnt are never used
-    if (base + PT <= cnt && (((uintptr_t) (p + base)) & 15) == 0)
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); }
+};
+struct OpMin
+{
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return min(a, b); }
+};
+struct OpAdd
+{
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+
+// Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order.
+template <bool FWD, typename Op>
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op)
+{
+    if (FWD)
     {
-        const uint4 v = *reinterpret_cast<const uint4*>(p + base);
-        const uint32_t wds[4] = {v.x, v.y, v.z, v.w};
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x111, 0xf, 0xf, false));  // row_shr:1
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x112, 0xf, 0xf, false));  // row_shr:2
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x114, 0xf, 0xf, false));  // row_shr:4
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x118, 0xf, 0xf, false));  // row_shr:8
+        const uint32_t t0 = __builtin_amdgcn_readlane(x, 15), t1 = __builtin_amdgcn_readlane(x, 31), t2 = __builtin_amdgcn_readlane(x, 47);
+        const uint32_t c1 = t0, c2 = op(t0, t1), c3 = op(c2, t2);
+        const uint32_t row = (uint32_t) lane_id() >> 4;
+        return op(x, row == 0 ? id : row == 1 ? c1 : row == 2 ? c2 : c3);
+    }
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x101, 0xf, 0xf, false));  // row_shl:1
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x102, 0xf, 0xf, false));  // row_shl:2
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x104, 0xf, 0xf, false));  // row_shl:4
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x108, 0xf, 0xf, false));  // row_shl:8
+    const uint32_t t1 = __builtin_amdgcn_readlane(x, 16), t2 = __builtin_amdgcn_readlane(x, 32), t3 = __builtin_amdgcn_readlane(x, 48);
+    const uint32_t c2 = t3, c1 = op(t2, t3), c0 = op(t1, c1);
+    const uint32_t row = (uint32_t) lane_id() >> 4;
+    return op(x, row == 3 ? id : row == 2 ? c2 : row == 1 ? c1 : c0);
+}
+
+// Exclusive scan over the 256 threads of the workgroup (thread order FWD or reversed), seeded
+// with `seed` (the value before the first / after the last thread).  tmp: 4 dwords of LDS.  If
+// `total` is given it receives the inclusive total including the seed.
+template <bool FWD, typename Op>
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t seed, uint32_t id, Op op, uint32_t* tmp, uint32_t* total = nullptr)
+{
+    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t inc  = wave_scan<FWD>(v, id, op);
+    if (lane == (FWD ? 63 : 0))
+        tmp[w] = inc;
+    // value of the neighbour lane before this one in scan order (id at the wave's first lane)
+    uint32_t ex = FWD ? (uint32_t) __shfl_up((int) inc, 1, 64) : (uint32_t) __shfl_down((int) inc, 1, 64);
+    if (lane == (FWD ? 0 : 63))
+        ex = id;
+    __syncthreads();
+    uint32_t pre = seed, all = seed;
 #pragma unroll
-        for (int i = 0; i < PT; ++i)
-            x[i] = (wds[i >> 2] >> (8 * (i & 3))) & 0xFF;
+    for (int i = 0; i < 4; ++i)
+    {
+        const int      k = FWD ? i : 3 - i;
+        const uint32_t t = tmp[k];
+        if (FWD ? (k < w) : (k > w))
+            pre = op(pre, t);
+        all = op(all, t);
+    }
+    __syncthreads();
+    if (total)
+        *total = all;
+    return op(pre, ex);
+}
+
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[4], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
+
+// Bit i set iff byte i differs from byte i-1 (bit 0: from `prev`), for the PT bytes of w.
+__device__ __forceinline__ uint32_t diff_mask(const uint32_t (&w)[4], uint32_t prev)
+{
+    uint32_t m = 0, carry = prev & 0xFFu;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+    {
+        const uint32_t z  = w[d] ^ ((w[d] << 8) | carry);          // byte j: x[j] ^ x[j-1]
+        const uint32_t nz = (((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;  // bit 7 of byte j: nonzero
+        m |= ((((nz >> 7) * 0x01020408u) >> 24) & 0xFu) << (4 * d);
+        carry = w[d] >> 24;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t hi_bit(uint32_t m) { return 31u - (uint32_t) __builtin_clz(m); }  // m != 0
+__device__ __forceinline__ uint32_t lo_bit(uint32_t m) { return (uint32_t) __builtin_ctz(m); }        // m != 0
+
+// One tile as the workgroup sees it: thread t holds positions [16t, 16t + nt) of the tile.
+struct TileThread
+{
+    uint32_t w[4];
+    uint32_t base, nt, n;
+    uint32_t bm;    // run boundaries at the thread's positions (position 0 of the tile always is one)
+};
+
+__device__ __forceinline__ void tile_load(const uint8_t* __restrict__ in, const Piece& P, TileThread& T)
+{
+    const uint8_t* p = in + P.off;
+    T.n              = P.len;
+    T.base           = threadIdx.x * PT;
+    T.nt             = T.base < T.n ? min((uint32_t) PT, T.n - T.base) : 0;
+    if (T.nt == PT && (((uintptr_t) (p + T.base)) & 15) == 0)
+    {
+        const uint4 v = *reinterpret_cast<const uint4*>(p + T.base);
+        T.w[0] = v.x, T.w[1] = v.y, T.w[2] = v.z, T.w[3] = v.w;
     }
     else
     {
 #pragma unroll
-        for (int i = 0; i < PT; ++i)
-            x[i] = (base + i < cnt) ? p[base + i] : 0;
-    }
-}
-
-// All per-thread loops below are fully unrolled over the PT positions (static register indices);
-// positions >= n (tile end) are masked.
-__device__ __forceinline__ uint32_t sel(const uint8_t (&x)[PT], uint32_t i)
-{
-    uint32_t r = 0;
-#pragma unroll
-    for (int j = 0; j < PT; ++j)
-        r = ((uint32_t) j == i) ? x[j] : r;
-    return r;
-}
-
-__device__ __forceinline__ RunSum thread_runsum(const uint8_t (&x)[PT], uint32_t n)
-{
-    RunSum s;
-    s.len = n;
-    s.pad = 0;
-    if (n == 0)
-    {
-        s.pre = s.suf = 0;
-        s.first = s.last = 0;
-        s.all            = 1;
-        return s;
-    }
-    const uint32_t last = sel(x, n - 1);
-    uint32_t       p = 1, q = 1;
-    bool           pr = true, qr = true;
-#pragma unroll
-    for (int i = 1; i < PT; ++i)
-    {
-        pr = pr && (uint32_t) i < n && x[i] == x[0];
-        p += pr ? 1 : 0;
-    }
-    // backwards from n-1: position n-1-j for j = 1..
-#pragma unroll
-    for (int i = PT - 2; i >= 0; --i)
-    {
-        const bool in = (uint32_t) i < n - 1;  // strictly before the last position
-        // walk i = n-2, n-3, ... : positions above n-2 are skipped (not yet in the run walk)
-        if (in)
+        for (int d = 0; d < 4; ++d)
         {
-            qr = qr && x[i] == last;
-            q += qr ? 1 : 0;
+            uint32_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (T.base + 4 * d + j < T.n)
+                    x |= (uint32_t) p[T.base + 4 * d + j] << (8 * j);
+            T.w[d] = x;
         }
     }
-    s.first = x[0];
-    s.last  = (uint8_t) last;
-    s.pre   = p;
-    s.suf   = q;
-    s.all   = (p == n);
-    return s;
+    const uint32_t prev = T.base > 0 && T.nt ? p[T.base - 1] : 0u;
+    uint32_t       bm   = diff_mask(T.w, prev);
+    if (T.base == 0)
+        bm |= 1u;
+    T.bm = T.nt ? bm & ((1u << T.nt) - 1u) : 0u;
 }
 
-// Per-position classification.  kind: 0 literal, 1 run-block start, 2 run continuation.
-// For run-block starts clen = block length.  `left` / `right`: run extension into this thread's
-// positions from before / after them (same byte as x[0] / x[n-1]).
-__device__ __forceinline__ void classify(const uint8_t (&x)[PT], uint32_t n, uint32_t left, uint32_t right, uint8_t (&kind)[PT],
-                                         uint8_t (&clen)[PT])
+// Classify the thread's positions: nl = non-literal (covered by run blocks), rs = run-block
+// starts, clen[i] = block length at a run-block start.  left / right: run extension into the tile
+// from before / after it (TileLink).
+__device__ __forceinline__ void tile_runs(const TileThread& T, uint32_t left, uint32_t right, uint32_t* tmp, uint32_t& nl, uint32_t& rs,
+                                          uint32_t (&clen)[PT])
 {
-    uint32_t k[PT];  // position inside its maximal run
-#pragma unroll
-    for (int i = 0; i < PT; ++i)
-        k[i] = (i == 0) ? left : (x[i] == x[i - 1] ? k[i - 1] + 1 : 0);
-    uint32_t nxt = 0;
-#pragma unroll
-    for (int i = PT - 1; i >= 0; --i)
-    {
-        uint32_t r;  // positions from i to the end of its run, inclusive
-        if ((uint32_t) i >= n)
-            r = 0;
-        else if ((uint32_t) i == n - 1)
-            r = 1 + right;
-        else
-            r = (x[i] == x[i + 1]) ? nxt + 1 : 1;
-        nxt                 = r;
-        const uint32_t L    = k[i] + r;
-        const uint32_t full = L >> 7, rm = L & 127, q = k[i] >> 7;
-        uint8_t        kd = 0, cl = 0;
-        if (L >= 3)
-        {
-            if (q < full)
-            {
-                kd = (k[i] & 127) == 0 ? 1 : 2;
-                cl = 128;
-            }
-            else if (rm >= 3)
-            {
-                kd = (k[i] == (full << 7)) ? 1 : 2;
-                cl = (uint8_t) rm;
-            }
-        }
-        kind[i] = kd;
-        clen[i] = cl;
-    }
-}
-
-__device__ __forceinline__ GapSum thread_gapsum(const uint8_t (&kind)[PT], uint32_t n)
-{
-    GapSum   g{n, 0, 0, 0};
-    bool     lead = true;
-    uint32_t trail = 0;
+    const uint32_t lastB  = T.bm ? T.base + hi_bit(T.bm) : 0u;
+    const uint32_t firstB = T.bm ? T.base + lo_bit(T.bm) : T.n;
+    const uint32_t Sprev  = block_scan_excl<true>(lastB, 0u, 0u, OpMax(), tmp);
+    const uint32_t Enext  = block_scan_excl<false>(firstB, T.n, T.n, OpMin(), tmp);
+    nl = rs = 0;
 #pragma unroll
     for (int i = 0; i < PT; ++i)
     {
-        if ((uint32_t) i < n)
+        clen[i] = 0;
+        if ((uint32_t) i >= T.nt)
+            continue;
+        const uint32_t p  = T.base + i;
+        const uint32_t sm = T.bm & ((2u << i) - 1u);
+        const uint32_t em = T.bm & ~((2u << i) - 1u);
+        const uint32_t S  = sm ? T.base + hi_bit(sm) : Sprev;
+        const uint32_t E  = em ? T.base + lo_bit(em) : Enext;
+        const uint32_t k  = p - S + (S == 0 ? left : 0u);       // position inside the maximal run
+        const uint32_t r  = E - p + (E == T.n ? right : 0u);    // positions from p to the run end
+        const uint32_t L  = k + r, tail = L & 127u;
+        const uint32_t cut = tail < 3 ? tail : 0u;              // 1 or 2 tail bytes become literals
+        if (L >= 3 && k < L - cut)
         {
-            const bool lit = kind[i] == 0;
-            lead           = lead && lit;
-            g.lead += lead ? 1 : 0;
-            g.has |= lit ? 0u : 1u;
-            trail = lit ? trail + 1 : 0;
+            nl |= 1u << i;
+            if ((k & 127u) == 0)
+            {
+                rs |= 1u << i;
+                clen[i] = min(128u, L - k);
+            }
         }
     }
-    g.trail = trail;
-    return g;
 }
 
+// Output bytes of the thread's positions; with WRITE, also stages them at stage[pos...].
+// g_in: gap offset of the tile's first position if the gap comes from before the tile;
+// rem_after: literals following the tile in its trailing gap.
+template <bool WRITE>
+__device__ __forceinline__ uint32_t tile_emit(const TileThread& T, uint32_t nl, uint32_t rs, const uint32_t (&clen)[PT], uint32_t GSprev,
+                                              uint32_t GEnext, uint32_t g_in, uint32_t rem_after, uint8_t* stage, uint32_t pos)
+{
+    uint32_t bytes = 0;
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+    {
+        if ((uint32_t) i >= T.nt)
+            continue;
+        const uint32_t p = T.base + i;
+        const uint32_t x = byte_at(T.w, i);
+        if (nl & (1u << i))
+        {
+            if (rs & (1u << i))
+            {
+                if (WRITE)
+                {
+                    stage[pos + bytes]     = (uint8_t) (int8_t) (1 - (int) clen[i]);
+                    stage[pos + bytes + 1] = (uint8_t) x;
+                }
+                bytes += 2;
+            }
+            continue;
+        }
+        const uint32_t gm  = nl & ((1u << i) - 1u);
+        const uint32_t GS  = gm ? T.base + hi_bit(gm) + 1 : GSprev;   // start of the literal gap
+        const uint32_t go  = p - GS + (GS == 0 ? g_in : 0u);
+        const bool     ctl = (go & 127u) == 0;
+        if (WRITE)
+        {
+            if (ctl)
+            {
+                const uint32_t em  = nl & ~((2u << i) - 1u);
+                const uint32_t GE  = em ? T.base + lo_bit(em) : GEnext;  // end of the literal gap
+                const uint32_t rem = GE - p + (GE == T.n ? rem_after : 0u);
+                stage[pos + bytes] = (uint8_t) (min(rem, 128u) - 1);
+            }
+            stage[pos + bytes + (ctl ? 1 : 0)] = (uint8_t) x;
+        }
+        bytes += ctl ? 2 : 1;
+    }
+    return bytes;
+}
+
+// Tile run summary: leading / trailing run length, first / last byte, all one run.
 __global__ void __launch_bounds__(TPB) k_rle_runs(const uint8_t* __restrict__ in, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                   TileRun* __restrict__ out)
 {
-    __shared__ RunSum lds[4];
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t edge[2];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
-        const Piece    P = tiles[t];
-        uint8_t        x[PT];
-        const uint32_t base = threadIdx.x * PT;
-        load16(in + P.off, P.len, base, x);
-        const uint32_t n = base < P.len ? min((uint32_t) PT, P.len - base) : 0;
-        RunSum         s = thread_runsum(x, n);
-        RunSum         z{0, 0, 0, 0, 0, 0, 0};
-        auto           comb = [](const RunSum& a, const RunSum& b) { return run_combine(a, b); };
-        // inclusive total via exclusive + own
-        RunSum ex  = block_scan_fwd(s, z, z, lds, comb, shfl_run);
-        RunSum inc = run_combine(ex, s);
-        if (threadIdx.x == TPB - 1)
-            out[t] = TileRun{inc.len, inc.pre, inc.suf, (uint32_t) inc.first | ((uint32_t) inc.last << 8) | ((uint32_t) inc.all << 16)};
+        const Piece P = tiles[t];
+        TileThread  T;
+        tile_load(in, P, T);
+        if (T.nt && T.base + T.nt == T.n)
+            edge[1] = byte_at(T.w, (int) T.nt - 1);
+        if (threadIdx.x == 0)
+            edge[0] = byte_at(T.w, 0);
+        // first boundary after position 0 and the last boundary
+        const uint32_t b1 = T.bm & ~(T.base == 0 ? 1u : 0u);
+        uint32_t       lo, hi;
+        block_scan_excl<true>(T.bm ? T.base + hi_bit(T.bm) : 0u, 0u, 0u, OpMax(), tmp, &hi);
+        block_scan_excl<true>(b1 ? T.base + lo_bit(b1) : T.n, T.n, T.n, OpMin(), tmp, &lo);
+        if (threadIdx.x == 0)
+        {
+            const uint32_t all = lo >= T.n ? 1u : 0u;
+            out[t]             = TileRun{T.n, lo, T.n - hi, edge[0] | (edge[1] << 8) | (all << 16)};
+        }
         __syncthreads();
     }
 }
@@ -336,112 +319,31 @@ __global__ void k_rle_link(const uint32_t* __restrict__ first, const uint32_t* _
     }
 }
 
-// Shared per-tile analysis: run classification, gap scans, output byte counts.
-struct TileView
-{
-    uint8_t  x[PT];
-    uint8_t  kind[PT];
-    uint8_t  clen[PT];
-    uint32_t n;
-};
-
-__device__ __forceinline__ void tile_classify(const uint8_t* __restrict__ in, const Piece& P, TileLink L, RunSum* lds, TileView& v)
-{
-    const uint32_t base = threadIdx.x * PT;
-    load16(in + P.off, P.len, base, v.x);
-    v.n      = base < P.len ? min((uint32_t) PT, P.len - base) : 0;
-    RunSum s = thread_runsum(v.x, v.n);
-    // seeds: the run entering from the left has the tile's first byte; from the right, its last byte
-    __shared__ uint8_t edge[2];
-    if (threadIdx.x == 0)
-        edge[0] = v.x[0];
-    if (base < P.len && base + v.n == P.len)
-        edge[1] = (uint8_t) sel(v.x, v.n - 1);
-    __syncthreads();
-    RunSum sl{L.left, L.left, L.left, edge[0], edge[0], 1, 0};
-    RunSum sr{L.right, L.right, L.right, edge[1], edge[1], 1, 0};
-    auto   comb = [](const RunSum& a, const RunSum& b) { return run_combine(a, b); };
-    RunSum E    = block_scan_fwd(s, sl, sl, lds, comb, shfl_run);
-    RunSum F    = block_scan_bwd(s, sr, lds, comb, shfl_run);
-    uint32_t left  = (v.n && E.len && E.last == v.x[0]) ? E.suf : 0;
-    uint32_t right = (v.n && F.len && F.first == sel(v.x, v.n - 1)) ? F.pre : 0;
-    classify(v.x, v.n, left, right, v.kind, v.clen);
-}
-
-// Output bytes of this thread's positions given the gap offset of its first position (go0) and
-// the literal count following its last position (rem_after).  Optionally writes them to `stage`.
-template <bool WRITE>
-__device__ __forceinline__ uint32_t emit_thread(const TileView& v, uint32_t go0, uint32_t rem_after, uint8_t* stage, uint32_t pos)
-{
-    // remaining literals from position i to the gap end (inclusive), computed backwards
-    uint32_t rem[PT];
-    uint32_t run = rem_after;
-#pragma unroll
-    for (int i = PT - 1; i >= 0; --i)
-    {
-        if ((uint32_t) i < v.n)
-            run = (v.kind[i] == 0) ? run + 1 : 0;
-        rem[i] = run;
-    }
-    uint32_t go = go0, bytes = 0;
-#pragma unroll
-    for (int i = 0; i < PT; ++i)
-    {
-        if ((uint32_t) i >= v.n)
-            continue;
-        if (v.kind[i] == 0)
-        {
-            const bool ctl = (go & 127) == 0;
-            if (WRITE)
-            {
-                if (ctl)
-                    stage[pos + bytes] = (uint8_t) (min(rem[i], 128u) - 1);
-                stage[pos + bytes + (ctl ? 1 : 0)] = v.x[i];
-            }
-            bytes += ctl ? 2 : 1;
-            ++go;
-        }
-        else
-        {
-            go = 0;
-            if (v.kind[i] == 1)
-            {
-                if (WRITE)
-                {
-                    stage[pos + bytes]     = (uint8_t) (int8_t) (1 - (int) v.clen[i]);
-                    stage[pos + bytes + 1] = v.x[i];
-                }
-                bytes += 2;
-            }
-        }
-    }
-    return bytes;
-}
 
 __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ in, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                    const TileLink* __restrict__ link, TileGap* __restrict__ tg)
 {
-    __shared__ RunSum   lds[4];
-    __shared__ GapSum   glds[4];
     __shared__ uint32_t tmp[8];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
-        const Piece P = tiles[t];
-        TileView    v;
-        tile_classify(in, P, link[t], lds, v);
-        const GapSum gs   = thread_gapsum(v.kind, v.n);
-        auto         comb = [](const GapSum& a, const GapSum& b) { return gap_combine(a, b); };
-        const GapSum z{0, 0, 0, 0};
-        const GapSum E = block_scan_fwd(gs, z, z, glds, comb, shfl_gap);
-        const GapSum F = block_scan_bwd(gs, z, glds, comb, shfl_gap);
-        const uint32_t bytes = emit_thread<false>(v, E.trail, F.lead, nullptr, 0);
+        const Piece    P = tiles[t];
+        const TileLink K = link[t];
+        TileThread     T;
+        tile_load(in, P, T);
+        uint32_t nl, rs, clen[PT];
+        tile_runs(T, K.left, K.right, tmp, nl, rs, clen);
+        uint32_t       maxNL, minNL;
+        const uint32_t GSprev = block_scan_excl<true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), tmp, &maxNL);
+        block_scan_excl<true>(nl ? T.base + lo_bit(nl) : T.n, T.n, T.n, OpMin(), tmp, &minNL);
+        const uint32_t bytes = tile_emit<false>(T, nl, rs, clen, GSprev, 0, 0, 0, nullptr, 0);
         uint32_t       total;
         block256_exclusive_sum(bytes, tmp, &total);
-        if (threadIdx.x == TPB - 1)
+        if (threadIdx.x == 0)
         {
-            const GapSum tot = gap_combine(E, gs);
-            // leading stretch control bytes were counted with gap offset 0: ceil(lead/128)
-            tg[t] = TileGap{tot.lead, tot.trail, tot.has, total - (tot.lead + 127) / 128};
+            const uint32_t has  = maxNL > 0 ? 1u : 0u;
+            const uint32_t lead = has ? minNL : T.n;
+            // the leading stretch's control bytes were counted with gap offset 0: ceil(lead/128)
+            tg[t] = TileGap{lead, has ? T.n - maxNL : T.n, has, total - (lead + 127) / 128};
         }
         __syncthreads();
     }
@@ -480,29 +382,25 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ rle_base, uint8_t* __restrict__ out,
                                                    uint32_t* __restrict__ hist)
 {
-    __shared__ RunSum   lds[4];
-    __shared__ GapSum   glds[4];
     __shared__ uint32_t tmp[8];
     __shared__ uint8_t  stage[RLE_TILE + RLE_TILE / 64 + 64];
     __shared__ uint32_t h[256];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
-        const Piece   P = tiles[t];
-        const TileOff O = to[t];
-        h[threadIdx.x]  = 0;
-        TileView v;
-        tile_classify(in, P, link[t], lds, v);
-        const GapSum gs   = thread_gapsum(v.kind, v.n);
-        auto         comb = [](const GapSum& a, const GapSum& b) { return gap_combine(a, b); };
-        const GapSum z{0, 0, 0, 0};
-        const GapSum sl{O.g_in, O.g_in, O.g_in, 0};
-        const GapSum sr{O.rem_after, O.rem_after, O.rem_after, 0};
-        const GapSum E     = block_scan_fwd(gs, sl, z, glds, comb, shfl_gap);
-        const GapSum F     = block_scan_bwd(gs, sr, glds, comb, shfl_gap);
-        const uint32_t by  = emit_thread<false>(v, E.trail, F.lead, nullptr, 0);
+        const Piece    P = tiles[t];
+        const TileOff  O = to[t];
+        const TileLink K = link[t];
+        h[threadIdx.x]   = 0;
+        TileThread T;
+        tile_load(in, P, T);
+        uint32_t nl, rs, clen[PT];
+        tile_runs(T, K.left, K.right, tmp, nl, rs, clen);
+        const uint32_t GSprev = block_scan_excl<true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), tmp);
+        const uint32_t GEnext = block_scan_excl<false>(nl ? T.base + lo_bit(nl) : T.n, T.n, T.n, OpMin(), tmp);
+        const uint32_t by     = tile_emit<false>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, nullptr, 0);
         uint32_t       total;
         const uint32_t pos = block256_exclusive_sum(by, tmp, &total);
-        emit_thread<true>(v, E.trail, F.lead, stage, pos);
+        tile_emit<true>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, stage, pos);
         __syncthreads();
         uint8_t* dst = out + rle_base[P.block] + O.out_off;
         for (uint32_t i = threadIdx.x; i < total; i += TPB)
