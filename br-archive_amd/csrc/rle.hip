@@ -291,34 +291,97 @@ __global__ void __launch_bounds__(TPB) k_rle_runs(const uint8_t* __restrict__ in
     }
 }
 
-// One thread per block walks its tiles forward and backward.
-__global__ void k_rle_link(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
-                           const TileRun* __restrict__ tr, TileLink* __restrict__ link)
+// Run summary of a stretch of tiles (the run monoid): length, first / last byte, leading /
+// trailing run length, all one run.
+struct RunSum
 {
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    uint32_t len, pre, suf, first, last, all;
+};
+
+__device__ __forceinline__ RunSum run_combine(const RunSum& A, const RunSum& B)
+{
+    if (A.len == 0)
+        return B;
+    if (B.len == 0)
+        return A;
+    const bool join = A.last == B.first;
+    return RunSum{A.len + B.len, (A.all && join) ? A.len + B.pre : A.pre, (B.all && join) ? B.len + A.suf : B.suf, A.first, B.last,
+                  (A.all && B.all && join) ? 1u : 0u};
+}
+
+__device__ __forceinline__ RunSum shfl_run(const RunSum& x, int src)
+{
+    return RunSum{(uint32_t) __shfl((int) x.len, src, 64), (uint32_t) __shfl((int) x.pre, src, 64), (uint32_t) __shfl((int) x.suf, src, 64),
+                  (uint32_t) __shfl((int) x.first, src, 64), (uint32_t) __shfl((int) x.last, src, 64), (uint32_t) __shfl((int) x.all, src, 64)};
+}
+
+// Gap-offset recurrence g -> h ? v : g + v of one tile (or a stretch of tiles: composition).
+struct GapFn
+{
+    uint32_t h, v;
+};
+
+__device__ __forceinline__ GapFn gap_then(const GapFn& a, const GapFn& b) { return b.h ? b : GapFn{a.h, a.v + b.v}; }
+
+__device__ __forceinline__ GapFn shfl_gap(const GapFn& x, int src)
+{
+    return GapFn{(uint32_t) __shfl((int) x.h, src, 64), (uint32_t) __shfl((int) x.v, src, 64)};
+}
+
+// Inclusive scan across the 64 lanes of a wave with a generic combine (lane order FWD or reversed):
+// comb(earlier, later) in scan order.
+template <bool FWD, typename T, typename Comb, typename Shfl>
+__device__ __forceinline__ T wave_scan_t(T x, Comb comb, Shfl shfl)
+{
+    const int lane = lane_id();
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const T o = shfl(x, FWD ? max(lane - d, 0) : min(lane + d, 63));
+        if (FWD ? lane >= d : lane + d < 64)
+            x = FWD ? comb(o, x) : comb(x, o);
+    }
+    return x;
+}
+
+// One wave per block: run extension into every tile from the left and from the right.
+__global__ void __launch_bounds__(64) k_rle_link(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
+                                                 const TileRun* __restrict__ tr, TileLink* __restrict__ link)
+{
+    const int  lane  = lane_id();
+    const auto comb  = [](const RunSum& a, const RunSum& b) { return run_combine(a, b); };
+    const auto load  = [&](uint32_t t) {
+        const TileRun T = tr[t];
+        return RunSum{T.len, T.pre, T.suf, T.flags & 0xFFu, (T.flags >> 8) & 0xFFu, (T.flags >> 16) & 1u};
+    };
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint32_t t0 = first[b], nt = count[b];
-        uint32_t       last = 0, suf = 0;
-        for (uint32_t i = 0; i < nt; ++i)
+        RunSum         carry{0, 0, 0, 0, 0, 1};  // tiles before the chunk
+        for (uint32_t c = 0; c < nt; c += 64)
         {
-            const TileRun  T   = tr[t0 + i];
-            const uint32_t fb  = T.flags & 0xFF, lb = (T.flags >> 8) & 0xFF, all = (T.flags >> 16) & 1;
-            link[t0 + i].left  = (i > 0 && last == fb) ? suf : 0;
-            suf                = (i > 0 && all && fb == last) ? suf + T.len : T.suf;
-            last               = lb;
+            const uint32_t i   = c + lane;
+            const RunSum   me  = i < nt ? load(t0 + i) : RunSum{0, 0, 0, 0, 0, 1};
+            const RunSum   inc = wave_scan_t<true>(me, comb, shfl_run);
+            RunSum         ex  = shfl_run(inc, max(lane - 1, 0));
+            ex                 = lane == 0 ? carry : run_combine(carry, ex);
+            if (i < nt)
+                link[t0 + i].left = (ex.len && ex.last == me.first) ? ex.suf : 0u;
+            carry = run_combine(carry, shfl_run(inc, 63));
         }
-        uint32_t firstb = 0, pre = 0;
-        for (int i = (int) nt - 1; i >= 0; --i)
+        carry = RunSum{0, 0, 0, 0, 0, 1};  // tiles after the chunk
+        for (int c = (int) ((nt + 63) / 64) * 64 - 64; c >= 0; c -= 64)
         {
-            const TileRun  T   = tr[t0 + i];
-            const uint32_t fb  = T.flags & 0xFF, lb = (T.flags >> 8) & 0xFF, all = (T.flags >> 16) & 1;
-            link[t0 + i].right = (i < (int) nt - 1 && firstb == lb) ? pre : 0;
-            pre                = (i < (int) nt - 1 && all && lb == firstb) ? pre + T.len : T.pre;
-            firstb             = fb;
+            const uint32_t i   = (uint32_t) c + lane;
+            const RunSum   me  = i < nt ? load(t0 + i) : RunSum{0, 0, 0, 0, 0, 1};
+            const RunSum   inc = wave_scan_t<false>(me, comb, shfl_run);
+            RunSum         ex  = shfl_run(inc, min(lane + 1, 63));
+            ex                 = lane == 63 ? carry : run_combine(ex, carry);
+            if (i < nt)
+                link[t0 + i].right = (ex.len && ex.first == me.last) ? ex.pre : 0u;
+            carry = run_combine(shfl_run(inc, 0), carry);
         }
     }
 }
-
 
 __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ in, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                    const TileLink* __restrict__ link, TileGap* __restrict__ tg)
@@ -349,30 +412,60 @@ __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ i
     }
 }
 
-__global__ void k_rle_offsets(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
-                              const Piece* __restrict__ tiles, const TileGap* __restrict__ tg, TileOff* __restrict__ to,
-                              uint32_t* __restrict__ rle_size)
+// One wave per block: gap offset entering each tile, output offset, literals after the tile.
+__global__ void __launch_bounds__(64) k_rle_offsets(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
+                                                    const Piece* __restrict__ tiles, const TileGap* __restrict__ tg, TileOff* __restrict__ to,
+                                                    uint32_t* __restrict__ rle_size)
 {
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    const int  lane = lane_id();
+    const auto fwd  = [](const GapFn& a, const GapFn& b) { return gap_then(a, b); };
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint32_t t0 = first[b], nt = count[b];
-        uint32_t       g = 0, run = 0;
-        for (uint32_t i = 0; i < nt; ++i)
+        GapFn          carry{0, 0};
+        uint32_t       run = 0;
+        for (uint32_t c = 0; c < nt; c += 64)
         {
-            const TileGap  G    = tg[t0 + i];
-            const uint32_t ctrl = (g + G.lead + 127) / 128 - (g + 127) / 128;
-            to[t0 + i].g_in     = g;
-            to[t0 + i].out_off  = run;
-            run += G.fixed + ctrl;
-            g = G.has ? G.trail : g + G.lead;
+            const uint32_t i = c + lane;
+            TileGap        G{0, 0, 0, 0};
+            if (i < nt)
+                G = tg[t0 + i];
+            const GapFn    me  = i < nt ? GapFn{G.has, G.has ? G.trail : G.lead} : GapFn{0, 0};
+            const GapFn    inc = wave_scan_t<true>(me, fwd, shfl_gap);
+            GapFn          ex  = shfl_gap(inc, max(lane - 1, 0));
+            ex                 = lane == 0 ? carry : gap_then(carry, ex);
+            const uint32_t g    = ex.v;  // the recurrence starts from g = 0
+            const uint32_t cost = i < nt ? G.fixed + (g + G.lead + 127) / 128 - (g + 127) / 128 : 0u;
+            const uint32_t csum = wave_scan<true>(cost, 0u, OpAdd());
+            if (i < nt)
+            {
+                to[t0 + i].g_in    = g;
+                to[t0 + i].out_off = run + csum - cost;
+            }
+            run += __builtin_amdgcn_readlane(csum, 63);
+            carry = gap_then(carry, shfl_gap(inc, 63));
         }
-        rle_size[b]  = run;
-        uint32_t rem = 0;
-        for (int i = (int) nt - 1; i >= 0; --i)
+        if (lane == 0)
+            rle_size[b] = run;
+        // literals after each tile: rem -> has ? lead : len + rem, applied from the block end
+        GapFn rc{0, 0};
+        for (int c = (int) ((nt + 63) / 64) * 64 - 64; c >= 0; c -= 64)
         {
-            to[t0 + i].rem_after = rem;
-            const TileGap G      = tg[t0 + i];
-            rem                  = G.has ? G.lead : tiles[t0 + i].len + rem;
+            const uint32_t i = (uint32_t) c + lane;
+            GapFn          me{0, 0};
+            if (i < nt)
+            {
+                const TileGap G = tg[t0 + i];
+                me              = GapFn{G.has, G.has ? G.lead : tiles[t0 + i].len};
+            }
+            // composition in reverse: apply later tiles first
+            const auto  bwd = [](const GapFn& a, const GapFn& b) { return gap_then(b, a); };
+            const GapFn inc = wave_scan_t<false>(me, bwd, shfl_gap);
+            GapFn       ex  = shfl_gap(inc, min(lane + 1, 63));
+            ex              = lane == 63 ? rc : gap_then(rc, ex);
+            if (i < nt)
+                to[t0 + i].rem_after = ex.v;
+            rc = gap_then(rc, shfl_gap(inc, 0));
         }
     }
 }
@@ -438,7 +531,7 @@ bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_
     }
     {
         BRA_PROF(P_RLE_LINK, s);
-        hipLaunchKernelGGL(k_rle_link, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, runs, link);
+        hipLaunchKernelGGL(k_rle_link, dim3(std::min<uint32_t>(nblocks, 4096)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, runs, link);
     }
     {
         BRA_PROF(P_RLE_SIZES, s);
@@ -446,7 +539,7 @@ bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_
     }
     {
         BRA_PROF(P_RLE_OFFSETS, s);
-        hipLaunchKernelGGL(k_rle_offsets, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
+        hipLaunchKernelGGL(k_rle_offsets, dim3(std::min<uint32_t>(nblocks, 4096)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
                            w.tiling.d_pieces, gaps, offs, d_rle_size);
     }
     {
