@@ -137,21 +137,53 @@ __device__ __forceinline__ void wave_bitonic_sort4(uint64_t (&k)[4], uint32_t (&
 }
 
 // Inclusive max-scan over 256 elements (4 per lane) in element order.
+// ---- wave / workgroup scans on one dword per thread (DPP inside rows of 16, row totals by
+// readlane; no LDS inside a wave) ----
+struct OpMax
+{
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); }
+};
+struct OpMin
+{
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return min(a, b); }
+};
+struct OpAdd
+{
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+
+// Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order.
+template <bool FWD, typename Op>
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op)
+{
+    if (FWD)
+    {
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x111, 0xf, 0xf, false));  // row_shr:1
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x112, 0xf, 0xf, false));  // row_shr:2
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x114, 0xf, 0xf, false));  // row_shr:4
+        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x118, 0xf, 0xf, false));  // row_shr:8
+        const uint32_t t0 = __builtin_amdgcn_readlane(x, 15), t1 = __builtin_amdgcn_readlane(x, 31), t2 = __builtin_amdgcn_readlane(x, 47);
+        const uint32_t c1 = t0, c2 = op(t0, t1), c3 = op(c2, t2);
+        const uint32_t row = (uint32_t) lane_id() >> 4;
+        return op(x, row == 0 ? id : row == 1 ? c1 : row == 2 ? c2 : c3);
+    }
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x101, 0xf, 0xf, false));  // row_shl:1
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x102, 0xf, 0xf, false));  // row_shl:2
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x104, 0xf, 0xf, false));  // row_shl:4
+    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x108, 0xf, 0xf, false));  // row_shl:8
+    const uint32_t t1 = __builtin_amdgcn_readlane(x, 16), t2 = __builtin_amdgcn_readlane(x, 32), t3 = __builtin_amdgcn_readlane(x, 48);
+    const uint32_t c2 = t3, c1 = op(t2, t3), c0 = op(t1, c1);
+    const uint32_t row = (uint32_t) lane_id() >> 4;
+    return op(x, row == 3 ? id : row == 2 ? c2 : row == 1 ? c1 : c0);
+}
+
 __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
 {
-    x[1]         = max(x[1], x[0]);
-    x[2]         = max(x[2], x[1]);
-    x[3]         = max(x[3], x[2]);
-    uint32_t agg = x[3];
-    for (int d = 1; d < WAVE; d <<= 1)
-    {
-        uint32_t o = __shfl_up(agg, d, WAVE);
-        if (lane_id() >= d)
-            agg = max(agg, o);
-    }
-    uint32_t ex = __shfl_up(agg, 1, WAVE);
-    if (lane_id() == 0)
-        ex = 0;
+    x[1]              = max(x[1], x[0]);
+    x[2]              = max(x[2], x[1]);
+    x[3]              = max(x[3], x[2]);
+    const uint32_t in = wave_scan<true>(x[3], 0u, OpMax());
+    uint32_t       ex = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) in, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane 0: 0)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         x[r] = max(x[r], ex);
@@ -284,19 +316,11 @@ __device__ __forceinline__ void wave_excl_max4(const uint32_t (&x)[4], uint32_t 
 // Inclusive min-scan over 256 elements (4 per lane) in REVERSE element order.
 __device__ __forceinline__ void wave_min_rscan4(uint32_t (&x)[4])
 {
-    x[2]         = min(x[2], x[3]);
-    x[1]         = min(x[1], x[2]);
-    x[0]         = min(x[0], x[1]);
-    uint32_t agg = x[0];
-    for (int d = 1; d < WAVE; d <<= 1)
-    {
-        uint32_t o = __shfl_down(agg, d, WAVE);
-        if (lane_id() + d < WAVE)
-            agg = min(agg, o);
-    }
-    uint32_t ex = __shfl_down(agg, 1, WAVE);
-    if (lane_id() == WAVE - 1)
-        ex = 0xFFFFFFFFu;
+    x[2]              = min(x[2], x[3]);
+    x[1]              = min(x[1], x[2]);
+    x[0]              = min(x[0], x[1]);
+    const uint32_t in = wave_scan<false>(x[0], 0xFFFFFFFFu, OpMin());
+    const uint32_t ex = (uint32_t) __builtin_amdgcn_update_dpp(-1, (int) in, 0x130, 0xf, 0xf, false);  // wave_shl:1 (lane 63: ~0)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         x[r] = min(x[r], ex);

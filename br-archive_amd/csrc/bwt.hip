@@ -373,7 +373,10 @@ constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into
 // so every job holds < JOB_MAX elements), workgroup jobs (<= mjob_max), next-level buckets (with
 // their tiles) or fallback groups.  The four waves' list slots are reserved with one atomic per
 // list per workgroup (jobs and workgroup jobs share a 64-bit atomic, so do buckets and tiles).
-constexpr int SCAN_WAVES = 16;
+#ifndef BRA_SCAN_WAVES
+#define BRA_SCAN_WAVES 4   // 16 and 8 measured slower (waves of one workgroup wait for its largest bucket)
+#endif
+constexpr int SCAN_WAVES = BRA_SCAN_WAVES;  // buckets (waves) per scan workgroup
 
 struct ScanWaveCounts
 {
@@ -1172,14 +1175,8 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
         ex[r] = c;
         c += f[r] ? 1u : 0u;
     }
-    uint32_t x = c;
-    for (int d = 1; d < WAVE; d <<= 1)
-    {
-        const uint32_t o = __shfl_up(x, d, WAVE);
-        if (lane >= d)
-            x += o;
-    }
-    uint32_t wtot = __shfl(x, 63, WAVE), pre = x - c;
+    const uint32_t x    = wave_scan<true>(c, 0u, OpAdd());
+    uint32_t       wtot = __builtin_amdgcn_readlane(x, 63), pre = x - c;
     if (W > 1)
     {
         if (lane == 63)
@@ -1241,6 +1238,38 @@ __device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[4][4], uint64_t ke
     }
 }
 
+// Stage whose partners sit 16 or 32 lanes away (J = 64 or 128 slots): a permlane swap of the
+// registers of elements (0, 1) and of (2, 3) gathers each partner pair into ONE lane (element r0's
+// pair in the lower rows, r1's in the upper rows, the lower slot in the first register), an
+// in-lane compare-exchange orders it, and the same swap puts the elements back: 10 VALU per
+// element instead of 24 with per-dword partner fetches.
+template <int LM>
+__device__ __forceinline__ void net_stage_swap(uint32_t (&k)[4][4], uint64_t asc)
+{
+#pragma unroll
+    for (int q = 0; q < 4; q += 2)
+    {
+        uint32_t a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+        {
+            const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(k[i][q], k[i][q + 1], false, false)
+                                      : __builtin_amdgcn_permlane32_swap(k[i][q], k[i][q + 1], false, false);
+            a[i] = t[0];
+            b[i] = t[1];
+        }
+        cx128_pair(a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], asc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+        {
+            const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(a[i], b[i], false, false)
+                                      : __builtin_amdgcn_permlane32_swap(a[i], b[i], false, false);
+            k[i][q]     = t[0];
+            k[i][q + 1] = t[1];
+        }
+    }
+}
+
 // Stage (SIZE, J) of the bitonic network and, recursively, the rest of its merge phase.  All
 // stage parameters are compile-time, so a phase is straight-line code with the keys in fixed
 // registers (a runtime stage loop made the compiler copy every key between register sets at each
@@ -1265,6 +1294,10 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uin
             cx128(k[0][r], k[1][r], k[2][r], k[3][r], o.x, o.y, o.z, o.w, keep_min);
         }
     }
+#ifndef BRA_NO_SWAP_STAGES
+    else if constexpr (J == 64 || J == 128)
+        net_stage_swap<J / 4>(k, __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0));
+#endif
     else if constexpr (J >= 4)
     {
         const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));

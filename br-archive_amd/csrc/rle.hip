@@ -46,46 +46,6 @@ struct TileOff
     uint32_t g_in, out_off, rem_after, pad;
 };
 
-// ---- wave / workgroup scans on one dword per thread (DPP inside rows of 16, row totals by
-// readlane; no LDS inside a wave) ----
-struct OpMax
-{
-    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return max(a, b); }
-};
-struct OpMin
-{
-    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return min(a, b); }
-};
-struct OpAdd
-{
-    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
-};
-
-// Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order.
-template <bool FWD, typename Op>
-__device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op)
-{
-    if (FWD)
-    {
-        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x111, 0xf, 0xf, false));  // row_shr:1
-        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x112, 0xf, 0xf, false));  // row_shr:2
-        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x114, 0xf, 0xf, false));  // row_shr:4
-        x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x118, 0xf, 0xf, false));  // row_shr:8
-        const uint32_t t0 = __builtin_amdgcn_readlane(x, 15), t1 = __builtin_amdgcn_readlane(x, 31), t2 = __builtin_amdgcn_readlane(x, 47);
-        const uint32_t c1 = t0, c2 = op(t0, t1), c3 = op(c2, t2);
-        const uint32_t row = (uint32_t) lane_id() >> 4;
-        return op(x, row == 0 ? id : row == 1 ? c1 : row == 2 ? c2 : c3);
-    }
-    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x101, 0xf, 0xf, false));  // row_shl:1
-    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x102, 0xf, 0xf, false));  // row_shl:2
-    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x104, 0xf, 0xf, false));  // row_shl:4
-    x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x108, 0xf, 0xf, false));  // row_shl:8
-    const uint32_t t1 = __builtin_amdgcn_readlane(x, 16), t2 = __builtin_amdgcn_readlane(x, 32), t3 = __builtin_amdgcn_readlane(x, 48);
-    const uint32_t c2 = t3, c1 = op(t2, t3), c0 = op(t1, c1);
-    const uint32_t row = (uint32_t) lane_id() >> 4;
-    return op(x, row == 3 ? id : row == 2 ? c2 : row == 1 ? c1 : c0);
-}
-
 // Exclusive scan over the 256 threads of the workgroup (thread order FWD or reversed), seeded
 // with `seed` (the value before the first / after the last thread).  tmp: 4 dwords of LDS.  If
 // `total` is given it receives the inclusive total including the seed.
