@@ -52,7 +52,10 @@ namespace bra {
 
 namespace {
 
-constexpr int      TILE         = 4096;  // elements per tile (256 threads x 16)
+#ifndef BRA_TILE
+#define BRA_TILE 4096
+#endif
+constexpr int      TILE         = BRA_TILE;  // elements per MSD tile (256 threads x 16)
 constexpr int      TPB          = 256;
 constexpr int      PER_THREAD   = TILE / TPB;
 constexpr uint32_t JOB_MAX      = 256;  // elements one wave sorts in registers
@@ -208,7 +211,7 @@ __global__ void __launch_bounds__(TPB) k_l0_hist(const uint8_t* __restrict__ in,
         const BlockDesc B   = blocks[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
         const uint8_t*  p   = in + B.off + T.start;
-        if (cnt == TILE && (((uintptr_t) p) & 15) == 0)
+        if (PER_THREAD == 16 && cnt == TILE && (((uintptr_t) p) & 15) == 0)
         {
             const uint4    q    = reinterpret_cast<const uint4*>(p)[threadIdx.x];  // 16 bytes per thread
             const uint32_t w[4] = {q.x, q.y, q.z, q.w};

@@ -12,3 +12,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-f
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- $B > $O/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- $B > $O/write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS -d $O/sq1 -o run --output-format csv -- $B > $O/sq1.log 2>&1
+cd "$GRAFT_REPO_ROOT"
+for v in ${VARIANTS:-}; do
+  BRA_HIP_LIB=$PWD/br-archive_amd/build/variants/$v/libbra_hip.so timeout -k 10 200 python bench.py --steps 3 --warmup 1 --profile-all --no-cpu-baseline --no-secondary --no-check > $O/var_$v.json 2> $O/var_$v.err
+done
