@@ -1349,8 +1349,23 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
         k[2][r] = (uint32_t) kh[r];
         k[3][r] = (uint32_t) (kh[r] >> 32);
     }
+    // A wave whose slots all hold padding keys (all ones) skips the phases that stay inside the
+    // wave (SIZE <= 256: no barriers, no data from other waves); any order of equal keys is
+    // sorted.  Only workgroup jobs have such waves (the tail of a job whose length is not a power
+    // of two, or the waves beyond P in later rounds).
+    bool dead = false;
+    if (W > 1)
+    {
+        uint32_t a = ~0u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            a &= k[0][r] & k[1][r] & k[2][r] & k[3][r];
+        dead = __builtin_amdgcn_ballot_w64(a != ~0u) == 0;
+    }
     for (int size = 2; size <= P; size <<= 1)
     {
+        if (dead && size <= 256)
+            continue;
         switch (size)
         {
         case 2: net_phase<W, 2>(k, S, e0); break;

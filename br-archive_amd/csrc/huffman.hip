@@ -78,11 +78,12 @@ __global__ void __launch_bounds__(64) k_huff_build(const uint32_t* __restrict__ 
         uint32_t head = 0, len = 0;
         auto insert = [&](uint32_t id, uint32_t f) {
             // position = 0 if empty or head.f > f, else max(1, #entries with freq < f)
-            uint32_t lt = 0;
-            for (uint32_t j = lane; j < len; j += 64)
-                lt += S.list_f[head + j] < f;
-            for (int d = 32; d > 0; d >>= 1)
-                lt += __shfl_xor(lt, d, 64);
+            uint32_t lt = 0;  // wave-uniform: ballot popcounts, no cross-lane reduction through LDS
+            for (uint32_t j0 = 0; j0 < len; j0 += 64)
+            {
+                const uint32_t j = j0 + lane;
+                lt += (uint32_t) __builtin_popcountll(__builtin_amdgcn_ballot_w64(j < len && S.list_f[head + j] < f));
+            }
             uint32_t p;
             if (len == 0 || S.list_f[head] > f)
                 p = 0;
