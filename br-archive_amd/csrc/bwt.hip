@@ -67,6 +67,9 @@ constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
+#ifndef MJOB_MIN_WAVES
+#define MJOB_MIN_WAVES 1
+#endif
 #define JOB_MIN_WAVES 1                  // min waves per SIMD the job kernels are compiled for (1 = compiler choice; 6 and 8 measured slower)
 #endif
 
@@ -136,12 +139,13 @@ struct TileOrder
 {
     const TileDesc* desc;
     const uint32_t* xseg;
+    uint32_t        natural;  // desc is in tile order: workgroup w takes tiles w, w + grid, ...
 };
 
 // List position of a workgroup's i-th tile, or ~0u when its XCD's part is exhausted.
 __device__ __forceinline__ uint32_t tile_pos(const TileOrder& o, uint32_t i, uint32_t ntiles)
 {
-    if (!o.desc)
+    if (!o.desc || o.natural)
     {
         const uint32_t t = blockIdx.x + i * gridDim.x;
         return t < ntiles ? t : ~0u;
@@ -354,6 +358,7 @@ struct ScanArgs
     Bucket*         next;
     uint32_t        cap_next;
     uint32_t*       tile_bucket_next;  // tile -> bucket map of the next level
+    TileDesc*       tdesc_next;        // STRING: descriptors of the next level's tiles in tile order
     uint32_t        cap_tiles;
     Job*            jobs;
     uint32_t        cap_jobs;
@@ -661,6 +666,13 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                         a.next[slot] = Bucket{s0, tot[r], nd, kd, B.block, obuf, B.gdepth, t0};
                         for (uint32_t t = 0; t < ntl[r]; ++t)
                             a.tile_bucket_next[t0 + t] = slot;
+                        if (MODE == MODE_STRING)
+                        {
+                            const BlockDesc BD = a.blocks[B.block];
+                            for (uint32_t t = 0; t < ntl[r]; ++t)
+                                a.tdesc_next[t0 + t] = TileDesc{t0 + t, slot, s0 + t * TILE, min((uint32_t) TILE, tot[r] - t * TILE), nd,
+                                                                s0, tot[r], obuf, (uint32_t) BD.off, BD.len, kd, 0};
+                        }
                     }
                     else
                         atomicExch(&a.ctr->overflow, 1u);
@@ -1296,6 +1308,16 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uin
             const uint4 o = X[(e0 + r) ^ J];
             cx128(k[0][r], k[1][r], k[2][r], k[3][r], o.x, o.y, o.z, o.w, keep_min);
         }
+        if constexpr (J == 256)
+        {
+            // the rest of the phase stays inside the wave: a wave left with padding only skips it
+            uint32_t a = ~0u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                a &= k[0][r] & k[1][r] & k[2][r] & k[3][r];
+            if (__builtin_amdgcn_ballot_w64(a != ~0u) == 0)
+                return;
+        }
     }
 #ifndef BRA_NO_SWAP_STAGES
     else if constexpr (J == 64 || J == 128)
@@ -1720,7 +1742,7 @@ __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
 }
 
 template <uint32_t MODE, int W>
-__global__ void __launch_bounds__(64 * W, JOB_MIN_WAVES) k_mjobs(JobArgs a)
+__global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     JobLds<W>&     S   = *reinterpret_cast<JobLds<W>*>(smem);
@@ -2120,6 +2142,7 @@ struct BwtWorkspace
     uint32_t* h_job_cnt      = nullptr;  // pinned: counts back, cursors out
     uint32_t* tile_cnt       = nullptr;  // MSD tile order: key counts, cursors, xseg[9]
     TileDesc* tile_order     = nullptr;
+    TileDesc* tdesc[2]       = {nullptr, nullptr};  // STRING: tile-order descriptors written by the scan (per level, ping-pong)
     Group*    groups[2]      = {nullptr, nullptr};
     Counters* ctr            = nullptr;
     Counters* h_ctr          = nullptr;  // pinned
@@ -2130,6 +2153,7 @@ struct BwtWorkspace
     uint32_t  jobs_grid = 8192;         // workgroups of the wave-job launch (env BRA_JOBS_GRID)
     uint32_t* jobq      = nullptr;      // per-XCD claim counters of the three job launches (3 x 8 x 32 dwords)
     int       jobq_on   = 1;            // dynamic job order (env BRA_JOBQ=0: static strides)
+    int       tile_order_mode = 1;      // MSD tile order: 0 scan order, 1 XCD-major on re-gather levels, 2 always (env BRA_TILE_ORDER)
     uint32_t  jobq_chunk = 2;           // wave jobs claimed at once (env BRA_JOBQ_CH)
     uint32_t  nblocks   = 0;            // blocks of the current call
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
@@ -2244,6 +2268,8 @@ static void ws_free(BwtWorkspace& w)
     (void) hipFree(w.job_cnt);
     (void) hipFree(w.tile_cnt);
     (void) hipFree(w.tile_order);
+    (void) hipFree(w.tdesc[0]);
+    (void) hipFree(w.tdesc[1]);
     (void) hipHostFree(w.h_job_cnt);
     (void) hipFree(w.mjobs);
     (void) hipFree(w.ctr);
@@ -2278,6 +2304,8 @@ static void ws_env(BwtWorkspace& w)
         g_mjobs_grid = std::max(8, atoi(e));
     if (const char* e = getenv("BRA_JOBQ"))
         w.jobq_on = atoi(e) != 0;
+    if (const char* e = getenv("BRA_TILE_ORDER"))
+        w.tile_order_mode = atoi(e);
     if (const char* e = getenv("BRA_JOBQ_CH"))
         w.jobq_chunk = (uint32_t) std::max(1, atoi(e));
 }
@@ -2322,6 +2350,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     BRA_HIP_CHECK(hipMalloc(&w.job_cnt, 8 * nkeys * 4));
     BRA_HIP_CHECK(hipMalloc(&w.tile_cnt, (2 * nkeys + 16) * 4));
     BRA_HIP_CHECK(hipMalloc(&w.tile_order, (size_t) w.cap_tiles * sizeof(TileDesc)));
+    BRA_HIP_CHECK(hipMalloc(&w.tdesc[0], (size_t) w.cap_tiles * sizeof(TileDesc)));
+    BRA_HIP_CHECK(hipMalloc(&w.tdesc[1], (size_t) w.cap_tiles * sizeof(TileDesc)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
     BRA_HIP_CHECK(hipMalloc(&w.jobq, 3 * 8 * 32 * 4));
@@ -2362,11 +2392,20 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
     uint32_t nelems = w.h_ctr->n_elems_next;
     const size_t lds  = tile_stage_bytes();
     const int    grid = w.grid;
+    // STRING levels start at depth 1 with payloads carrying digits [1, 1 + CARRY); a level whose
+    // scatter re-gathers digits (once per CARRY levels) lists its tiles XCD-major and block-major
+    // (the gathers then stay in the XCD's L2); the other levels only stream payloads and take the
+    // scan's tile-order descriptors as they are (no ordering kernels).
+    uint32_t lvl_d = 1, lvl_kd = 1;
     while (nbig > 0)
     {
         hipLaunchKernelGGL(k_level_start, dim3(1), dim3(1), 0, s, w.ctr); BRA_DSYNC(s);
-        TileOrder to{nullptr, nullptr};
-        if (MODE == MODE_STRING)
+        TileOrder  to{nullptr, nullptr, 0};
+        const bool rg      = lvl_d + 1 - lvl_kd >= CARRY;
+        const bool ordered = w.tile_order_mode == 2 || (w.tile_order_mode == 1 && rg);
+        if (MODE == MODE_STRING && !ordered)
+            to = TileOrder{w.tdesc[cur], nullptr, 1};
+        else if (MODE == MODE_STRING)
         {
             // XCD-major, block-major tile list (the scatter's digit gathers stay in the XCD's L2)
             const uint32_t kb0 = div_up(w.nblocks, 8), q = div_up(kb0, 1024u), kb = div_up(kb0, q), nk = 8 * kb;
@@ -2378,7 +2417,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             hipLaunchKernelGGL(k_tile_scatter, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cur_, d_blocks,
                                w.tile_order);
             BRA_DSYNC(s);
-            to = TileOrder{w.tile_order, xs};
+            to = TileOrder{w.tile_order, xs, 0};
         }
         {
             BRA_PROF(P_BWT_HIST, s);
@@ -2386,7 +2425,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                                w.pay[1], w.tile_hist, ntiles, to); BRA_DSYNC(s);
         }
         ScanArgs a{d_blocks, w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
-                   w.cap_big,   w.tile_bucket[cur ^ 1],   w.cap_tiles, w.jobs,       w.cap_jobs,
+                   w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
                    w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
                    (uint32_t) (g_prof != nullptr), w.mjob_max()};
         {
@@ -2417,6 +2456,9 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         nbig   = w.h_ctr->n_big;
         ntiles = w.h_ctr->n_tiles_next;
         cur ^= 1;
+        if (rg)
+            lvl_kd = lvl_d + 1;
+        ++lvl_d;
     }
     return true;
 }
@@ -2496,7 +2538,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist); BRA_DSYNC(s);
     }
     ScanArgs a0{d_blocks, w.big[1],  nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
-                w.tile_bucket[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
+                w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max()};
     {
         BRA_PROF(P_BWT_SCAN, s);
