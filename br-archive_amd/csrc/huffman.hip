@@ -267,6 +267,26 @@ __global__ void __launch_bounds__(TPB) k_huff_offsets(const HuffMetaRec* __restr
 }
 
 // tiles over the RLE-output CAPACITY of each block; a tile beyond the block's RLE size is empty
+// The 16 symbols [i0, i0 + 16) of a tile (one 16-byte load when the tile is full and aligned;
+// symbols at or beyond cnt read as 0).
+__device__ __forceinline__ void load_syms(const uint8_t* __restrict__ p, uint32_t cnt, uint32_t i0, uint8_t (&sym)[16])
+{
+    if (i0 + 16 <= cnt && (((uintptr_t) (p + i0)) & 15) == 0)
+    {
+        const uint4    v    = *reinterpret_cast<const uint4*>(p + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            sym[k] = (uint8_t) (w[k >> 2] >> (8 * (k & 3)));
+    }
+    else
+    {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            sym[k] = (i0 + k < cnt) ? p[i0 + k] : 0;
+    }
+}
+
 __global__ void __launch_bounds__(TPB) k_huff_tilebits(const uint8_t* __restrict__ rle, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                        const HuffMetaRec* __restrict__ meta, uint32_t* __restrict__ tbits)
 {
@@ -280,8 +300,11 @@ __global__ void __launch_bounds__(TPB) k_huff_tilebits(const uint8_t* __restrict
         __syncthreads();
         const uint32_t cnt = P.start < rs ? min(P.len, rs - P.start) : 0;
         uint32_t       acc = 0;
-        for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
-            acc += L[rle[P.off + i]];
+        uint8_t        sym[16];
+        load_syms(rle + P.off, cnt, threadIdx.x * 16, sym);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            acc += (threadIdx.x * 16 + k < cnt) ? L[sym[k]] : 0u;
         uint32_t total;
         block256_exclusive_sum(acc, tmp, &total);
         if (threadIdx.x == 0)
@@ -371,15 +394,14 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
                 img[i] = 0;
         __syncthreads();
         // this thread's contiguous symbols
+        static_assert(PT == 16, "16 symbols per thread");
         const uint32_t i0 = threadIdx.x * PT;
         uint8_t        sym[PT];
         uint32_t       mybits = 0;
+        load_syms(rle + P.off, cnt, i0, sym);
 #pragma unroll
         for (int k = 0; k < PT; ++k)
-        {
-            sym[k] = (i0 + k < cnt) ? rle[P.off + i0 + k] : 0;
             mybits += (i0 + k < cnt) ? L[sym[k]] : 0;
-        }
         if (!lds)
         {
             // global path (codes > 32 bits make the tile image too large for LDS): the words strictly
@@ -390,21 +412,66 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
         }
         const uint32_t ex  = block256_exclusive_sum(mybits, tmp);  // (contains __syncthreads)
         uint64_t       pos = lds ? (uint64_t) sh + ex : g0 + ex;
-        uint32_t*      dst = lds ? img : out_words;
-#pragma unroll
-        for (int k = 0; k < PT; ++k)
+        if (lds)
         {
-            if (i0 + k >= cnt)
-                break;
-            uint32_t       nb = L[sym[k]];
-            const uint32_t c  = C[sym[k]];
-            if (nb > 32)
+            // the thread's bits are contiguous: gather them in a 64-bit register and store whole
+            // words; only the first and the last word can be shared with a neighbour (atomicOr)
+            uint32_t word = (uint32_t) (pos >> 5), nacc = (uint32_t) (pos & 31);
+            uint64_t acc   = 0;  // pending bits, MSB-first from bit 63; the first nacc are the neighbour's
+            bool     first = true;
+            const auto flush = [&]() {
+                while (nacc >= 32)
+                {
+                    const uint32_t v = (uint32_t) (acc >> 32);
+                    if (first)
+                    {
+                        if (v)
+                            atomicOr(&img[word], v);
+                        first = false;
+                    }
+                    else
+                        img[word] = v;
+                    acc <<= 32;
+                    nacc -= 32;
+                    ++word;
+                }
+            };
+#pragma unroll
+            for (int k = 0; k < PT; ++k)
             {
-                pos += nb - 32;  // leading zero bits of a wrapped long code
-                nb = 32;
+                if (i0 + k >= cnt)
+                    break;
+                uint32_t nb = L[sym[k]];
+                if (nb > 32)
+                {
+                    nacc += nb - 32;  // leading zero bits of a wrapped long code
+                    flush();
+                    nb = 32;
+                }
+                acc |= ((uint64_t) C[sym[k]] << (64 - nb)) >> nacc;
+                nacc += nb;
+                flush();
             }
-            or_bits(dst, pos, c, nb, !lds);
-            pos += nb;
+            if (nacc && (uint32_t) (acc >> 32))
+                atomicOr(&img[word], (uint32_t) (acc >> 32));
+        }
+        else
+        {
+#pragma unroll
+            for (int k = 0; k < PT; ++k)
+            {
+                if (i0 + k >= cnt)
+                    break;
+                uint32_t       nb = L[sym[k]];
+                const uint32_t c  = C[sym[k]];
+                if (nb > 32)
+                {
+                    pos += nb - 32;  // leading zero bits of a wrapped long code
+                    nb = 32;
+                }
+                or_bits(out_words, pos, c, nb, true);
+                pos += nb;
+            }
         }
         __syncthreads();
         if (lds)
