@@ -64,6 +64,11 @@ constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket go
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
 #ifndef JOB_MIN_WAVES
+constexpr uint32_t CSTRIDE    = 256 + 16;  // digit-counter copies (TileStagePN, k_hist): 16 banks apart
+#ifndef BRA_SCATTER_NC
+#define BRA_SCATTER_NC 4
+#endif
+constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
@@ -255,6 +260,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
                                               uint32_t* __restrict__ tile_hist, uint32_t ntiles, TileOrder to)
 {
     __shared__ uint32_t h[256];
+    __shared__ uint32_t hc[SCATTER_NC * CSTRIDE];  // per-copy counters (copy = lane & (NC - 1), see TileStagePN)
     if (MODE == MODE_STRING && BRA_HIST_PIPE)
     {
         // software-pipelined over the workgroup's tiles: the next tile's descriptor and payloads
@@ -284,16 +290,23 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
             TileDesc       Dn{};
             uint32_t       wn[PER_THREAD];
             load(pn, Dn, wn);
-            h[threadIdx.x] = 0;
+#pragma unroll
+            for (int c = 0; c < SCATTER_NC; ++c)
+                hc[c * CSTRIDE + threadIdx.x] = 0;
             __syncthreads();
             const uint32_t j  = D.d - D.kd;
             const uint32_t sh = j < 4 ? 24 - 8 * j : 24;
+            const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
 #pragma unroll
             for (int i = 0; i < PER_THREAD; ++i)
                 if (threadIdx.x + i * TPB < D.cnt)
-                    atomicAdd(&h[(w[i] >> sh) & 0xFFu], 1u);
+                    atomicAdd(&hc[cp + ((w[i] >> sh) & 0xFFu)], 1u);
             __syncthreads();
-            tile_hist[(size_t) D.t * 256 + threadIdx.x] = h[threadIdx.x];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int c = 0; c < SCATTER_NC; ++c)
+                tot += hc[c * CSTRIDE + threadIdx.x];
+            tile_hist[(size_t) D.t * 256 + threadIdx.x] = tot;
             p = pn;
             D = Dn;
 #pragma unroll
@@ -705,40 +718,70 @@ struct TileStage
     uint32_t tmp[8];
 };
 
-// STRING-mode tile staging: 64-bit payloads (index + carried digits).
-struct TileStageP
+// STRING-mode tile staging: 64-bit payloads (index + carried digits).  The digit counters come in
+// NC copies (copy = lane & (NC - 1)) CSTRIDE words apart, so that lanes of one instruction with
+// the same digit hit NC different counters in different banks (same-address LDS atomics
+// serialise; skewed digits are the norm for text).
+template <int NC>
+struct TileStagePN
 {
     uint64_t pay[TILE];
-    uint32_t cnt[256];
-    uint32_t base[256];
-    uint32_t goff[256];  // sub-bucket slot of the tile's first element per digit (bit 31: next-level bucket)
+    uint32_t cnt[NC * CSTRIDE];  // per copy: count, then the copy's first staging slot per digit
+    uint32_t base[256];          // first staging slot per digit
+    uint32_t goff[256];          // sub-bucket slot of the tile's first element per digit (bit 31: next-level bucket)
     uint32_t tmp[8];
 };
+using TileStageP = TileStagePN<1>;
+using TileStageS = TileStagePN<SCATTER_NC>;
 constexpr uint32_t NEXT_FLAG = 0x80000000u;
 
-// Ranks the tile's elements by digit in LDS and stages them in digit order; returns nothing, the
-// caller reads S.pay[q] back in order (coalesced output runs per digit).
-template <typename V>
-__device__ __forceinline__ void stage_p(TileStageP& S, const V (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
+template <int NC>
+__device__ __forceinline__ void stage_zero(TileStagePN<NC>& S)
 {
-    uint32_t rank[PER_THREAD];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+        S.cnt[c * CSTRIDE + threadIdx.x] = 0;
+}
+
+// Ranks the tile's elements by digit in LDS and stages them in digit order; the caller reads
+// S.pay[q] back in order (coalesced output runs per digit) and finds a staged element's digit
+// offset as q - S.base[digit].
+template <int NC, typename V>
+__device__ __forceinline__ void stage_p(TileStagePN<NC>& S, const V (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
+{
+    const uint32_t cp = (NC > 1) ? (uint32_t) (lane_id() & (NC - 1)) * CSTRIDE : 0u;
+    uint32_t       rank[PER_THREAD];
 #pragma unroll
     for (int i = 0; i < PER_THREAD; ++i)
     {
         const uint32_t e = threadIdx.x + i * TPB;
         if (e < cnt)
-            rank[i] = atomicAdd(&S.cnt[dgt[i]], 1u);
+            rank[i] = atomicAdd(&S.cnt[cp + dgt[i]], 1u);
     }
     __syncthreads();
-    const uint32_t c    = S.cnt[threadIdx.x];
-    S.base[threadIdx.x] = block256_exclusive_sum(c, S.tmp);
+    uint32_t c[NC], tot = 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+    {
+        c[k] = S.cnt[k * CSTRIDE + threadIdx.x];
+        tot += c[k];
+    }
+    const uint32_t b    = block256_exclusive_sum(tot, S.tmp);
+    S.base[threadIdx.x] = b;
+    uint32_t run        = b;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+    {
+        S.cnt[k * CSTRIDE + threadIdx.x] = run;
+        run += c[k];
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PER_THREAD; ++i)
     {
         const uint32_t e = threadIdx.x + i * TPB;
         if (e < cnt)
-            S.pay[S.base[dgt[i]] + rank[i]] = v[i];
+            S.pay[S.cnt[cp + dgt[i]] + rank[i]] = v[i];
     }
     __syncthreads();
 }
@@ -868,7 +911,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                                                    uint64_t* __restrict__ pay1, uint32_t ntiles, TileOrder to)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStageP& S = *reinterpret_cast<TileStageP*>(smem);
+    TileStageS& S = *reinterpret_cast<TileStageS*>(smem);
     for (uint32_t it = 0;; ++it)
     {
         const uint32_t p = tile_pos(to, it, ntiles);
@@ -920,7 +963,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
             continue;
         }
         uint64_t* op        = B.buf ? pay0 : pay1;
-        S.cnt[threadIdx.x]  = 0;
+        stage_zero(S);
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x];
         __syncthreads();
         uint64_t v[PER_THREAD];
@@ -2435,7 +2478,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         {
             BRA_PROF(P_BWT_SCATTER, s);
             if (MODE == MODE_STRING)
-                hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageP), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
+                hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
                                    ntiles, to);
             else
                 hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,

@@ -313,17 +313,24 @@ __global__ void __launch_bounds__(TPB) k_huff_tilebits(const uint8_t* __restrict
     }
 }
 
-__global__ void k_huff_tilescan(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
-                                const uint64_t* __restrict__ payload_off, uint32_t* __restrict__ tbits, uint64_t* __restrict__ tbit0)
+// One wave per block: exclusive scan of the tiles' bit counts (64 tiles per step).
+__global__ void __launch_bounds__(64) k_huff_tilescan(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
+                                                      const uint64_t* __restrict__ payload_off, uint32_t* __restrict__ tbits,
+                                                      uint64_t* __restrict__ tbit0)
 {
-    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    const int lane = lane_id();
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
-        uint64_t run = payload_off[b] * 8;
-        for (uint32_t i = 0; i < count[b]; ++i)
+        uint64_t       run = payload_off[b] * 8;
+        const uint32_t t0 = first[b], nt = count[b];
+        for (uint32_t c = 0; c < nt; c += 64)
         {
-            const uint32_t t = first[b] + i;
-            tbit0[t]         = run;
-            run += tbits[t];
+            const uint32_t i   = c + lane;
+            const uint32_t v   = i < nt ? tbits[t0 + i] : 0u;
+            const uint32_t inc = wave_scan<true>(v, 0u, OpAdd());  // a tile holds < 2^27 bits: 64 of them fit 32 bits
+            if (i < nt)
+                tbit0[t0 + i] = run + inc - v;
+            run += __builtin_amdgcn_readlane(inc, 63);
         }
     }
 }
@@ -1010,7 +1017,7 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
     }
     {
         BRA_PROF(P_HUF_TILESCAN, s);
-        hipLaunchKernelGGL(k_huff_tilescan, dim3(div_up(nblocks, 64)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
+        hipLaunchKernelGGL(k_huff_tilescan, dim3(std::min<uint32_t>(nblocks, 4096)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
                            d_payload_off, w.tbits, w.tbit0);
     }
     BRA_HIP_CHECK(hipMemcpyAsync(h_total, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s));
