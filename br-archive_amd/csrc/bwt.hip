@@ -211,11 +211,14 @@ struct L0Tile
 __global__ void __launch_bounds__(TPB) k_l0_hist(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
                                                  const L0Tile* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ tile_hist)
 {
-    __shared__ uint32_t h[256];
+    __shared__ uint32_t h[SCATTER_NC * CSTRIDE];  // counter copies, see TileStagePN
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
-        h[threadIdx.x] = 0;
+#pragma unroll
+        for (int c = 0; c < SCATTER_NC; ++c)
+            h[c * CSTRIDE + threadIdx.x] = 0;
         __syncthreads();
+        const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
         const L0Tile    T   = tiles[t];
         const BlockDesc B   = blocks[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
@@ -226,13 +229,17 @@ __global__ void __launch_bounds__(TPB) k_l0_hist(const uint8_t* __restrict__ in,
             const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-                atomicAdd(&h[(w[i >> 2] >> (8 * (i & 3))) & 0xFF], 1u);
+                atomicAdd(&h[cp + ((w[i >> 2] >> (8 * (i & 3))) & 0xFF)], 1u);
         }
         else
             for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
-                atomicAdd(&h[p[i]], 1u);
+                atomicAdd(&h[cp + p[i]], 1u);
         __syncthreads();
-        tile_hist[(size_t) t * 256 + threadIdx.x] = h[threadIdx.x];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int c = 0; c < SCATTER_NC; ++c)
+            tot += h[c * CSTRIDE + threadIdx.x];
+        tile_hist[(size_t) t * 256 + threadIdx.x] = tot;
         __syncthreads();
     }
 }
@@ -733,6 +740,10 @@ struct TileStagePN
 };
 using TileStageP = TileStagePN<1>;
 using TileStageS = TileStagePN<SCATTER_NC>;
+#ifndef BRA_L0_NC
+#define BRA_L0_NC 4
+#endif
+using TileStageL0 = TileStagePN<BRA_L0_NC>;  // level 0 (plus the input window: 4 copies cost one workgroup per CU)
 constexpr uint32_t NEXT_FLAG = 0x80000000u;
 
 template <int NC>
@@ -840,8 +851,8 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStageP& S   = *reinterpret_cast<TileStageP*>(smem);
-    uint8_t*    win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageP));  // TILE + 32 bytes, 16-aligned
+    TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
+    uint8_t*     win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageL0));  // TILE + 32 bytes, 16-aligned
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile    T   = tiles[t];
@@ -866,7 +877,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                 win[i + 15] = blk[q];
             }
         }
-        S.cnt[threadIdx.x]  = 0;
+        stage_zero(S);
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x] & ~NEXT_FLAG;
         __syncthreads();
         uint32_t v[PER_THREAD], dg[PER_THREAD];
@@ -2552,7 +2563,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageP) + TILE + 48)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageL0) + TILE + 48)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
@@ -2589,7 +2600,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
-        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageP) + TILE + 48, s, d_in, d_blocks,
+        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageL0) + TILE + 48, s, d_in, d_blocks,
                            w.l0tiles, nt0, w.tile_off, w.key[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
