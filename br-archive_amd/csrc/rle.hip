@@ -437,13 +437,16 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
 {
     __shared__ uint32_t tmp[8];
     __shared__ uint8_t  stage[RLE_TILE + RLE_TILE / 64 + 64];
-    __shared__ uint32_t h[256];
+    constexpr int       HC = 4, HS = 256 + 16;  // histogram copies (lane & 3), 16 banks apart: output bytes are skewed
+    __shared__ uint32_t h[HC * HS];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const Piece    P = tiles[t];
         const TileOff  O = to[t];
         const TileLink K = link[t];
-        h[threadIdx.x]   = 0;
+#pragma unroll
+        for (int c = 0; c < HC; ++c)
+            h[c * HS + threadIdx.x] = 0;
         TileThread T;
         tile_load(in, P, T);
         uint32_t nl, rs, clen[PT];
@@ -455,16 +458,21 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
         const uint32_t pos = block256_exclusive_sum(by, tmp, &total);
         tile_emit<true>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, stage, pos);
         __syncthreads();
-        uint8_t* dst = out + rle_base[P.block] + O.out_off;
+        uint8_t*       dst = out + rle_base[P.block] + O.out_off;
+        const uint32_t cp  = (uint32_t) (lane_id() & (HC - 1)) * HS;
         for (uint32_t i = threadIdx.x; i < total; i += TPB)
         {
             const uint8_t c = stage[i];
             dst[i]          = c;
-            atomicAdd(&h[c], 1u);
+            atomicAdd(&h[cp + c], 1u);
         }
         __syncthreads();
-        if (h[threadIdx.x])
-            atomicAdd(&hist[(size_t) P.block * 256 + threadIdx.x], h[threadIdx.x]);
+        uint32_t hv = 0;
+#pragma unroll
+        for (int c = 0; c < HC; ++c)
+            hv += h[c * HS + threadIdx.x];
+        if (hv)
+            atomicAdd(&hist[(size_t) P.block * 256 + threadIdx.x], hv);
         __syncthreads();
     }
 }
