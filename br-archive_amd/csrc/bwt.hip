@@ -63,7 +63,6 @@ constexpr int      MJ_WAVES_DEF = 4;    // waves of a workgroup job (2, 4, 8 or 
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
-#ifndef JOB_MIN_WAVES
 constexpr uint32_t CSTRIDE    = 256 + 16;  // digit-counter copies (TileStagePN, k_hist): 16 banks apart
 #ifndef BRA_SCATTER_NC
 #define BRA_SCATTER_NC 4
@@ -72,10 +71,13 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
+// min waves per SIMD the job kernels are compiled for (1 = compiler choice: 6 for the wave jobs,
+// 5 for the workgroup jobs today; forcing 6 on the workgroup jobs spilled and measured no faster)
 #ifndef MJOB_MIN_WAVES
 #define MJOB_MIN_WAVES 1
 #endif
-#define JOB_MIN_WAVES 1                  // min waves per SIMD the job kernels are compiled for (1 = compiler choice; 6 and 8 measured slower)
+#ifndef JOB_MIN_WAVES
+#define JOB_MIN_WAVES 1
 #endif
 
 enum : uint32_t { MODE_STRING = 0, MODE_RANK = 1 };
