@@ -137,7 +137,7 @@ struct TileDesc
     uint32_t boff;    // block offset in the batch / block length
     uint32_t nlen;
     uint32_t kd;      // the payloads carry digits [kd, kd + CARRY)
-    uint32_t pad;
+    uint32_t pdig;    // 1: the bucket stayed in place, its digits are read from the payloads (not dig[])
 };
 
 // Ordered tile list of a level: XCD x's part is [xseg[x], xseg[x + 1]) (workgroup w works on
@@ -170,6 +170,7 @@ constexpr uint32_t CARRY = 5;
 __device__ __forceinline__ uint32_t p_idx(uint64_t P) { return (uint32_t) P & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t p_digit(uint64_t P, uint32_t j) { return (uint32_t) (P >> (56 - 8 * j)) & 0xFFu; }
 typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
+typedef uint4 __attribute__((aligned(1))) uint4_u;
 // payload carrying bytes [st, st + CARRY) (cyclic) of a block of n bytes
 __device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ blk, uint32_t n, uint32_t st, uint32_t idx)
 {
@@ -266,7 +267,8 @@ template <uint32_t MODE>
 __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
                                               const uint64_t* __restrict__ key0, const uint64_t* __restrict__ key1,
                                               const uint32_t* __restrict__ pay0, const uint32_t* __restrict__ pay1,
-                                              uint32_t* __restrict__ tile_hist, uint32_t ntiles, TileOrder to)
+                                              uint32_t* __restrict__ tile_hist, uint32_t ntiles, TileOrder to,
+                                              const uint8_t* __restrict__ dig0, const uint8_t* __restrict__ dig1)
 {
     __shared__ uint32_t h[256];
     __shared__ uint32_t hc[SCATTER_NC * CSTRIDE];  // per-copy counters (copy = lane & (NC - 1), see TileStagePN)
@@ -274,22 +276,34 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
     {
         // software-pipelined over the workgroup's tiles: the next tile's descriptor and payloads
         // are loaded before the current tile's LDS histogram is built
-        // Only the payload dword holding the digit is loaded (p_digit: digits 0-3 in the high
-        // dword, digit 4 in bits 24-31 of the low one).
+        // STRING digits come from the byte array the previous scatter wrote beside the payloads
+        // (dig[buf][slot] = the element's digit at this level): 16 contiguous digits per thread.
         uint32_t p = tile_pos(to, 0, ntiles);
         TileDesc D{};
-        uint32_t w[PER_THREAD];
-        const auto load = [&](uint32_t pp, TileDesc& DD, uint32_t (&ww)[PER_THREAD]) {
+        uint4    w;
+        const auto load = [&](uint32_t pp, TileDesc& DD, uint4& ww) {
             if (pp == ~0u)
                 return;
-            DD                  = to.desc[pp];
-            const uint32_t  jj  = DD.d - DD.kd;
-            const uint32_t* pay = reinterpret_cast<const uint32_t*>((DD.buf ? key1 : key0) + DD.s0) + (jj < 4 ? 1 : 0);
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
+            DD               = to.desc[pp];
+            const uint8_t* g = (DD.buf ? dig1 : dig0) + DD.s0 + threadIdx.x * 16;
+            if (DD.pdig)
             {
-                const uint32_t e = threadIdx.x + i * TPB;
-                ww[i]            = e < DD.cnt ? pay[2 * e] : 0u;
+                // digits still in the payloads (the bucket did not move at the previous level)
+                const uint64_t* pay = (DD.buf ? key1 : key0) + DD.s0 + threadIdx.x * 16;
+                const uint32_t  jj  = DD.d - DD.kd;
+                uint32_t        x[4] = {0, 0, 0, 0};
+                for (uint32_t i = 0; threadIdx.x * 16 + i < DD.cnt && i < 16; ++i)
+                    x[i >> 2] |= p_digit(pay[i], jj) << (8 * (i & 3));
+                ww = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+            else if (threadIdx.x * 16 + 16 <= DD.cnt)
+                ww = *reinterpret_cast<const uint4_u*>(g);
+            else
+            {
+                uint32_t x[4] = {0, 0, 0, 0};
+                for (uint32_t i = 0; threadIdx.x * 16 + i < DD.cnt && i < 16; ++i)
+                    x[i >> 2] |= (uint32_t) g[i] << (8 * (i & 3));
+                ww = make_uint4(x[0], x[1], x[2], x[3]);
             }
         };
         load(p, D, w);
@@ -297,19 +311,18 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
         {
             const uint32_t pn = tile_pos(to, it, ntiles);
             TileDesc       Dn{};
-            uint32_t       wn[PER_THREAD];
+            uint4          wn;
             load(pn, Dn, wn);
 #pragma unroll
             for (int c = 0; c < SCATTER_NC; ++c)
                 hc[c * CSTRIDE + threadIdx.x] = 0;
             __syncthreads();
-            const uint32_t j  = D.d - D.kd;
-            const uint32_t sh = j < 4 ? 24 - 8 * j : 24;
-            const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
+            const uint32_t cp   = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
+            const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-                if (threadIdx.x + i * TPB < D.cnt)
-                    atomicAdd(&hc[cp + ((w[i] >> sh) & 0xFFu)], 1u);
+            for (int i = 0; i < 16; ++i)
+                if (threadIdx.x * 16 + i < D.cnt)
+                    atomicAdd(&hc[cp + ((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
             __syncthreads();
             uint32_t tot = 0;
 #pragma unroll
@@ -318,9 +331,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
             tile_hist[(size_t) D.t * 256 + threadIdx.x] = tot;
             p = pn;
             D = Dn;
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-                w[i] = wn[i];
+            w = wn;
         }
         return;
     }
@@ -693,7 +704,8 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                             const BlockDesc BD = a.blocks[B.block];
                             for (uint32_t t = 0; t < ntl[r]; ++t)
                                 a.tdesc_next[t0 + t] = TileDesc{t0 + t, slot, s0 + t * TILE, min((uint32_t) TILE, tot[r] - t * TILE), nd,
-                                                                s0, tot[r], obuf, (uint32_t) BD.off, BD.len, kd, 0};
+                                                                s0, tot[r], obuf, (uint32_t) BD.off, BD.len, kd,
+                                                                (nomove && !regather) ? 1u : 0u};
                         }
                     }
                     else
@@ -850,7 +862,8 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
 // Level 0: every element gets its payload carrying rotation bytes 1..CARRY (the next digits).
 __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
                                                     const L0Tile* __restrict__ tiles, uint32_t ntiles,
-                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay)
+                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay,
+                                                    uint8_t* __restrict__ odig)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
@@ -907,7 +920,10 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                 const uint32_t  lo = __builtin_amdgcn_alignbyte(a1, a0, sh), hi = __builtin_amdgcn_alignbyte(a2, a1, sh);
                 const uint64_t  kk = __builtin_bswap64(((uint64_t) hi << 32) | lo);
                 if (BRA_DCHECK(slot >= B.off && slot < B.off + B.len, "l0 scatter slot %u outside block %u", slot, T.block))
+                {
                     opay[slot] = ((kk << 8) & 0xFFFFFFFFFF000000ull) | (T.start + e);
+                    odig[slot] = (uint8_t) (kk >> 48);  // rotation byte 1: the level-1 digit
+                }
             }
         }
         __syncthreads();
@@ -921,7 +937,8 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
 // payloads are re-gathered in place.
 __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ pay0,
-                                                   uint64_t* __restrict__ pay1, uint32_t ntiles, TileOrder to)
+                                                   uint64_t* __restrict__ pay1, uint32_t ntiles, TileOrder to, uint8_t* __restrict__ dig0,
+                                                   uint8_t* __restrict__ dig1)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageS& S = *reinterpret_cast<TileStageS*>(smem);
@@ -933,7 +950,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
         const TileDesc D  = to.desc[p];
         const uint32_t nm = nomove[D.bi];
         if (nm == 1)
-            continue;  // uniform per workgroup
+            continue;  // uniform per workgroup: the bucket stays as it is (the next level reads its digits from the payloads)
         const uint32_t t   = D.t;
         const uint8_t* blk = in + D.boff;
         const uint32_t cnt = D.cnt;
@@ -950,6 +967,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
         const uint32_t  dn = (B.d + 1) % BD.len;      // their first digit's depth
         const size_t    s0 = D.s0;
         uint64_t*       ip = (B.buf ? pay1 : pay0) + s0;
+        uint8_t*        id = (B.buf ? dig1 : dig0) + s0;
         if (nm == 2)
         {
             uint64_t v[PER_THREAD];
@@ -970,12 +988,15 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                     uint32_t       st  = idx + dn;
                     if (st >= BD.len)
                         st -= BD.len;
-                    ip[e] = p_make(blk, BD.len, st, idx);
+                    const uint64_t np = p_make(blk, BD.len, st, idx);
+                    ip[e]             = np;
+                    id[e]             = (uint8_t) p_digit(np, 0);
                 }
             }
             continue;
         }
         uint64_t* op        = B.buf ? pay0 : pay1;
+        uint8_t*  od        = B.buf ? dig0 : dig1;
         stage_zero(S);
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x];
         __syncthreads();
@@ -1010,7 +1031,11 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                     nv = p_make(blk, BD.len, st, idx);
                 }
                 if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
+                {
                     op[slot] = nv;
+                    if (g & NEXT_FLAG)  // the next level's digit, for its histogram
+                        od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));
+                }
             }
         }
         __syncthreads();
@@ -1274,7 +1299,6 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
 // 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian.  A non-wrapping read is
 // one 16-byte load at the byte address (gfx950 global loads need no alignment; one L2 request
 // unless it straddles a line, where two aligned loads always made two).
-typedef uint4 __attribute__((aligned(1))) uint4_u;
 
 __device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint32_t n, uint32_t start, uint64_t& w0, uint64_t& w1)
 {
@@ -1965,7 +1989,8 @@ __global__ void __launch_bounds__(256) k_tile_prefix(const uint32_t* __restrict_
 
 __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket, uint32_t n,
                                                       uint32_t kb, uint32_t q, uint32_t nkeys, uint32_t* __restrict__ cursor,
-                                                      const BlockDesc* __restrict__ blocks, TileDesc* __restrict__ order)
+                                                      const BlockDesc* __restrict__ blocks, const TileDesc* __restrict__ nat,
+                                                      TileDesc* __restrict__ order)
 {
     extern __shared__ uint32_t h[];
     constexpr int PT = JOB_CHUNK / 256;
@@ -2001,7 +2026,8 @@ __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__
                 const BlockDesc BD = blocks[B.block];
                 const uint32_t  f  = (j - B.tile0) * TILE;
                 order[h[key[i]] + rank[i]] =
-                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, (uint32_t) BD.off, BD.len, B.kd, 0};
+                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, (uint32_t) BD.off, BD.len, B.kd,
+                             nat[j].pdig};
             }
         }
         __syncthreads();
@@ -2198,7 +2224,8 @@ struct BwtWorkspace
     uint32_t* h_job_cnt      = nullptr;  // pinned: counts back, cursors out
     uint32_t* tile_cnt       = nullptr;  // MSD tile order: key counts, cursors, xseg[9]
     TileDesc* tile_order     = nullptr;
-    TileDesc* tdesc[2]       = {nullptr, nullptr};  // STRING: tile-order descriptors written by the scan (per level, ping-pong)
+    TileDesc* tdesc[2]       = {nullptr, nullptr};
+    uint8_t*  dig[2]         = {nullptr, nullptr};  // STRING: digit of the current level beside each payload of key[b]  // STRING: tile-order descriptors written by the scan (per level, ping-pong)
     Group*    groups[2]      = {nullptr, nullptr};
     Counters* ctr            = nullptr;
     Counters* h_ctr          = nullptr;  // pinned
@@ -2325,6 +2352,8 @@ static void ws_free(BwtWorkspace& w)
     (void) hipFree(w.tile_cnt);
     (void) hipFree(w.tile_order);
     (void) hipFree(w.tdesc[0]);
+    (void) hipFree(w.dig[0]);
+    (void) hipFree(w.dig[1]);
     (void) hipFree(w.tdesc[1]);
     (void) hipHostFree(w.h_job_cnt);
     (void) hipFree(w.mjobs);
@@ -2407,6 +2436,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     BRA_HIP_CHECK(hipMalloc(&w.tile_cnt, (2 * nkeys + 16) * 4));
     BRA_HIP_CHECK(hipMalloc(&w.tile_order, (size_t) w.cap_tiles * sizeof(TileDesc)));
     BRA_HIP_CHECK(hipMalloc(&w.tdesc[0], (size_t) w.cap_tiles * sizeof(TileDesc)));
+    BRA_HIP_CHECK(hipMalloc(&w.dig[0], N + 16));
+    BRA_HIP_CHECK(hipMalloc(&w.dig[1], N + 16));
     BRA_HIP_CHECK(hipMalloc(&w.tdesc[1], (size_t) w.cap_tiles * sizeof(TileDesc)));
     BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault));
     BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
@@ -2471,14 +2502,14 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             hipLaunchKernelGGL(k_tile_count, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cnt); BRA_DSYNC(s);
             hipLaunchKernelGGL(k_tile_prefix, dim3(1), dim3(256), 0, s, cnt, nk, kb, cur_, xs); BRA_DSYNC(s);
             hipLaunchKernelGGL(k_tile_scatter, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cur_, d_blocks,
-                               w.tile_order);
+                               w.tdesc[cur], w.tile_order);
             BRA_DSYNC(s);
             to = TileOrder{w.tile_order, xs, 0};
         }
         {
             BRA_PROF(P_BWT_HIST, s);
             hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
-                               w.pay[1], w.tile_hist, ntiles, to); BRA_DSYNC(s);
+                               w.pay[1], w.tile_hist, ntiles, to, w.dig[0], w.dig[1]); BRA_DSYNC(s);
         }
         ScanArgs a{d_blocks, w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
                    w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
@@ -2492,7 +2523,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             BRA_PROF(P_BWT_SCATTER, s);
             if (MODE == MODE_STRING)
                 hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
-                                   ntiles, to);
+                                   ntiles, to, w.dig[0], w.dig[1]);
             else
                 hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
                                    w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles);
@@ -2603,7 +2634,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
         hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageL0) + TILE + 48, s, d_in, d_blocks,
-                           w.l0tiles, nt0, w.tile_off, w.key[0]); BRA_DSYNC(s);
+                           w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     if (!read_ctr(w, s))
