@@ -743,10 +743,10 @@ struct TileStage
 // NC copies (copy = lane & (NC - 1)) CSTRIDE words apart, so that lanes of one instruction with
 // the same digit hit NC different counters in different banks (same-address LDS atomics
 // serialise; skewed digits are the norm for text).
-template <int NC>
+template <int NC, typename PAY = uint64_t>
 struct TileStagePN
 {
-    uint64_t pay[TILE];
+    PAY      pay[TILE];
     uint32_t cnt[NC * CSTRIDE];  // per copy: count, then the copy's first staging slot per digit
     uint32_t base[256];          // first staging slot per digit
     uint32_t goff[256];          // sub-bucket slot of the tile's first element per digit (bit 31: next-level bucket)
@@ -757,11 +757,11 @@ using TileStageS = TileStagePN<SCATTER_NC>;
 #ifndef BRA_L0_NC
 #define BRA_L0_NC 4
 #endif
-using TileStageL0 = TileStagePN<BRA_L0_NC>;  // level 0 (plus the input window: 4 copies cost one workgroup per CU)
+using TileStageL0 = TileStagePN<BRA_L0_NC, uint32_t>;  // level 0 stages 32-bit (digit << 24 | position) values  // level 0 (plus the input window: 4 copies cost one workgroup per CU)
 constexpr uint32_t NEXT_FLAG = 0x80000000u;
 
-template <int NC>
-__device__ __forceinline__ void stage_zero(TileStagePN<NC>& S)
+template <int NC, typename PAY>
+__device__ __forceinline__ void stage_zero(TileStagePN<NC, PAY>& S)
 {
 #pragma unroll
     for (int c = 0; c < NC; ++c)
@@ -771,8 +771,8 @@ __device__ __forceinline__ void stage_zero(TileStagePN<NC>& S)
 // Ranks the tile's elements by digit in LDS and stages them in digit order; the caller reads
 // S.pay[q] back in order (coalesced output runs per digit) and finds a staged element's digit
 // offset as q - S.base[digit].
-template <int NC, typename V>
-__device__ __forceinline__ void stage_p(TileStagePN<NC>& S, const V (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
+template <int NC, typename PAY, typename V>
+__device__ __forceinline__ void stage_p(TileStagePN<NC, PAY>& S, const V (&v)[PER_THREAD], const uint32_t (&dgt)[PER_THREAD], uint32_t cnt)
 {
     const uint32_t cp = (NC > 1) ? (uint32_t) (lane_id() & (NC - 1)) * CSTRIDE : 0u;
     uint32_t       rank[PER_THREAD];
