@@ -183,7 +183,10 @@ __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
     x[2]              = max(x[2], x[1]);
     x[3]              = max(x[3], x[2]);
     const uint32_t in = wave_scan<true>(x[3], 0u, OpMax());
-    uint32_t       ex = (uint32_t) __builtin_amdgcn_update_dpp(0, (int) in, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane 0: 0)
+    // previous lane's value (DPP wave shifts do not cross rows on gfx950: ds_bpermute)
+    uint32_t       ex = (uint32_t) __shfl_up((int) in, 1, WAVE);
+    if (lane_id() == 0)
+        ex = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         x[r] = max(x[r], ex);
@@ -283,15 +286,9 @@ __device__ __forceinline__ uint64_t xlane64(uint64_t x)
 __device__ __forceinline__ void wave_excl_sum4(const uint32_t (&x)[4], uint32_t (&ex)[4], uint32_t* total = nullptr)
 {
     const uint32_t l1 = x[0], l2 = l1 + x[1], l3 = l2 + x[2], l4 = l3 + x[3];
-    uint32_t       agg = l4;
-    for (int d = 1; d < WAVE; d <<= 1)
-    {
-        const uint32_t o = __shfl_up(agg, d, WAVE);
-        if (lane_id() >= d)
-            agg += o;
-    }
+    const uint32_t agg = wave_scan<true>(l4, 0u, OpAdd());
     if (total)
-        *total = __shfl(agg, WAVE - 1, WAVE);
+        *total = __builtin_amdgcn_readlane(agg, WAVE - 1);
     const uint32_t pre = agg - l4;
     ex[0]              = pre;
     ex[1]              = pre + l1;
@@ -304,13 +301,13 @@ __device__ __forceinline__ void wave_excl_max4(const uint32_t (&x)[4], uint32_t 
 {
     uint32_t inc[4] = {x[0], x[1], x[2], x[3]};
     wave_max_scan4(inc);
-    uint32_t prev = __shfl_up(inc[3], 1, WAVE);
+    uint32_t       prev = (uint32_t) __shfl_up((int) inc[3], 1, WAVE);
     if (lane_id() == 0)
         prev = 0;
-    ex[0] = prev;
-    ex[1] = inc[0];
-    ex[2] = inc[1];
-    ex[3] = inc[2];
+    ex[0]               = prev;
+    ex[1]               = inc[0];
+    ex[2]               = inc[1];
+    ex[3]               = inc[2];
 }
 
 // Inclusive min-scan over 256 elements (4 per lane) in REVERSE element order.
@@ -320,7 +317,9 @@ __device__ __forceinline__ void wave_min_rscan4(uint32_t (&x)[4])
     x[1]              = min(x[1], x[2]);
     x[0]              = min(x[0], x[1]);
     const uint32_t in = wave_scan<false>(x[0], 0xFFFFFFFFu, OpMin());
-    const uint32_t ex = (uint32_t) __builtin_amdgcn_update_dpp(-1, (int) in, 0x130, 0xf, 0xf, false);  // wave_shl:1 (lane 63: ~0)
+    uint32_t       ex = (uint32_t) __shfl_down((int) in, 1, WAVE);  // next lane's value (ds_bpermute, see wave_max_scan4)
+    if (lane_id() == WAVE - 1)
+        ex = 0xFFFFFFFFu;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         x[r] = min(x[r], ex);
@@ -329,14 +328,8 @@ __device__ __forceinline__ void wave_min_rscan4(uint32_t (&x)[4])
 // Block-wide exclusive sum over 256 threads (one value per thread).  `tmp` >= 8 words of LDS.
 __device__ __forceinline__ uint32_t block256_exclusive_sum(uint32_t v, uint32_t* tmp, uint32_t* total = nullptr)
 {
-    const int lane = lane_id(), w = threadIdx.x >> 6;
-    uint32_t  x    = v;
-    for (int d = 1; d < WAVE; d <<= 1)
-    {
-        uint32_t o = __shfl_up(x, d, WAVE);
-        if (lane >= d)
-            x += o;
-    }
+    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t x    = wave_scan<true>(v, 0u, OpAdd());
     if (lane == WAVE - 1)
         tmp[w] = x;
     __syncthreads();
