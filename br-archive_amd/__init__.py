@@ -34,7 +34,7 @@ ABI_SYMBOLS = (
     "bra_rle_encode", "bra_rle_decode_compute_size", "bra_rle_decode",
     "bra_huffman_encode", "bra_huffman_decode", "bra_huffman_chunk_free",
     "bra_gpu_ctx_create", "bra_gpu_ctx_destroy", "bra_gpu_num_blocks", "bra_gpu_payload_bound",
-    "bra_gpu_encode_blocks", "bra_gpu_decode_blocks", "bra_gpu_stage_ptr", "bra_gpu_version",
+    "bra_gpu_encode_blocks", "bra_gpu_decode_blocks", "bra_gpu_stage_ptr", "bra_gpu_version", "bra_gpu_selftest",
     "bra_gpu_prof_enable", "bra_gpu_prof_reset", "bra_gpu_prof_read",
     "bra_gpu_crc32c", "bra_gpu_chunks_crc32c", "bra_gpu_crc32c_combine", "bra_gpu_entry_crc32c", "bra_gpu_chunks_bound",
     "bra_gpu_frame_chunks", "bra_gpu_unframe_chunks", "bra_gpu_compress_chunks", "bra_gpu_decompress_chunks",
@@ -124,6 +124,8 @@ def _load() -> C.CDLL:
     lib.bra_gpu_prof_read.restype = C.c_int
     lib.bra_gpu_version.argtypes = []
     lib.bra_gpu_version.restype = C.c_char_p
+    lib.bra_gpu_selftest.argtypes = []
+    lib.bra_gpu_selftest.restype = C.c_int
     u64p = C.POINTER(C.c_uint64)
     lib.bra_gpu_crc32c.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp]
     lib.bra_gpu_crc32c.restype = C.c_int

@@ -210,6 +210,13 @@ int  bra_gpu_prof_read(bra_gpu_ctx_t* ctx, int slot, const char** name, double* 
 /* Library identification for the loader tests. */
 const char* bra_gpu_version(void);
 
+/*
+ * Device self-test of the wave / workgroup scan primitives the kernels are built from (lane
+ * exchanges through DPP, readlane and ds_bpermute): 0 = all match a serial restatement, > 0 =
+ * number of mismatches, < 0 = HIP error.  Diagnostics only; no codec state is touched.
+ */
+int bra_gpu_selftest(void);
+
 #ifdef __cplusplus
 }
 #endif

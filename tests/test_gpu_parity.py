@@ -28,6 +28,12 @@ def codec(bra):
 
 
 # ---- reference known answers (test/test_bra_encoders.cpp) through the single-block C-ABI ----------
+def test_device_scan_primitives(bra):
+    """The lane-exchange scans every kernel is built from, against a serial restatement on the device
+    (a wrong lane shift can stay invisible in codec outputs: it only adds refinement rounds)."""
+    assert bra.lib.bra_gpu_selftest() == 0
+
+
 def test_kat_bwt(bra):
     assert bra.bwt_encode(b"BANANA") == (b"NNBAAA", 3)
     fox = b"The quick brown fox jumps over the lazy dog."
