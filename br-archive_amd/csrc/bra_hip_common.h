@@ -153,9 +153,14 @@ struct OpAdd
 };
 
 // Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order.
+// Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order; with `ex`,
+// also the exclusive value (the scan of the lanes before this one in scan order, id for the first).
+// DPP row shifts inside rows of 16 lanes, row totals by readlane (DPP wave shifts do not cross
+// rows on gfx950).
 template <bool FWD, typename Op>
-__device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op)
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op, uint32_t* ex = nullptr)
 {
+    const uint32_t row = (uint32_t) lane_id() >> 4;
     if (FWD)
     {
         x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x111, 0xf, 0xf, false));  // row_shr:1
@@ -164,8 +169,10 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op)
         x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x118, 0xf, 0xf, false));  // row_shr:8
         const uint32_t t0 = __builtin_amdgcn_readlane(x, 15), t1 = __builtin_amdgcn_readlane(x, 31), t2 = __builtin_amdgcn_readlane(x, 47);
         const uint32_t c1 = t0, c2 = op(t0, t1), c3 = op(c2, t2);
-        const uint32_t row = (uint32_t) lane_id() >> 4;
-        return op(x, row == 0 ? id : row == 1 ? c1 : row == 2 ? c2 : c3);
+        const uint32_t carry = row == 0 ? id : row == 1 ? c1 : row == 2 ? c2 : c3;
+        if (ex)
+            *ex = op(carry, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x111, 0xf, 0xf, false));
+        return op(x, carry);
     }
     x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x101, 0xf, 0xf, false));  // row_shl:1
     x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x102, 0xf, 0xf, false));  // row_shl:2
@@ -173,8 +180,10 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x, uint32_t id, Op op)
     x = op(x, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x108, 0xf, 0xf, false));  // row_shl:8
     const uint32_t t1 = __builtin_amdgcn_readlane(x, 16), t2 = __builtin_amdgcn_readlane(x, 32), t3 = __builtin_amdgcn_readlane(x, 48);
     const uint32_t c2 = t3, c1 = op(t2, t3), c0 = op(t1, c1);
-    const uint32_t row = (uint32_t) lane_id() >> 4;
-    return op(x, row == 3 ? id : row == 2 ? c2 : row == 1 ? c1 : c0);
+    const uint32_t carry = row == 3 ? id : row == 2 ? c2 : row == 1 ? c1 : c0;
+    if (ex)
+        *ex = op(carry, (uint32_t) __builtin_amdgcn_update_dpp((int) id, (int) x, 0x101, 0xf, 0xf, false));
+    return op(x, carry);
 }
 
 __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
@@ -182,11 +191,8 @@ __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
     x[1]              = max(x[1], x[0]);
     x[2]              = max(x[2], x[1]);
     x[3]              = max(x[3], x[2]);
-    const uint32_t in = wave_scan<true>(x[3], 0u, OpMax());
-    // previous lane's value (DPP wave shifts do not cross rows on gfx950: ds_bpermute)
-    uint32_t       ex = (uint32_t) __shfl_up((int) in, 1, WAVE);
-    if (lane_id() == 0)
-        ex = 0;
+    uint32_t ex;
+    wave_scan<true>(x[3], 0u, OpMax(), &ex);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         x[r] = max(x[r], ex);
@@ -300,11 +306,15 @@ __device__ __forceinline__ void wave_excl_sum4(const uint32_t (&x)[4], uint32_t 
 __device__ __forceinline__ void wave_excl_max4(const uint32_t (&x)[4], uint32_t (&ex)[4])
 {
     uint32_t inc[4] = {x[0], x[1], x[2], x[3]};
-    wave_max_scan4(inc);
-    uint32_t       prev = (uint32_t) __shfl_up((int) inc[3], 1, WAVE);
-    if (lane_id() == 0)
-        prev = 0;
-    ex[0]               = prev;
+    inc[1]          = max(inc[1], inc[0]);
+    inc[2]          = max(inc[2], inc[1]);
+    inc[3]          = max(inc[3], inc[2]);
+    uint32_t prev;
+    wave_scan<true>(inc[3], 0u, OpMax(), &prev);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        inc[r] = max(inc[r], prev);
+    ex[0] = prev;
     ex[1]               = inc[0];
     ex[2]               = inc[1];
     ex[3]               = inc[2];
@@ -316,10 +326,8 @@ __device__ __forceinline__ void wave_min_rscan4(uint32_t (&x)[4])
     x[2]              = min(x[2], x[3]);
     x[1]              = min(x[1], x[2]);
     x[0]              = min(x[0], x[1]);
-    const uint32_t in = wave_scan<false>(x[0], 0xFFFFFFFFu, OpMin());
-    uint32_t       ex = (uint32_t) __shfl_down((int) in, 1, WAVE);  // next lane's value (ds_bpermute, see wave_max_scan4)
-    if (lane_id() == WAVE - 1)
-        ex = 0xFFFFFFFFu;
+    uint32_t ex;
+    wave_scan<false>(x[0], 0xFFFFFFFFu, OpMin(), &ex);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
         x[r] = min(x[r], ex);

@@ -53,13 +53,10 @@ template <bool FWD, typename Op>
 __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t seed, uint32_t id, Op op, uint32_t* tmp, uint32_t* total = nullptr)
 {
     const int      lane = lane_id(), w = threadIdx.x >> 6;
-    const uint32_t inc  = wave_scan<FWD>(v, id, op);
+    uint32_t       ex;  // scan of the lanes before this one in scan order (id at the wave's first lane)
+    const uint32_t inc = wave_scan<FWD>(v, id, op, &ex);
     if (lane == (FWD ? 63 : 0))
         tmp[w] = inc;
-    // value of the neighbour lane before this one in scan order (id at the wave's first lane)
-    uint32_t ex = FWD ? (uint32_t) __shfl_up((int) inc, 1, 64) : (uint32_t) __shfl_down((int) inc, 1, 64);
-    if (lane == (FWD ? 0 : 63))
-        ex = id;
     __syncthreads();
     uint32_t pre = seed, all = seed;
 #pragma unroll
