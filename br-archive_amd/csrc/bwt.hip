@@ -71,13 +71,14 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
-// min waves per SIMD the job kernels are compiled for (1 = compiler choice: 6 for the wave jobs,
-// 5 for the workgroup jobs today; forcing 6 on the workgroup jobs spilled and measured no faster)
+// min waves per SIMD the job kernels are compiled for (wave jobs: 6, i.e. <= 80 VGPRs, 8 bytes of
+// spill, faster than the compiler's 84 VGPRs at 5; workgroup jobs: compiler choice, 5 -- forcing 6
+// spilled and measured no faster)
 #ifndef MJOB_MIN_WAVES
 #define MJOB_MIN_WAVES 1
 #endif
 #ifndef JOB_MIN_WAVES
-#define JOB_MIN_WAVES 1
+#define JOB_MIN_WAVES 6
 #endif
 
 enum : uint32_t { MODE_STRING = 0, MODE_RANK = 1 };
@@ -1501,35 +1502,53 @@ __device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64
 {
     constexpr uint32_t SLOTS = 256 * W;
     const int          lane  = lane_id();
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
+    // previous slot's key: the lane's own element r - 1, the previous lane's element 3 (ds_bpermute),
+    // or (lane 0 of waves > 0) the previous wave's last element through LDS
+    uint64_t ph = (uint64_t) __shfl_up((long long) kh[3], 1, WAVE), pm = (uint64_t) __shfl_up((long long) km[3], 1, WAVE);
+    if (W > 1)
     {
-        const uint32_t c = wj * 256 + lane * 4 + r;
-        S.kh[c]          = kh[r];
-        S.kl[c]          = km[r];
+        if (lane == 63)
+        {
+            S.kh[wj * 256 + 255] = kh[3];
+            S.kl[wj * 256 + 255] = km[3];
+        }
+        job_sync<W>();
+        if (lane == 0 && wj > 0)
+        {
+            ph = S.kh[wj * 256 - 1];
+            pm = S.kl[wj * 256 - 1];
+        }
     }
-    job_sync<W>();
     uint32_t x[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         const uint32_t c  = wj * 256 + lane * 4 + r;
-        const bool     hd = (c == 0) || c >= T || S.kh[c - 1] != kh[r] || S.kl[c - 1] != km[r];
+        const uint64_t qh = r ? kh[r - 1] : ph, qm = r ? km[r - 1] : pm;
+        const bool     hd = (c == 0) || c >= T || qh != kh[r] || qm != km[r];
         g[r]              = hd ? c : 0;
         x[r]              = hd ? c : 0xFFFFFFFFu;
     }
     job_max_scan<W>(g, S, wj);
     job_min_rscan<W>(x, S, wj);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        S.nx[wj * 256 + lane * 4 + r] = x[r];
-    job_sync<W>();
+    // next slot's x: own element r + 1, the next lane's element 0, or the next wave's first
+    uint32_t nx3 = (uint32_t) __shfl_down((int) x[0], 1, WAVE);
+    if (lane == 63)
+        nx3 = 0xFFFFFFFFu;
+    if (W > 1)
+    {
+        if (lane == 0)
+            S.nx[wj * 256] = x[0];
+        job_sync<W>();
+        if (lane == 63 && wj + 1 < W)
+            nx3 = S.nx[(wj + 1) * 256];
+    }
     bool any = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         const uint32_t c   = wj * 256 + lane * 4 + r;
-        const uint32_t nh  = (c + 1 < SLOTS) ? S.nx[c + 1] : 0xFFFFFFFFu;
+        const uint32_t nh  = (c + 1 < SLOTS) ? (r < 3 ? x[r + 1] : nx3) : 0xFFFFFFFFu;
         const uint32_t end = min(nh == 0xFFFFFFFFu ? SLOTS : nh, T);
         gend[r]            = end;
         tied[r]            = c < T && (end - g[r]) >= 2;
