@@ -2328,7 +2328,7 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, con
 
 static uint32_t round8(uint32_t g) { return (g + 7u) & ~7u; }
 
-static uint32_t g_mjobs_grid = 2048;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID)
+static uint32_t g_mjobs_grid = 4096;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID; 2048 left the 2-wave jobs short of full occupancy)
 
 template <uint32_t MODE>
 static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
