@@ -389,7 +389,7 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     int32_t* st = reinterpret_cast<int32_t*>(w.state);
     {
         BRA_PROF(P_MTF_LASTOCC, s);
-        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(nseg, 8192)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
+        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(nseg, 65536)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
     }
     {
         BRA_PROF(P_MTF_SCAN, s);
