@@ -2252,7 +2252,9 @@ struct BwtWorkspace
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
     int       grid = 16384;  // workgroups of the MSD / level-0 tile kernels (env BRA_GRID; 2048: 11.9, 8192: 12.3, 16384: 12.5 GB/s)
     int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
-    uint32_t  jobs_grid = 8192;         // workgroups of the wave-job launch (env BRA_JOBS_GRID)
+    uint32_t  jobs_grid = 2048;         // workgroups of the wave-job launch (env BRA_JOBS_GRID): about the resident
+                                        // capacity (6 waves/SIMD = 1536 four-wave groups); with the dynamic job
+                                        // queues extra groups only cost launch overhead (8192: 2.94 ms, 2048: 2.67)
     uint32_t* jobq      = nullptr;      // per-XCD claim counters of the three job launches (3 x 8 x 32 dwords)
     int       jobq_on   = 1;            // dynamic job order (env BRA_JOBQ=0: static strides)
     int       tile_order_mode = 1;      // MSD tile order: 0 scan order, 1 XCD-major on re-gather levels, 2 always (env BRA_TILE_ORDER)
@@ -2328,12 +2330,14 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, con
 
 static uint32_t round8(uint32_t g) { return (g + 7u) & ~7u; }
 
-static uint32_t g_mjobs_grid = 4096;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID; 2048 left the 2-wave jobs short of full occupancy)
+static uint32_t g_mjobs_grid = 0;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID; 0 = by size class)
 
 template <uint32_t MODE>
 static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
 {
-    const dim3 g(round8(std::min<uint32_t>(n, g_mjobs_grid)));
+    // about the resident capacity: 2-wave jobs fit twice as many groups per CU as 4-wave ones
+    const uint32_t cap = g_mjobs_grid ? g_mjobs_grid : (waves <= 2 ? 3072u : 1536u);
+    const dim3     g(round8(std::min<uint32_t>(n, cap)));
     if (waves == 16)
         hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>) + 16, s, a);
     else if (waves == 8)
