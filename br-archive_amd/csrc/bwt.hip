@@ -418,7 +418,10 @@ constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into
 #ifndef BRA_SCAN_WAVES
 #define BRA_SCAN_WAVES 4   // 16 and 8 measured slower (waves of one workgroup wait for its largest bucket)
 #endif
-constexpr int SCAN_WAVES = BRA_SCAN_WAVES;  // buckets (waves) per scan workgroup
+constexpr int SCAN_WAVES = BRA_SCAN_WAVES;
+#ifndef BRA_SCAN_MIN_WAVES
+#define BRA_SCAN_MIN_WAVES 1  // min waves per SIMD the scan is compiled for (1: compiler choice, 143 VGPRs)
+#endif  // buckets (waves) per scan workgroup
 
 struct ScanWaveCounts
 {
@@ -426,7 +429,7 @@ struct ScanWaveCounts
 };
 
 template <uint32_t MODE>
-__global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
+__global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(ScanArgs a)
 {
     __shared__ uint32_t       key_s[SCAN_WAVES][256];
     __shared__ uint32_t       jlen_s[SCAN_WAVES][256];
