@@ -1,21 +1,31 @@
 #!/usr/bin/env python3
 """bench.py -- br-archive block codec on MI355X: encode GB/s of input bytes (BASELINE.json metric).
 
-One step = one pass of the hot path (BWT -> MTF -> PackBits RLE -> canonical Huffman, the chunk
-encoder of lib_bra_io_file_chunks.c:217-245) over one batch of synthetic blocks that is already
-resident in HBM: BASELINE configs[1], 256 x 1 MiB "enwik-style" text blocks per GPU.  With N > 1
-GPUs (torchrun, one process per GPU, RCCL) every rank encodes its own 256 MiB (weak scaling) and the
-compressed chunks are gathered to rank 0 over xGMI inside the step (SURVEY 8.1 row e).
+One step = one pass of the hot path over one batch of synthetic blocks already resident in HBM:
+every block goes through BWT -> MTF -> PackBits RLE -> canonical Huffman (the chunk encoder of
+lib_bra_io_file_chunks.c:217-245), the chunk-stream CRC32C is computed (:248-249) and the compressed
+chunks are assembled in global block order on rank 0 (SURVEY 8.1 rows d, e, f2).
 
-Printed (rank 0, one JSON line): the metric, `roofline` for the dominant kernel (algorithmic bytes
-per launch / average launch time measured with HIP events on the codec's stream during the timed
-steps), and `cpu_baseline`: the reference's own src/encoders (oracle/_ref/libbraref.so, compiled
-from the reference sources) timed on this host on a bounded sample of the same blocks.
+Sharding (SURVEY 8.1 row e, BASELINE configs[3]): global block b is encoded by rank b mod G (round
+robin); with G > 1 the compressed chunks and CRC shares are gathered to rank 0 over RCCL/xGMI inside
+the step.  Weak scaling (default): every rank holds --bytes-per-gpu (256 MiB = configs[1] per GPU; at
+G = 8 this is configs[3]'s 2 GiB).  Strong scaling: --total-bytes fixes the global input (2 GiB for
+configs[3] at any G); a rank then encodes its share in batches of at most --batch-bytes.
+
+`python bench.py --gpus N` with N > 1 and no torchrun environment starts torchrun itself (a child
+process launched before anything touches the GPU) and relays its output and exit code.
+
+Printed (rank 0, one JSON line): the metric, `roofline` for the dominant kernel (algorithmic bytes per
+launch / average launch time measured with HIP events on the codec's stream during the timed steps),
+and `cpu_baseline`: the reference's own src/encoders (oracle/_ref/libbraref.so, compiled from the
+reference sources) timed on this host, single-threaded and on all the cores this box gives us.
 """
 import argparse
 import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,6 +35,14 @@ sys.path.insert(0, ROOT)
 METRIC = "encode GB/s (input bytes) on 256 MiB synthetic blocks, 1/2/4/8 GPU; bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 KINDS = {"text": 0, "random": 1, "sym16": 2, "tiled": 3}
+# the BASELINE.json config each input kind is quoted on
+WORKLOADS = {
+    "text": "BASELINE configs[1]: 1 MiB enwik-style synthetic text blocks (Zipf word stream)",
+    "random": "BASELINE configs[2]: uniform-random bytes",
+    "sym16": "BASELINE configs[4]: 16-symbol geometric low-entropy blocks",
+    "tiled": "BASELINE configs[0] input: test/test.txt (19 B) tiled",
+}
+CPU_SHARE = 16  # host CPUs per GPU on the box (os.cpu_count() reports the whole machine)
 
 
 def parse():
@@ -34,46 +52,85 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kind", default="text", choices=sorted(KINDS))
     ap.add_argument("--block-size", type=int, default=1 << 20)
-    ap.add_argument("--bytes-per-gpu", type=int, default=256 << 20)
-    ap.add_argument("--cpu-blocks", type=int, default=32, help="blocks in the CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--bytes-per-gpu", type=int, default=256 << 20, help="weak scaling: input bytes per rank")
+    ap.add_argument("--total-bytes", type=int, default=0, help="strong scaling: global input bytes (e.g. 2147483648)")
+    ap.add_argument("--batch-bytes", type=int, default=256 << 20, help="largest batch one encode call takes")
+    ap.add_argument("--cpu-threads", type=int, default=CPU_SHARE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--profile-all", action="store_true", help="time every kernel during the timed steps")
-    ap.add_argument("--no-secondary", action="store_true", help="skip the PCIe-inclusive encode measurement")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the decode and PCIe-inclusive measurements")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     return ap.parse_args()
 
 
-def cpu_baseline(data_np, bs, nblocks, threads, gpu_chunks):
-    """Reference encoders on host cores: one block per task, `threads` workers (ctypes drops the GIL)."""
+def spawn_torchrun(args) -> int:
+    """Relaunch this script under torchrun with one rank per GPU; no GPU call has happened yet."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_sample_sizes(nb, bs, threads):
+    """Blocks timed single-threaded (about 4 MiB) and on `threads` workers (about 2 MiB per thread):
+    10-30 s of reference CPU work for 1 MiB text or random blocks."""
+    return max(1, min(nb, (4 << 20) // bs)), max(1, min(nb, threads * max(1, (2 << 20) // bs)))
+
+
+def cpu_baseline(data_np, bs, threads, gpu_chunks):
+    """The reference encoders on host cores (one block per task; ctypes drops the GIL), on a bounded
+    sample of the benchmark's own blocks: single-threaded, then `threads` workers."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import Oracle, Reference, have_ref
 
     impl, kind = (Reference(), "reference") if have_ref() else (Oracle(), "port")
-    nblocks = min(nblocks, data_np.size // bs)
-    blocks = [data_np[i * bs:(i + 1) * bs].tobytes() for i in range(nblocks)]
-    threads = max(1, min(threads, nblocks))
+    n1, nm = cpu_sample_sizes(data_np.size // bs, bs, threads)
+    blocks = [data_np[i * bs:(i + 1) * bs].tobytes() for i in range(max(n1, nm))]
+    t0 = time.perf_counter()
+    one = [impl.encode_block(b) for b in blocks[:n1]]
+    dt1 = time.perf_counter() - t0
+    threads = max(1, min(threads, nm))
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
-        chunks = list(ex.map(impl.encode_block, blocks))
-    dt = time.perf_counter() - t0
-    same = all(
-        (c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) == g for c, g in zip(chunks, gpu_chunks[:nblocks])
-    )
+        many = list(ex.map(impl.encode_block, blocks[:nm]))
+    dtm = time.perf_counter() - t0
+    chunks = many if nm >= n1 else one
+    same = all((c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) == g for c, g in zip(chunks, gpu_chunks))
     return {
-        "value": round(nblocks * bs / dt / 1e9, 6),
+        "value": round(nm * bs / dtm / 1e9, 6),
         "unit": "GB/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"{nblocks} x {bs} B blocks of the benchmark input, one block per task on {threads} threads "
-                  f"({os.cpu_count()} host CPUs visible), {dt:.2f} s wall",
+        "sample": f"{nm} x {bs} B blocks of the benchmark input, one block per task on {threads} threads ({dtm:.2f} s wall); "
+                  f"{cpu_model()}, {os.cpu_count()} host CPUs visible, {CPU_SHARE} per GPU on this box",
+        "single_thread": {"value": round(n1 * bs / dt1 / 1e9, 6), "unit": "GB/s", "cores": 1,
+                          "sample": f"{n1} x {bs} B blocks, {dt1:.2f} s"},
         "bit_exact_vs_gpu": bool(same),
+        "blocks_checked": len(chunks),
     }
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_torchrun(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -84,34 +141,55 @@ def main():
 
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        else:
+            dist.init_process_group(args.backend)
     bra = importlib.import_module("br-archive_amd")
+    dmod = importlib.import_module("br-archive_amd.dist")
 
     bs = args.block_size
-    total = args.bytes_per_gpu
-    nb = bra.BlockCodec.num_blocks(total, bs)
-    first_block, _ = importlib.import_module("br-archive_amd.dist").shard_blocks(nb, rank)
-    data_np = bra.synth_fill(KINDS[args.kind], total, bs, first_block=first_block)
+    strong = args.total_bytes > 0
+    global_total = args.total_bytes if strong else world * args.bytes_per_gpu
+    nbg = dmod.num_blocks(global_total, bs)
+    my_blocks = dmod.shard_blocks(nbg, rank, world)
+    my_bytes = dmod.shard_bytes(global_total, bs, rank, world)
+    nb = len(my_blocks)
+    data_np = bra.synth_fill(KINDS[args.kind], my_bytes, bs, first_block=rank, stride=world)
     d = torch.from_numpy(data_np).cuda()
     codec = bra.BlockCodec(local)
-    hdr = torch.empty((nb, bra.HEADER_BYTES), dtype=torch.uint8, device=d.device)
-    off = torch.empty((nb + 1,), dtype=torch.int64, device=d.device)
-    pay = torch.empty((int(total * 1.25) + 64 * nb + 65536,), dtype=torch.uint8, device=d.device)
-
-    # RCCL gather of the compressed chunks to rank 0 (br-archive_amd/dist.py)
-    gather = importlib.import_module("br-archive_amd.dist").ChunkGather(dist, rank, world) if world > 1 else None
-
-    def gather_to_root():
-        gather(hdr, off[nb:nb + 1], pay)
-
-    # encode and gather on one torch stream: RCCL's work then waits for the encode's kernels
+    dev = d.device
+    hdr = torch.empty((nb, bra.HEADER_BYTES), dtype=torch.uint8, device=dev)
+    off = torch.empty((nb + 1,), dtype=torch.int64, device=dev)
+    pay = torch.empty((int(my_bytes * 1.25) + 64 * nb + 65536,), dtype=torch.uint8, device=dev)
+    crc_share = torch.zeros((1,), dtype=torch.int32, device=dev)
+    per_batch = max(1, args.batch_bytes // bs)
+    batches = [(b0, min(nb, b0 + per_batch)) for b0 in range(0, nb, per_batch)]
+    off_b = torch.empty((per_batch + 1,), dtype=torch.int64, device=dev)
+    gather = dmod.ChunkGather(dist, rank, world) if world > 1 else None
     work_stream = torch.cuda.Stream()
+    result = {}
 
     def step():
+        """Encode this rank's blocks, CRC share, gather to rank 0, assemble there in global order."""
         with torch.cuda.stream(work_stream):
-            codec.encode(d, bs, hdr, off, pay, stream=work_stream)
+            if len(batches) == 1:
+                codec.encode(d, bs, hdr, off, pay, stream=work_stream)
+            else:
+                base = 0
+                for b0, b1 in batches:
+                    lo, hi = b0 * bs, min(my_bytes, b1 * bs)
+                    codec.encode(d[lo:hi], bs, hdr[b0:b1], off_b, pay[base:], stream=work_stream)
+                    off[b0:b1 + 1] = off_b[: b1 - b0 + 1] + base
+                    base += int(off_b[b1 - b0].item())
+            codec.chunks_crc32c_shard(d, hdr, bs, rank, world, global_total, rank == 0, out=crc_share, stream=work_stream)
             if world > 1:
-                gather_to_root()
+                parts = gather(hdr, off, pay, crc_share)
+            else:
+                parts = [(hdr, off, pay[: int(off[nb].item())], crc_share)]
+            if rank == 0:
+                result["stream"] = dmod.assemble(codec, parts, round_robin=True)
+                result["crc"] = dmod.merge_crc(parts)
 
     # ---- find the dominant kernel (one untimed, fully profiled pass) ----
     kernel_slots = [s for s in codec.SLOTS if not s.startswith("stage.")]
@@ -140,126 +218,133 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=d.device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     prof = codec.prof_read()
 
-    value = world * total * args.steps / elapsed / 1e9
+    value = global_total * args.steps / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     dms, dcnt, dbytes = prof[dominant]
     avg_ms = dms / max(1, dcnt)
     bytes_per_launch = dbytes / max(1, dcnt)
     achieved = bytes_per_launch / (avg_ms / 1e3) / 1e9 if avg_ms > 0 else 0.0
 
-    # ---- outside the timed region: ratio, round trip, reference check ----
-    off_h = off.cpu().numpy()
-    payload_bytes = int(off_h[nb])
-    hdr_h = hdr.cpu().numpy()
-    rle_bytes = int(sum(int.from_bytes(hdr_h[b, 260:264].tobytes(), "little") for b in range(nb)))
-    pipeline_alg = 14 * total + 3 * rle_bytes + payload_bytes + 267 * nb  # SURVEY 8.1 row d
-    stage_ms = {s.split(".")[1]: round(prof[s][0] / max(1, prof[s][1]), 3) for s in stage_slots}
-    encode_dev_ms = sum(stage_ms.values())
-    check = None
-    secondary = {}
-    if not args.no_check:
-        out = codec.decode(hdr, off, pay, total, bs)
-        torch.cuda.synchronize()
-        check = bool(torch.equal(out, d))
-        # decode throughput of the same batch (output bytes / s), inputs resident in HBM
-        t1 = time.perf_counter()
-        for _ in range(3):
-            codec.decode(hdr, off, pay, total, bs, out=out)
-        torch.cuda.synchronize()
-        secondary["decode_GBps"] = round(3 * total / (time.perf_counter() - t1) / 1e9, 4)
-        del out
-    if not args.no_secondary and world == 1:
-        # PCIe-inclusive encode: pinned host input -> HBM, encode, headers + payload back to pinned host
-        h_in = torch.from_numpy(data_np).pin_memory()
-        h_hdr = torch.empty(hdr.shape, dtype=torch.uint8).pin_memory()
-        h_pay = torch.empty((payload_bytes + 4096,), dtype=torch.uint8).pin_memory()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(2):
-            with torch.cuda.stream(work_stream):
-                d.copy_(h_in, non_blocking=True)
-                codec.encode(d, bs, hdr, off, pay, stream=work_stream)
-                h_hdr.copy_(hdr, non_blocking=True)
-                h_pay[: payload_bytes].copy_(pay[: payload_bytes], non_blocking=True)
-        torch.cuda.synchronize()
-        secondary["encode_pcie_inclusive_GBps"] = round(2 * total / (time.perf_counter() - t1) / 1e9, 4)
-
-    line = {
-        "metric": METRIC,
-        "value": round(value, 4),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic",
-        "config": {
-            "workload": f"{nb} x {bs} B {args.kind} blocks per GPU (BASELINE configs[1]: 256 x 1 MiB enwik-style text), "
-                        "encode BWT+MTF+RLE+Huffman, inputs resident in HBM",
-            "block_size": bs,
-            "bytes_per_gpu": total,
-            "parallelism": f"dp{world}: blocks sharded per GPU" + (", RCCL gather of compressed chunks to rank 0" if world > 1 else ""),
-        },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dominant,
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "avg_launch_ms": round(avg_ms, 4),
-            "launches": dcnt,
-            "algorithmic_bytes_per_launch": int(bytes_per_launch),
-        },
-        "pipeline": {
-            "stage_ms": stage_ms,
-            "encode_device_ms": round(encode_dev_ms, 3),
-            "algorithmic_bytes": pipeline_alg,
-            "hbm_frac": round(pipeline_alg / (ms_per_step / 1e3) / (HBM_PEAK_GBS * 1e9), 4),
-            "ratio": round((payload_bytes + 267 * nb) / total, 4),
-            "rle_bytes": rle_bytes,
-            "payload_bytes": payload_bytes,
-            "roundtrip_bit_exact": check,
-        },
-        "secondary": secondary,
-        "cpu_baseline": None,
-    }
-    if args.profile_all:
-        line["kernels"] = {k: {"ms": round(v[0] / max(1, v[1]), 4), "launches": v[1], "GBps": round(v[2] / max(v[0], 1e-9) / 1e6, 1)}
-                           for k, v in prof.items() if v[1]}
-    # traffic from a committed PMC profile of the same kernel, if one exists (profiles/pmc_summary.json)
-    pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(pmc):
-        try:
-            pm = json.load(open(pmc))
-            k = pm.get("kernels", {}).get(dominant)
-            if k and k.get("workload") == line["config"]["workload"]:
-                line["roofline"]["traffic"] = k.get("hbm_bytes_per_launch")
-        except Exception:
-            pass
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gpu_chunks = []
-        pay_h = pay[: payload_bytes].cpu().numpy()
-        for b in range(min(args.cpu_blocks, nb)):
-            pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
-            gpu_chunks.append((pi, lens, osz, esz, pay_h[off_h[b]:off_h[b] + esz].tobytes()))
-        line["cpu_baseline"] = cpu_baseline(data_np, bs, args.cpu_blocks, args.cpu_threads, gpu_chunks)
-
+    line = None
     if rank == 0:
+        H, O, P = result["stream"]
+        off_h = O.cpu().numpy()
+        hdr_h = H.cpu().numpy()
+        payload_bytes = int(off_h[nbg])
+        rle_bytes = int(hdr_h[:, 260:264].copy().view(np.uint32).sum())
+        pipeline_alg = 14 * global_total + 3 * rle_bytes + payload_bytes + 267 * nbg  # SURVEY 8.1 row d
+        stage_ms = {s.split(".")[1]: round(prof[s][0] / max(1, prof[s][1]), 3) for s in stage_slots}
+        check, secondary = None, {}
+        if not args.no_check:
+            # decode the assembled global stream; its chunk-stream CRC must equal the merged shares
+            # (every rank's input took part), and the blocks this rank holds must come back exactly
+            out = codec.decode(H, O, P, global_total, bs)
+            torch.cuda.synchronize()
+            crc_dec = codec.chunks_crc32c(out, H, bs)
+            mine_ok = all(torch.equal(out[g * bs:g * bs + min(bs, global_total - g * bs)], d[i * bs:i * bs + min(bs, my_bytes - i * bs)])
+                          for i, g in enumerate(my_blocks[:64]))
+            check = bool(crc_dec == result["crc"] and mine_ok)
+            secondary["crc32c_chunk_stream"] = f"{result['crc']:08x}"
+            if not args.no_secondary and world == 1:
+                t1 = time.perf_counter()
+                for _ in range(3):
+                    codec.decode(H, O, P, global_total, bs, out=out)
+                torch.cuda.synchronize()
+                secondary["decode_GBps"] = round(3 * global_total / (time.perf_counter() - t1) / 1e9, 4)
+            del out
+        if not args.no_secondary and world == 1 and len(batches) == 1:
+            # PCIe-inclusive encode: pinned host input -> HBM, encode, headers + payload back to pinned host
+            h_in = torch.from_numpy(data_np).pin_memory()
+            h_hdr = torch.empty(hdr.shape, dtype=torch.uint8).pin_memory()
+            h_pay = torch.empty((payload_bytes + 4096,), dtype=torch.uint8).pin_memory()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(2):
+                with torch.cuda.stream(work_stream):
+                    d.copy_(h_in, non_blocking=True)
+                    codec.encode(d, bs, hdr, off, pay, stream=work_stream)
+                    h_hdr.copy_(hdr, non_blocking=True)
+                    h_pay[: payload_bytes].copy_(pay[: payload_bytes], non_blocking=True)
+            torch.cuda.synchronize()
+            secondary["encode_pcie_inclusive_GBps"] = round(2 * global_total / (time.perf_counter() - t1) / 1e9, 4)
+
+        line = {
+            "metric": METRIC,
+            "value": round(value, 4),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{nbg} x {bs} B {args.kind} blocks ({global_total >> 20} MiB global, "
+                            f"{'fixed total' if strong else f'{args.bytes_per_gpu >> 20} MiB per GPU'}; {WORKLOADS[args.kind]}), "
+                            "encode BWT+MTF+RLE+Huffman + chunk-stream CRC32C + chunks assembled in block order on rank 0, "
+                            "inputs resident in HBM",
+                "block_size": bs,
+                "global_bytes": global_total,
+                "batches_per_rank": len(batches),
+                "parallelism": f"dp{world}: block b on GPU b mod {world} (round robin)"
+                               + (", RCCL gather of compressed chunks + CRC shares to rank 0" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dominant,
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_ms": round(avg_ms, 4),
+                "launches": dcnt,
+                "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            },
+            "pipeline": {
+                "stage_ms": stage_ms,
+                "encode_device_ms": round(sum(stage_ms.values()), 3),
+                "algorithmic_bytes": pipeline_alg,
+                "hbm_frac": round(pipeline_alg / (ms_per_step / 1e3) / (HBM_PEAK_GBS * 1e9), 4),
+                "ratio": round((payload_bytes + 267 * nbg) / global_total, 4),
+                "rle_bytes": rle_bytes,
+                "payload_bytes": payload_bytes,
+                "roundtrip_bit_exact": check,
+            },
+            "secondary": secondary,
+            "cpu_baseline": None,
+        }
+        if args.profile_all:
+            line["kernels"] = {k: {"ms": round(v[0] / max(1, v[1]), 4), "launches": v[1], "GBps": round(v[2] / max(v[0], 1e-9) / 1e6, 1)}
+                               for k, v in prof.items() if v[1]}
+        # traffic from a committed PMC profile of the same kernel and workload (profiles/pmc_summary.json)
+        pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
+        if os.path.exists(pmc):
+            try:
+                k = json.load(open(pmc)).get("kernels", {}).get(dominant)
+                if k and k.get("workload") == line["config"]["workload"]:
+                    line["roofline"]["traffic"] = k.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                pass
+        if world == 1 and not args.no_cpu_baseline:
+            gpu_chunks = []
+            pay_h = P.cpu().numpy()
+            for b in range(max(cpu_sample_sizes(nb, bs, args.cpu_threads))):
+                pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
+                gpu_chunks.append((pi, lens, osz, esz, pay_h[off_h[b]:off_h[b] + esz].tobytes()))
+            line["cpu_baseline"] = cpu_baseline(data_np, bs, args.cpu_threads, gpu_chunks)
         print(json.dumps(line), flush=True)
     codec.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

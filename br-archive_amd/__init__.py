@@ -38,6 +38,7 @@ ABI_SYMBOLS = (
     "bra_gpu_prof_enable", "bra_gpu_prof_reset", "bra_gpu_prof_read",
     "bra_gpu_crc32c", "bra_gpu_chunks_crc32c", "bra_gpu_crc32c_combine", "bra_gpu_entry_crc32c", "bra_gpu_chunks_bound",
     "bra_gpu_frame_chunks", "bra_gpu_unframe_chunks", "bra_gpu_compress_chunks", "bra_gpu_decompress_chunks",
+    "bra_gpu_chunks_crc32c_shard", "bra_gpu_assemble_shards",
 )
 MAX_CHUNK_SIZE = 256 * 1024  # BRA_MAX_CHUNK_SIZE (src/lib_bra_defs.h:93): the .BRa chunk size
 
@@ -145,6 +146,12 @@ def _load() -> C.CDLL:
     lib.bra_gpu_compress_chunks.restype = C.c_int
     lib.bra_gpu_decompress_chunks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, u64p, C.c_uint32, u32p, vp]
     lib.bra_gpu_decompress_chunks.restype = C.c_int
+    lib.bra_gpu_chunks_crc32c_shard.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int,
+                                                vp, vp]
+    lib.bra_gpu_chunks_crc32c_shard.restype = C.c_int
+    lib.bra_gpu_assemble_shards.argtypes = [vp, C.c_uint32, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), u32p, C.c_int, vp, vp, vp,
+                                            C.c_uint64, vp]
+    lib.bra_gpu_assemble_shards.restype = C.c_int
     return lib
 
 
@@ -409,6 +416,50 @@ class BlockCodec:
             raise ValueError(f"bra_gpu_decompress_chunks rejected the stream ({rc})")
         return out[: osz.value], crc.value
 
+    # ---- sharded streams (row e) ----
+    def chunks_crc32c_shard(self, data, headers, block_size: int, first_chunk: int, chunk_stride: int, global_total: int,
+                            with_init: bool, out=None, prev: int = 0, stream=None):
+        """This shard's CRC word (int32 CUDA tensor [1]) of the global chunk stream; XOR over the shards
+        gives the stream's CRC32C when exactly one shard has with_init.  Asynchronous on `stream`."""
+        import torch
+
+        if out is None:
+            out = torch.empty((1,), dtype=torch.int32, device=data.device)
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_chunks_crc32c_shard(self.ctx, data.data_ptr(), data.numel(), block_size, headers.data_ptr(), first_chunk,
+                                             chunk_stride, global_total, prev, 1 if with_init else 0, out.data_ptr(), s)
+        if rc != 0:
+            raise RuntimeError(f"bra_gpu_chunks_crc32c_shard failed ({rc})")
+        return out
+
+    def assemble_shards(self, parts, round_robin: bool = True, headers=None, offsets=None, payload=None, stream=None):
+        """parts: [(headers [n_p,268] u8, offsets [n_p+1] i64, payload u8)] on this device.  Returns
+        (headers, offsets, payload) of all blocks in global order (round robin: block g from part g % P)."""
+        import torch
+
+        P = len(parts)
+        nbs = [int(h.shape[0]) for h, _, _ in parts]
+        nb = sum(nbs)
+        dev = parts[0][0].device
+        total_pay = sum(int(p.numel()) for _, _, p in parts)
+        if headers is None:
+            headers = torch.empty((nb, HEADER_BYTES), dtype=torch.uint8, device=dev)
+        if offsets is None:
+            offsets = torch.empty((nb + 1,), dtype=torch.int64, device=dev)
+        if payload is None:
+            payload = torch.empty((max(total_pay, 1),), dtype=torch.uint8, device=dev)
+        arr = C.c_void_p * P
+        hp = arr(*[h.data_ptr() for h, _, _ in parts])
+        op = arr(*[o.data_ptr() for _, o, _ in parts])
+        pp = arr(*[p.data_ptr() for _, _, p in parts])
+        nn = (C.c_uint32 * P)(*nbs)
+        s = stream.cuda_stream if stream is not None else None
+        rc = lib.bra_gpu_assemble_shards(self.ctx, P, hp, op, pp, nn, 1 if round_robin else 0, headers.data_ptr(), offsets.data_ptr(),
+                                         payload.data_ptr(), payload.numel(), s)
+        if rc != 0:
+            raise RuntimeError(f"bra_gpu_assemble_shards failed ({rc})")
+        return headers, offsets, payload
+
     def prof_enable(self, mask: int):
         """Time the selected kernel slots with HIP events (bit i = slot i, see csrc/prof.h)."""
         lib.bra_gpu_prof_enable(self.ctx, mask)
@@ -477,6 +528,7 @@ def synth_lib():
         _synth = C.CDLL(SYNTH_PATH)
         _synth.bra_synth_block.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_uint64]
         _synth.bra_synth_fill.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64]
+        _synth.bra_synth_fill_strided.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint64]
     return _synth
 
 
@@ -486,10 +538,10 @@ def synth_block(kind: int, index: int, n: int) -> bytes:
     return bytes(b)[:n]
 
 
-def synth_fill(kind: int, total: int, block_size: int, first_block: int = 0):
-    """numpy uint8 array of `total` bytes: consecutive synthetic blocks."""
+def synth_fill(kind: int, total: int, block_size: int, first_block: int = 0, stride: int = 1):
+    """numpy uint8 array of `total` bytes: synthetic blocks first_block, first_block + stride, ..."""
     import numpy as np
 
     a = np.empty(total, dtype=np.uint8)
-    synth_lib().bra_synth_fill(kind, first_block, a.ctypes.data, total, block_size)
+    synth_lib().bra_synth_fill_strided(kind, first_block, stride, a.ctypes.data, total, block_size)
     return a

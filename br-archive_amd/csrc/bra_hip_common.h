@@ -34,6 +34,34 @@ namespace bra {
 
 constexpr int WAVE = 64;
 
+// (Re)allocate device buffer p for `elems` elements of T, dropping its old contents.  On failure p
+// is null and false is returned; callers zero their capacity field BEFORE calling and set it only
+// after every allocation of the group succeeded, so a failed grow never leaves a stale capacity
+// next to a null pointer (a later, smaller request would otherwise launch kernels on null).
+template <typename T>
+inline bool dev_alloc(T*& p, uint64_t elems)
+{
+    (void) hipFree(p);
+    p            = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), (size_t) (elems ? elems : 1) * sizeof(T));
+    if (e != hipSuccess)
+    {
+        p = nullptr;
+        (void) hipGetLastError();
+        bra_hip_report("device allocation of %llu bytes failed: %s", (unsigned long long) (elems * sizeof(T)), hipGetErrorString(e));
+        return false;
+    }
+    return true;
+}
+
+inline bool dev_alloc_bytes(void*& p, uint64_t bytes)
+{
+    uint8_t*   q  = static_cast<uint8_t*>(p);
+    const bool ok = dev_alloc(q, bytes);
+    p             = q;
+    return ok;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Batch geometry: a batch is `nblocks` independent blocks laid out back to back in HBM.
 // ---------------------------------------------------------------------------------------------

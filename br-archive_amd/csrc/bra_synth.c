@@ -144,3 +144,17 @@ int bra_synth_fill(int kind, uint64_t first_block, uint8_t* out, uint64_t total,
     }
     return 1;
 }
+
+/* Fill `total` bytes with the blocks first_block, first_block + stride, ... (a round-robin shard of a
+ * global stream: rank r of G ranks holds global blocks r, r + G, ...), back to back. */
+int bra_synth_fill_strided(int kind, uint64_t first_block, uint64_t stride, uint8_t* out, uint64_t total, uint64_t block_size)
+{
+    uint64_t b = first_block;
+    for (uint64_t off = 0; off < total; off += block_size, b += stride)
+    {
+        const uint64_t len = (total - off) < block_size ? (total - off) : block_size;
+        if (!bra_synth_block(kind, b, out + off, len))
+            return 0;
+    }
+    return 1;
+}

@@ -30,6 +30,7 @@
 #include "prof.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <vector>
 
@@ -2432,46 +2433,44 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     ws_env(w);
     const uint64_t N = std::max<uint64_t>(n, 1 << 16);
     const uint32_t B = std::max<uint32_t>(nblocks, 64);
-    w.cap_n      = N;
-    w.cap_blocks = B;
     w.cap_l0     = (uint32_t) (N / TILE + B + 1);
     w.cap_big    = (uint32_t) (N / JOB_MAX + B + 16);
     w.cap_tiles  = (uint32_t) (N / TILE + w.cap_big + 16);
-    w.cap_jobs   = (uint32_t) (N / 8 + B + 1024);
-    w.cap_groups = (uint32_t) (N / 64 + B + 4096);
+    // Worst cases: every fallback group has >= 2 members and the groups of one list are disjoint, so
+    // a list holds <= N/2 of them (a duplicated region longer than the refinement cap emits about one
+    // 2-member group per byte); the fallback turns every group of <= JOB_MAX members into one wave
+    // job, so the unsorted wave-job list needs N/2 entries too.  The main path's wave jobs pack
+    // runs of small sub-buckets (<= N/128 + N/129 jobs), so the XCD-sorted copy stays at N/8.
+    w.cap_jobs   = (uint32_t) (N / 2 + B + 1024);
+    w.cap_groups = (uint32_t) (N / 2 + B + 64);
     w.cap_mjobs  = (uint32_t) (N / JOB_MAX + B + 64);
-    for (int i = 0; i < 2; ++i)
+    const uint32_t cap_sorted = (uint32_t) (N / 8 + B + 1024);
+    bool ok = true;
+    for (int i = 0; i < 2 && ok; ++i)
+        ok = dev_alloc(w.key[i], N) && dev_alloc(w.pay[i], N) && dev_alloc(w.big[i], w.cap_big) && dev_alloc(w.groups[i], w.cap_groups) &&
+             dev_alloc(w.tile_bucket[i], w.cap_tiles);
+    const uint32_t tmax  = std::max(w.cap_tiles, w.cap_l0);
+    const size_t   nkeys = 8 * (size_t) div_up(B, 8);
+    ok = ok && dev_alloc(w.fsa, N) && dev_alloc(w.isa, N) && dev_alloc(w.tile_hist, (uint64_t) tmax * 256) &&
+         dev_alloc(w.tile_off, (uint64_t) tmax * 256) && dev_alloc(w.nomove, std::max<uint32_t>(w.cap_big, B)) && dev_alloc(w.flag, B) &&
+         dev_alloc(w.jobs, w.cap_jobs) && dev_alloc(w.mjobs, w.cap_mjobs) && dev_alloc(w.jobs_sorted, cap_sorted) &&
+         dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 8 * nkeys) && dev_alloc(w.tile_cnt, 2 * nkeys + 16) &&
+         dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.tdesc[0], w.cap_tiles) && dev_alloc(w.tdesc[1], w.cap_tiles) &&
+         dev_alloc(w.dig[0], N + 16) && dev_alloc(w.dig[1], N + 16) && dev_alloc(w.ctr, 1) && dev_alloc(w.jobq, 3 * 8 * 32) &&
+         dev_alloc(w.l0tiles, w.cap_l0);
+    if (ok && hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault) != hipSuccess)
+        w.h_job_cnt = nullptr, ok = false;
+    if (ok && hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
+        w.h_ctr = nullptr, ok = false;
+    if (!ok)
     {
-        BRA_HIP_CHECK(hipMalloc(&w.key[i], N * 8));
-        BRA_HIP_CHECK(hipMalloc(&w.pay[i], N * 4));
-        BRA_HIP_CHECK(hipMalloc(&w.big[i], (size_t) w.cap_big * sizeof(Bucket)));
-        BRA_HIP_CHECK(hipMalloc(&w.groups[i], (size_t) w.cap_groups * sizeof(Group)));
-        BRA_HIP_CHECK(hipMalloc(&w.tile_bucket[i], (size_t) w.cap_tiles * 4));
+        bra_hip_report("bwt: workspace allocation for %llu elements failed", (unsigned long long) N);
+        ws_free(w);  // capacities back to zero: the next call retries the allocation
+        ws_env(w);
+        return false;
     }
-    BRA_HIP_CHECK(hipMalloc(&w.fsa, N * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.isa, N * 4));
-    const uint32_t tmax = std::max(w.cap_tiles, w.cap_l0);
-    BRA_HIP_CHECK(hipMalloc(&w.tile_hist, (size_t) tmax * 256 * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.tile_off, (size_t) tmax * 256 * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.nomove, std::max<uint32_t>(w.cap_big, B)));
-    BRA_HIP_CHECK(hipMalloc(&w.flag, B));
-    BRA_HIP_CHECK(hipMalloc(&w.jobs, (size_t) w.cap_jobs * sizeof(Job)));
-    BRA_HIP_CHECK(hipMalloc(&w.mjobs, (size_t) w.cap_mjobs * sizeof(Job)));
-    BRA_HIP_CHECK(hipMalloc(&w.jobs_sorted, (size_t) w.cap_jobs * sizeof(Job)));
-    BRA_HIP_CHECK(hipMalloc(&w.mjobs_sorted, (size_t) w.cap_mjobs * sizeof(Job)));
-    const size_t nkeys = 8 * (size_t) div_up(B, 8);
-    BRA_HIP_CHECK(hipMalloc(&w.job_cnt, 8 * nkeys * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.tile_cnt, (2 * nkeys + 16) * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.tile_order, (size_t) w.cap_tiles * sizeof(TileDesc)));
-    BRA_HIP_CHECK(hipMalloc(&w.tdesc[0], (size_t) w.cap_tiles * sizeof(TileDesc)));
-    BRA_HIP_CHECK(hipMalloc(&w.dig[0], N + 16));
-    BRA_HIP_CHECK(hipMalloc(&w.dig[1], N + 16));
-    BRA_HIP_CHECK(hipMalloc(&w.tdesc[1], (size_t) w.cap_tiles * sizeof(TileDesc)));
-    BRA_HIP_CHECK(hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault));
-    BRA_HIP_CHECK(hipMalloc(&w.ctr, sizeof(Counters)));
-    BRA_HIP_CHECK(hipMalloc(&w.jobq, 3 * 8 * 32 * 4));
-    BRA_HIP_CHECK(hipMalloc(&w.l0tiles, (size_t) w.cap_l0 * sizeof(L0Tile)));
-    BRA_HIP_CHECK(hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault));
+    w.cap_n      = N;
+    w.cap_blocks = B;
     return true;
 }
 
@@ -2619,8 +2618,12 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     BRA_HIP_CHECK(hipMemsetAsync(w.tile_hist, 0xA5, (size_t) std::max(w.cap_tiles, w.cap_l0) * 256 * 4, s));
     BRA_HIP_CHECK(hipMemsetAsync(w.tile_off, 0xA5, (size_t) std::max(w.cap_tiles, w.cap_l0) * 256 * 4, s));
 #endif
-    static bool attr_set = false;
-    if (!attr_set)
+    // kernel attributes are per device: set them once on every device this process encodes on
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0;
+    BRA_HIP_CHECK(hipGetDevice(&dev));
+    const uint64_t dev_bit = 1ull << (dev & 63);
+    if (!(attr_set.load() & dev_bit))
     {
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
@@ -2629,7 +2632,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
-        attr_set = true;
+        attr_set.fetch_or(dev_bit);
     }
     const int grid = w.grid;
 

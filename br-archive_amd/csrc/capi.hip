@@ -38,7 +38,7 @@ using namespace bra;
 
 // ---- event profiler (prof.h) ----
 namespace bra {
-Prof* g_prof = nullptr;
+thread_local Prof* g_prof = nullptr;
 
 const char* prof_name(int slot)
 {
@@ -132,17 +132,41 @@ __global__ void k_split_headers(const bra_io_chunk_header_t* __restrict__ hdr, u
     }
 }
 
+// Grow p to at least `need` elements; cap is set only once the allocation succeeded (dev_alloc).
 template <typename T>
 bool grow(T*& p, uint64_t& cap, uint64_t need)
 {
     if (need <= cap)
         return true;
-    (void) hipFree(p);
-    p   = nullptr;
-    cap = need + need / 8 + 256;
-    BRA_HIP_CHECK(hipMalloc(&p, cap * sizeof(T)));
+    cap              = 0;
+    const uint64_t c = need + need / 8 + 256;
+    if (!dev_alloc(p, c))
+        return false;
+    cap = c;
     return true;
 }
+
+// Makes `dev` current for the scope of a C-ABI call and restores the caller's device afterwards, so
+// a call never silently changes the calling thread's current HIP device.
+struct DevGuard
+{
+    int  prev = -1;
+    bool ok   = false;
+    explicit DevGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        ok = prev == dev || hipSetDevice(dev) == hipSuccess;
+    }
+    ~DevGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev)
+            (void) hipSetDevice(prev);
+    }
+    DevGuard(const DevGuard&)            = delete;
+    DevGuard& operator=(const DevGuard&) = delete;
+};
 
 }  // namespace
 
@@ -192,7 +216,9 @@ struct bra_gpu_ctx_s
 static bool ctx_init(bra_gpu_ctx_s* c, int device)
 {
     c->device = device;
-    BRA_HIP_CHECK(hipSetDevice(device));
+    DevGuard dg(device);
+    if (!dg.ok)
+        return false;
     BRA_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->bwt = bwt_workspace_create();
     return c->bwt != nullptr;
@@ -200,7 +226,7 @@ static bool ctx_init(bra_gpu_ctx_s* c, int device)
 
 static void ctx_free(bra_gpu_ctx_s* c)
 {
-    (void) hipSetDevice(c->device);
+    DevGuard dg(c->device);
     bwt_workspace_destroy(c->bwt);
     c->mtf.release();
     c->rle.release();
@@ -316,7 +342,7 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
 // out_cap).
 static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
                        const std::vector<BlockDesc>& hb, uint8_t* d_out, hipStream_t s, bool flex = false, uint64_t out_cap = 0,
-                       uint64_t* out_size = nullptr)
+                       uint64_t* out_size = nullptr, std::vector<uint32_t>* out_sizes = nullptr)
 {
     const uint32_t nb = (uint32_t) hb.size();
     if (nb == 0)
@@ -418,6 +444,12 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
     }
     if (out_size)
         *out_size = total;
+    if (out_sizes)
+    {
+        out_sizes->resize(nb);
+        for (uint32_t b = 0; b < nb; ++b)
+            (*out_sizes)[b] = g[b].len;
+    }
     if (total > out_cap)
     {
         bra_hip_report("decoded chunk stream needs %llu bytes, output holds %llu", (unsigned long long) total, (unsigned long long) out_cap);
@@ -481,7 +513,8 @@ int bra_gpu_encode_blocks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t total,
 {
     if (!c || !d_in || !total || !block_size || block_size >= (1u << 24) || !d_headers || !d_payload_off || !d_payload)
         return -1;
-    if (hipSetDevice(c->device) != hipSuccess)
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     g_prof       = c->prof.mask ? &c->prof : nullptr;
@@ -495,7 +528,8 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_heade
 {
     if (!c || !d_headers || !d_payload_off || !d_payload || !total || !block_size || block_size >= (1u << 24) || !d_out)
         return -1;
-    if (hipSetDevice(c->device) != hipSuccess)
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     return decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
@@ -503,7 +537,10 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_heade
 
 int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t prev, uint32_t* d_crc, void* stream)
 {
-    if (!c || !d_crc || (len && !d_data) || hipSetDevice(c->device) != hipSuccess)
+    if (!c || !d_crc || (len && !d_data))
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     if (!crc_stream_device(static_cast<const uint8_t*>(d_data), len, 0, nullptr, prev, d_crc, s))
@@ -514,7 +551,10 @@ int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t 
 int bra_gpu_chunks_crc32c(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_t total, uint32_t block_size, const bra_io_chunk_header_t* d_headers,
                           uint32_t prev, uint32_t* d_crc, void* stream)
 {
-    if (!c || !d_crc || !block_size || (total && (!d_data || !d_headers)) || hipSetDevice(c->device) != hipSuccess)
+    if (!c || !d_crc || !block_size || (total && (!d_data || !d_headers)))
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     if (!crc_stream_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), prev, d_crc, s))
@@ -541,7 +581,10 @@ uint64_t bra_gpu_chunks_bound(uint64_t total, uint32_t block_size)
 int bra_gpu_frame_chunks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
                          uint32_t nblocks, uint8_t* d_out, uint64_t out_cap, uint64_t* out_size, void* stream)
 {
-    if (!c || !d_headers || !d_payload_off || !d_payload || !d_out || hipSetDevice(c->device) != hipSuccess)
+    if (!c || !d_headers || !d_payload_off || !d_payload || !d_out)
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     uint64_t    P = 0;
@@ -560,7 +603,10 @@ int bra_gpu_frame_chunks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_header
 int bra_gpu_unframe_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t max_chunks, bra_io_chunk_header_t* d_headers,
                            uint64_t* d_payload_off, uint32_t* n_chunks, void* stream)
 {
-    if (!c || !d_stream || !d_headers || !d_payload_off || hipSetDevice(c->device) != hipSuccess)
+    if (!c || !d_stream || !d_headers || !d_payload_off)
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
     if (!grow(c->d_word, c->cap_word, 4))
@@ -583,7 +629,10 @@ int bra_gpu_unframe_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t s
 int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data_size, uint32_t block_size, uint8_t* d_out, uint64_t out_cap,
                             uint64_t* out_size, uint32_t* chunks_crc, void* stream)
 {
-    if (!c || !d_in || !data_size || !block_size || block_size >= (1u << 24) || !d_out || hipSetDevice(c->device) != hipSuccess)
+    if (!c || !d_in || !data_size || !block_size || block_size >= (1u << 24) || !d_out)
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t    s  = stream ? (hipStream_t) stream : c->stream;
     const auto     hb = geometry(data_size, block_size);
@@ -634,7 +683,10 @@ int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data
 int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
                               uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream)
 {
-    if (!c || !d_stream || !block_size || block_size >= (1u << 24) || !d_out || hipSetDevice(c->device) != hipSuccess)
+    if (!c || !d_stream || !block_size || block_size >= (1u << 24) || !d_out)
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
         return -1;
     hipStream_t    s        = stream ? (hipStream_t) stream : c->stream;
     const uint32_t max_recs = (uint32_t) std::min<uint64_t>(stream_size / (CHUNK_HDR_DISK + 1) + 1, 1u << 26);
@@ -652,7 +704,8 @@ int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_
     for (uint32_t b = 0; b < nb; ++b)
         caps[b] = BlockDesc{(uint64_t) b * block_size, block_size, 0};
     uint64_t total = 0;
-    int      rc    = decode_impl(c, c->d_hdr, c->d_off, d_stream, caps, d_out, s, true, out_cap, &total);
+    std::vector<uint32_t> dsz;
+    int      rc    = decode_impl(c, c->d_hdr, c->d_off, d_stream, caps, d_out, s, true, out_cap, &total, &dsz);
     if (out_size)
         *out_size = total;
     if (rc != 0)
@@ -664,11 +717,88 @@ int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_
     }
     if (crc_out)
     {
-        if (!crc_stream_device(d_out, total, block_size, reinterpret_cast<const uint8_t*>(c->d_hdr), prev_crc, c->d_word, s) ||
-            hipMemcpyAsync(crc_out, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-            return -1;
+        // The decode loop folds header b then decoded chunk b into me->crc32 (:396-397).  With every
+        // chunk but the last at block_size this is one device pass over the packed output; a stream
+        // with a short chunk in the middle (accepted like the reference does) is folded chunk by chunk.
+        bool regular = true;
+        for (uint32_t b = 0; b + 1 < nb; ++b)
+            regular = regular && dsz[b] == block_size;
+        uint32_t crc = prev_crc;
+        if (regular)
+        {
+            if (!crc_stream_device(d_out, total, block_size, reinterpret_cast<const uint8_t*>(c->d_hdr), prev_crc, c->d_word, s) ||
+                hipMemcpyAsync(&crc, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+                return -1;
+        }
+        else
+        {
+            uint64_t o = 0;
+            for (uint32_t b = 0; b < nb; o += dsz[b], ++b)
+                if (!crc_stream_device(d_out + o, dsz[b], dsz[b], reinterpret_cast<const uint8_t*>(c->d_hdr + b), crc, c->d_word, s) ||
+                    hipMemcpyAsync(&crc, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+                    return -1;
+        }
+        *crc_out = crc;
     }
     return 0;
+}
+
+int bra_gpu_chunks_crc32c_shard(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_t total, uint32_t block_size, const bra_io_chunk_header_t* d_headers,
+                                uint64_t first_chunk, uint64_t chunk_stride, uint64_t global_total, uint32_t prev, int with_init, uint32_t* d_crc,
+                                void* stream)
+{
+    if (!c || !d_crc || !block_size || !chunk_stride || (total && (!d_data || !d_headers)))
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    if (!crc_stream_shard_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), first_chunk, chunk_stride, global_total,
+                                 prev, with_init != 0, d_crc, s))
+        return -1;
+    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
+}
+
+int bra_gpu_assemble_shards(bra_gpu_ctx_t* c, uint32_t nparts, const bra_io_chunk_header_t* const* d_headers, const uint64_t* const* d_payload_off,
+                            const uint8_t* const* d_payload, const uint32_t* nblocks, int round_robin, bra_io_chunk_header_t* d_headers_out,
+                            uint64_t* d_payload_off_out, uint8_t* d_payload_out, uint64_t payload_cap, void* stream)
+{
+    if (!c || nparts == 0 || nparts > MAX_SHARDS || !d_headers || !d_payload_off || !d_payload || !nblocks || !d_headers_out ||
+        !d_payload_off_out || !d_payload_out)
+        return -1;
+    ShardParts P{};
+    P.n           = nparts;
+    P.round_robin = round_robin ? 1u : 0u;
+    uint64_t nb   = 0;
+    for (uint32_t p = 0; p < nparts; ++p)
+    {
+        if (!d_headers[p] || !d_payload_off[p] || (!d_payload[p] && nblocks[p]))
+            return -1;
+        P.hdr[p]   = reinterpret_cast<const uint8_t*>(d_headers[p]);
+        P.off[p]   = d_payload_off[p];
+        P.pay[p]   = d_payload[p];
+        P.first[p] = (uint32_t) nb;
+        nb += nblocks[p];
+    }
+    P.first[nparts] = (uint32_t) nb;
+    if (nb == 0 || nb >= (1ull << 31))
+        return -1;
+    if (round_robin)
+        for (uint32_t p = 0; p < nparts; ++p)  // part p must hold exactly the blocks g = p (mod nparts)
+            if ((uint64_t) nblocks[p] != (nb > p ? (nb - p + nparts - 1) / nparts : 0))
+                return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
+        return -1;
+    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    if (!grow(c->d_word, c->cap_word, 4) ||
+        !assemble_shards_device(P, (uint32_t) nb, reinterpret_cast<uint8_t*>(d_headers_out), d_payload_off_out, d_payload_out, payload_cap,
+                                c->d_word + 3, s))
+        return -1;
+    uint32_t err = 1;
+    if (hipMemcpyAsync(&err, c->d_word + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    return err ? -2 : 0;
 }
 
 const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)
@@ -722,30 +852,65 @@ int bra_gpu_prof_read(bra_gpu_ctx_t* c, int slot, const char** name, double* tot
 }  // extern "C"
 
 // =================================================================================================
-// Part 1: the reference encoder ABI on a lazily created process-wide context
+// Part 1: the reference encoder ABI on lazily created contexts of the caller's current device
 // =================================================================================================
 namespace {
 
-std::mutex     g_mu;
-bra_gpu_ctx_s* g_ctx = nullptr;
+// The reference encoders are reentrant (no globals), so calls from several host threads must not
+// queue behind one another: each call leases a context of the calling thread's current HIP device
+// from that device's pool (creating one when all are busy) and returns it afterwards.  Contexts live
+// until process exit; a pool grows to the number of threads that ever called concurrently.
+constexpr int MAX_DEVICES = 64;
 
-bra_gpu_ctx_s* global_ctx()
+struct CtxPool
 {
-    if (!g_ctx)
+    std::mutex                  mu;
+    std::vector<bra_gpu_ctx_s*> idle;
+};
+CtxPool g_pools[MAX_DEVICES];
+
+struct CtxLease
+{
+    bra_gpu_ctx_s* ctx = nullptr;
+    int            dev = -1;
+    CtxLease()
     {
-        auto* c = new bra_gpu_ctx_s();
-        if (!ctx_init(c, 0))
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES)
         {
+            (void) hipGetLastError();
             bra_hip_report("no usable HIP device for the block codec");
+            dev = -1;
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_pools[dev].mu);
+            if (!g_pools[dev].idle.empty())
+            {
+                ctx = g_pools[dev].idle.back();
+                g_pools[dev].idle.pop_back();
+                return;
+            }
+        }
+        auto* c = new bra_gpu_ctx_s();
+        if (!ctx_init(c, dev))
+        {
+            bra_hip_report("unable to create a block-codec context on HIP device %d", dev);
             ctx_free(c);
             delete c;
-            return nullptr;
+            return;
         }
-        g_ctx = c;
+        ctx = c;
     }
-    (void) hipSetDevice(g_ctx->device);
-    return g_ctx;
-}
+    ~CtxLease()
+    {
+        if (!ctx)
+            return;
+        std::lock_guard<std::mutex> lk(g_pools[dev].mu);
+        g_pools[dev].idle.push_back(ctx);
+    }
+    CtxLease(const CtxLease&)            = delete;
+    CtxLease& operator=(const CtxLease&) = delete;
+};
 
 bool upload(bra_gpu_ctx_s* c, const uint8_t* buf, uint64_t n)
 {
@@ -773,8 +938,8 @@ bool bra_bwt_encode2(const uint8_t* buf, const bra_bwt_index_t buf_size, bra_bwt
 {
     if (!buf || !buf_size || !primary_index || !out_buf)
         return false;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size))
         return false;
     auto hb = one_block(buf_size);
@@ -805,8 +970,8 @@ void bra_bwt_decode2(const uint8_t* buf, const bra_bwt_index_t buf_size, const b
 {
     if (!buf || !buf_size || !out_buf || primary_index >= buf_size)
         return;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size))
         return;
     auto hb = one_block(buf_size);
@@ -837,8 +1002,8 @@ bool bra_mtf_encode2(const uint8_t* buf, const size_t buf_size, uint8_t* out_buf
 {
     if (!buf || !buf_size || !out_buf || buf_size >= (1ull << 31))
         return false;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size) || !grow(c->d_mtf, c->cap_mtf, (uint64_t) buf_size + 16))
         return false;
     // blocks larger than 2^24 are fine for MTF: the segment scan is exact at any length
@@ -865,8 +1030,8 @@ void bra_mtf_decode2(const uint8_t* buf, const size_t buf_size, uint8_t* out_buf
 {
     if (!buf || !buf_size || !out_buf || buf_size >= (1ull << 31))
         return;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size) || !grow(c->d_mtf, c->cap_mtf, (uint64_t) buf_size + 16) ||
         !grow(c->d_tmp, c->cap_tmp, (uint64_t) buf_size + 16))
         return;
@@ -895,8 +1060,8 @@ bool bra_rle_encode(const uint8_t* buf, const size_t buf_size, uint8_t** out_buf
         *out_buf_size = 0;
     if (!buf || !out_buf || !out_buf_size || buf_size == 0 || buf_size >= (1ull << 31))
         return false;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size) || !ensure_block_arrays(c, 1))
         return false;
     const uint64_t cap = rle_capacity((uint32_t) buf_size);
@@ -948,8 +1113,8 @@ size_t bra_rle_decode_compute_size(const uint8_t* buf, const size_t buf_size)
 {
     if (!buf || buf_size == 0 || buf_size >= (1ull << 31))
         return 0;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     uint32_t                    s = 0;
     if (!c || !rle_decode_one(c, buf, buf_size, &s, false))
         return 0;
@@ -964,8 +1129,8 @@ bool bra_rle_decode(const uint8_t* buf, const size_t buf_size, uint8_t** out_buf
         *out_buf_size = 0;
     if (!buf || !out_buf || !out_buf_size || buf_size == 0 || buf_size >= (1ull << 31))
         return false;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     uint32_t                    s = 0;
     if (!c || !rle_decode_one(c, buf, buf_size, &s, true) || s == 0)
         return false;
@@ -989,8 +1154,8 @@ bra_huffman_chunk_t* bra_huffman_encode(const uint8_t* buf, const uint32_t buf_s
         bra_hip_report("unable to huffman encode");
         return nullptr;
     }
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size) || !ensure_block_arrays(c, 1) || !grow(c->d_off, c->cap_off, 4))
         return nullptr;
     std::vector<BlockDesc> hb{BlockDesc{0, buf_size, 0}};
@@ -1035,8 +1200,8 @@ uint8_t* bra_huffman_decode(const bra_huffman_t* meta, const uint8_t* data, uint
         *out_size = 0;
     if (!meta || !data || !out_size)
         return nullptr;
-    std::lock_guard<std::mutex> lk(g_mu);
-    bra_gpu_ctx_s*              c = global_ctx();
+    CtxLease       lease;
+    bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !ensure_block_arrays(c, 1) || !grow(c->d_off, c->cap_off, 4))
         return nullptr;
     if (!upload(c, data, meta->encoded_size) || !grow(c->d_tmp, c->cap_tmp, (uint64_t) meta->orig_size + 16))

@@ -23,6 +23,15 @@ uint32_t crc32c_combine_host(uint32_t a, uint32_t b, uint64_t len_b);  // == bra
 bool crc_stream_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_size, const uint8_t* d_hdr, uint32_t prev, uint32_t* d_crc,
                        hipStream_t s);
 
+// The same CRC for one shard of a stream whose chunks are spread over several devices: this
+// device's data holds global chunks g0, g0 + gstride, g0 + 2*gstride, ... back to back (chunks of
+// chunk_size bytes; only the global last chunk, which must then be this shard's last, is ragged)
+// and d_hdr their headers.  *d_crc receives the shard's share of the CRC of the whole
+// global_total-byte stream: XOR over the shards gives bra_crc32c of the stream chained from `prev`,
+// when exactly one shard passes with_init = true.  Round-robin sharding: g0 = rank, gstride = world.
+bool crc_stream_shard_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_size, const uint8_t* d_hdr, uint64_t g0, uint64_t gstride,
+                             uint64_t global_total, uint32_t prev, bool with_init, uint32_t* d_crc, hipStream_t s);
+
 // Write the .BRa chunk records (3-byte pi + 264-byte bra_huffman_t + payload, lib_bra_io_file_chunks.c:
 // 76-95,260) of nb chunks back to back into d_out.  Record b starts at payload_off[b] + 267 * b.
 bool frame_chunks_device(const uint8_t* d_hdr, const uint64_t* d_payload_off, const uint8_t* d_payload, uint32_t nb, uint8_t* d_out,
@@ -34,5 +43,24 @@ bool frame_chunks_device(const uint8_t* d_hdr, const uint64_t* d_payload_off, co
 // d_status receives {number of records, error flag}; cap is the capacity of d_hdr / d_payload_off.
 bool unframe_chunks_device(const uint8_t* d_stream, uint64_t size, uint32_t cap, uint32_t max_chunk, uint8_t* d_hdr, uint64_t* d_payload_off,
                            uint32_t* d_status, hipStream_t s);
+
+// Encoder output of up to MAX_SHARDS devices (headers, payload offsets, payloads; device memory of
+// the assembling device).  Global block g is part g % n's local block g / n with round_robin, else
+// part p holds the contiguous global blocks [first[p], first[p + 1]).
+constexpr uint32_t MAX_SHARDS = 16;
+struct ShardParts
+{
+    const uint8_t*  hdr[MAX_SHARDS];
+    const uint64_t* off[MAX_SHARDS];
+    const uint8_t*  pay[MAX_SHARDS];
+    uint32_t        first[MAX_SHARDS + 1];
+    uint32_t        n;
+    uint32_t        round_robin;
+};
+
+// Headers, payload offsets (nb + 1 entries) and payloads of all nb global blocks in global order;
+// *d_err != 0 when the payloads need more than cap bytes (the total is in d_off_out[nb]).
+bool assemble_shards_device(const ShardParts& parts, uint32_t nb, uint8_t* d_hdr_out, uint64_t* d_off_out, uint8_t* d_pay_out, uint64_t cap,
+                            uint32_t* d_err, hipStream_t s);
 
 }  // namespace bra

@@ -22,6 +22,8 @@
 // The constants (tables, powers) are generated at compile time from the polynomial.
 #include "crc.h"
 
+#include <algorithm>
+
 namespace bra {
 namespace {
 
@@ -173,6 +175,8 @@ struct StreamArgs
     uint32_t       nb;    // chunks
     uint32_t       ppc;   // pieces per chunk
     uint32_t*      crc;
+    uint64_t       g0;    // global index of local chunk 0 in the (possibly sharded) stream
+    uint64_t       gs;    // global index stride between local chunks (1 = contiguous)
 };
 
 // Workgroups [0, nb * ppc) take one 64 KiB piece of chunk data each (pieces aligned to the chunk
@@ -221,7 +225,8 @@ __global__ __launch_bounds__(CRC_TPB) void k_crc_stream(StreamArgs a, uint32_t n
 #pragma unroll
                 for (int k = 0; k < CRC_TPB / WAVE; ++k)
                     v ^= red[k];
-                const uint64_t end = (uint64_t) b * (a.cs + a.hb) + a.hb + (uint64_t) pend;  // stream position
+                const uint64_t g   = a.g0 + (uint64_t) b * a.gs;  // global chunk index
+                const uint64_t end = g * (a.cs + a.hb) + a.hb + (uint64_t) pend;  // stream position
                 const uint32_t f   = wave_x8n(a.V - end);
                 if (lane == 0)
                     atomicXor(a.crc, mulmod(v, f));
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(CRC_TPB) void k_crc_stream(StreamArgs a, uint32_t n
                 acc         = mulmod(crc16(load16(h + u, h), T), c_crc.K[HDR_UNITS - 1 - lane]);
             }
             acc                = wave_xor(acc);
-            const uint64_t end = (uint64_t) b * (a.cs + a.hb) + a.hb;
+            const uint64_t end = (a.g0 + (uint64_t) b * a.gs) * (a.cs + a.hb) + a.hb;
             const uint32_t f   = wave_x8n(a.V - end);
             if (lane == 0)
                 atomicXor(a.crc, mulmod(acc, f));
@@ -338,6 +343,98 @@ __global__ __launch_bounds__(256) void k_unframe_headers(const uint8_t* __restri
     }
 }
 
+// ---- assembly of sharded encoder output ---------------------------------------------------------
+
+// Source of global block g: part g % P at local index g / P (round robin), or the part whose
+// contiguous range holds g.
+__device__ __forceinline__ void shard_src(const ShardParts& P, uint32_t g, uint32_t& part, uint32_t& loc)
+{
+    if (P.round_robin)
+    {
+        part = g % P.n;
+        loc  = g / P.n;
+        return;
+    }
+    part = 0;
+    while (part + 1 < P.n && g >= P.first[part + 1])
+        ++part;
+    loc = g - P.first[part];
+}
+
+__device__ __forceinline__ uint32_t hdr_encoded_size(const uint8_t* h) { return rd32(h + CHUNK_HDR_MEM - 4); }
+
+// One workgroup: exclusive scan of the encoded sizes in global block order -> out offsets
+// (nb + 1 entries; the last one is the total payload).
+__global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t nb, uint64_t* __restrict__ off_out)
+{
+    __shared__ uint64_t part_sum[1024 / WAVE];
+    __shared__ uint64_t carry_s;
+    if (threadIdx.x == 0)
+        carry_s = 0;
+    __syncthreads();
+    const int lane = lane_id(), w = threadIdx.x / WAVE;
+    for (uint32_t c0 = 0; c0 < nb; c0 += 1024)
+    {
+        const uint32_t g = c0 + threadIdx.x;
+        uint64_t       v = 0;
+        if (g < nb)
+        {
+            uint32_t part, loc;
+            shard_src(P, g, part, loc);
+            v = hdr_encoded_size(P.hdr[part] + (uint64_t) CHUNK_HDR_MEM * loc);
+        }
+        uint64_t x = v;  // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1)
+        {
+            const uint64_t y = shfl_up64(x, d);
+            if (lane >= d)
+                x += y;
+        }
+        if (lane == WAVE - 1)
+            part_sum[w] = x;
+        __syncthreads();
+        uint64_t before = carry_s, all = 0;
+        for (int k = 0; k < 1024 / WAVE; ++k)
+        {
+            if (k < w)
+                before += part_sum[k];
+            all += part_sum[k];
+        }
+        if (g < nb)
+            off_out[g] = before + x - v;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            carry_s += all;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        off_out[nb] = carry_s;
+}
+
+// One workgroup per global block: its 268-byte header and payload into global order.  A block that
+// would end past `cap` is not written and sets *err.
+__global__ __launch_bounds__(256) void k_shard_copy(ShardParts P, uint32_t nb, const uint64_t* __restrict__ off_out, uint8_t* __restrict__ hdr_out,
+                                                    uint8_t* __restrict__ pay_out, uint64_t cap, uint32_t* __restrict__ err)
+{
+    for (uint32_t g = blockIdx.x; g < nb; g += gridDim.x)
+    {
+        uint32_t part, loc;
+        shard_src(P, g, part, loc);
+        const uint8_t* h = P.hdr[part] + (uint64_t) CHUNK_HDR_MEM * loc;
+        for (uint32_t i = threadIdx.x; i < CHUNK_HDR_MEM; i += blockDim.x)
+            hdr_out[(uint64_t) CHUNK_HDR_MEM * g + i] = h[i];
+        const uint64_t o = off_out[g], esz = off_out[g + 1] - o;
+        if (o + esz > cap)
+        {
+            if (threadIdx.x == 0)
+                atomicOr(err, 1u);
+            continue;
+        }
+        copy_bytes(pay_out + o, P.pay[part] + P.off[part][loc], esz);
+    }
+}
+
 }  // namespace
 
 uint32_t crc_mulmod(uint32_t a, uint32_t b) { return mulmod(a, b); }
@@ -362,10 +459,10 @@ uint32_t crc32c_host(const void* data, uint64_t len, uint32_t prev)
 
 uint32_t crc32c_combine_host(uint32_t a, uint32_t b, uint64_t len_b) { return len_b ? mulmod(a, crc_x8n(len_b)) ^ b : a; }
 
-bool crc_stream_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_size, const uint8_t* d_hdr, uint32_t prev, uint32_t* d_crc,
-                       hipStream_t s)
+bool crc_stream_shard_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_size, const uint8_t* d_hdr, uint64_t g0, uint64_t gstride,
+                             uint64_t global_total, uint32_t prev, bool with_init, uint32_t* d_crc, hipStream_t s)
 {
-    if (!d_crc || (total && !d_data))
+    if (!d_crc || (total && !d_data) || gstride == 0 || total > global_total)
         return false;
     StreamArgs a{};
     a.data  = d_data;
@@ -373,14 +470,29 @@ bool crc_stream_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_siz
     a.hdr   = d_hdr;
     a.hb    = d_hdr ? CHUNK_HDR_MEM : 0;
     a.cs    = d_hdr ? chunk_size : (1u << 30);
-    if (a.cs == 0)
+    if (a.cs == 0 || (!d_hdr && (g0 != 0 || gstride != 1 || total != global_total)))
         return false;
     a.nb  = (uint32_t) ((total + a.cs - 1) / a.cs);
     a.ppc = (a.cs + PIECE - 1) / PIECE;
-    a.V   = total + (uint64_t) a.nb * a.hb;
+    a.g0  = g0;
+    a.gs  = gstride;
+    const uint64_t nbg = (global_total + a.cs - 1) / a.cs;
+    if (a.nb && g0 + (uint64_t) (a.nb - 1) * gstride >= nbg)
+        return false;
+    if (a.nb)
+    {
+        // only the global last chunk may be ragged, and it must be this shard's last one
+        const uint64_t gl    = g0 + (uint64_t) (a.nb - 1) * gstride;
+        const uint64_t want  = std::min<uint64_t>(a.cs, global_total - gl * a.cs);
+        const uint64_t local = total - (uint64_t) (a.nb - 1) * a.cs;
+        if (want != local)
+            return false;
+    }
+    a.V   = global_total + nbg * a.hb;
     a.crc = d_crc;
-    // the result word starts as ~((~prev) * x^(8V)); every piece XORs in its raw contribution
-    const uint32_t init = ~mulmod(~prev, crc_x8n(a.V));
+    // the result word starts as ~((~prev) * x^(8V)) in exactly one shard; every piece XORs in its raw
+    // contribution moved to the end of the global stream, so the shards' words XOR to the stream CRC
+    const uint32_t init = with_init ? ~mulmod(~prev, crc_x8n(a.V)) : 0u;
     BRA_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_crc), (int) init, 1, s));
     const uint64_t n_pieces = (uint64_t) a.nb * a.ppc;
     const uint64_t n_hdr    = a.hb ? (a.nb + CRC_TPB / WAVE - 1) / (CRC_TPB / WAVE) : 0;
@@ -393,6 +505,12 @@ bool crc_stream_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_siz
     hipLaunchKernelGGL(k_crc_stream, dim3(grid), dim3(CRC_TPB), 0, s, a, (uint32_t) n_pieces, (uint32_t) n_work);
     BRA_HIP_CHECK(hipGetLastError());
     return true;
+}
+
+bool crc_stream_device(const uint8_t* d_data, uint64_t total, uint32_t chunk_size, const uint8_t* d_hdr, uint32_t prev, uint32_t* d_crc,
+                       hipStream_t s)
+{
+    return crc_stream_shard_device(d_data, total, chunk_size, d_hdr, 0, 1, total, prev, true, d_crc, s);
 }
 
 bool frame_chunks_device(const uint8_t* d_hdr, const uint64_t* d_payload_off, const uint8_t* d_payload, uint32_t nb, uint8_t* d_out,
@@ -416,6 +534,19 @@ bool unframe_chunks_device(const uint8_t* d_stream, uint64_t size, uint32_t cap,
                            d_hdr, d_status);
         BRA_HIP_CHECK(hipGetLastError());
     }
+    return true;
+}
+
+bool assemble_shards_device(const ShardParts& parts, uint32_t nb, uint8_t* d_hdr_out, uint64_t* d_off_out, uint8_t* d_pay_out, uint64_t cap,
+                            uint32_t* d_err, hipStream_t s)
+{
+    if (parts.n == 0 || parts.n > MAX_SHARDS || nb == 0)
+        return false;
+    BRA_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
+    hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(1024), 0, s, parts, nb, d_off_out);
+    BRA_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_shard_copy, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, parts, nb, d_off_out, d_hdr_out, d_pay_out, cap, d_err);
+    BRA_HIP_CHECK(hipGetLastError());
     return true;
 }
 

@@ -909,26 +909,26 @@ bool HuffWorkspace::reserve(uint32_t nblocks, uint32_t ntiles)
 {
     if (nblocks > cap_b)
     {
-        (void) hipFree(codes);
+        cap_b    = 0;
+        cap_tree = 0;  // decode buffers allocated lazily (reserve_tree)
         (void) hipFree(tree_child);
         (void) hipFree(tree_sym);
         (void) hipFree(table);
-        (void) hipFree(status);
-        cap_b = nblocks + 8;
-        BRA_HIP_CHECK(hipMalloc(&codes, (size_t) cap_b * 256 * 4));
-        tree_child = nullptr;  // decode buffers allocated lazily
+        tree_child = nullptr;
         tree_sym   = nullptr;
         table      = nullptr;
-        BRA_HIP_CHECK(hipMalloc(&status, (size_t) cap_b * 4));
-        cap_tree = 0;
+        const uint32_t c = nblocks + 8;
+        if (!dev_alloc(codes, (uint64_t) c * 256) || !dev_alloc(status, c))
+            return false;
+        cap_b = c;
     }
     if (ntiles > cap_t)
     {
-        (void) hipFree(tbits);
-        (void) hipFree(tbit0);
-        cap_t = ntiles + ntiles / 4 + 64;
-        BRA_HIP_CHECK(hipMalloc(&tbits, (size_t) cap_t * 4));
-        BRA_HIP_CHECK(hipMalloc(&tbit0, (size_t) cap_t * 8));
+        cap_t            = 0;
+        const uint32_t c = ntiles + ntiles / 4 + 64;
+        if (!dev_alloc(tbits, c) || !dev_alloc(tbit0, c))
+            return false;
+        cap_t = c;
     }
     return true;
 }
@@ -937,13 +937,11 @@ bool HuffWorkspace::reserve_tree(uint32_t nblocks)
 {
     if (nblocks <= cap_tree)
         return true;
-    (void) hipFree(tree_child);
-    (void) hipFree(tree_sym);
-    (void) hipFree(table);
+    cap_tree = 0;
+    if (!dev_alloc(tree_child, (uint64_t) nblocks * TREE_CAP * 2) || !dev_alloc(tree_sym, (uint64_t) nblocks * TREE_CAP) ||
+        !dev_alloc(table, (uint64_t) nblocks * (1u << PEEK)))
+        return false;
     cap_tree = nblocks;
-    BRA_HIP_CHECK(hipMalloc(&tree_child, (size_t) cap_tree * TREE_CAP * 8));
-    BRA_HIP_CHECK(hipMalloc(&tree_sym, (size_t) cap_tree * TREE_CAP));
-    BRA_HIP_CHECK(hipMalloc(&table, (size_t) cap_tree * (1u << PEEK) * 4));
     return true;
 }
 
@@ -951,24 +949,23 @@ bool HuffWorkspace::reserve_segs(uint32_t nseg, uint32_t nblocks)
 {
     if (nseg > cap_seg)
     {
-        (void) hipFree(seg);
-        (void) hipFree(seg_off);
-        cap_seg = nseg + nseg / 4 + 256;
-        BRA_HIP_CHECK(hipMalloc(&seg, (size_t) cap_seg * 3 * sizeof(HdSeg)));
-        BRA_HIP_CHECK(hipMalloc(&seg_off, (size_t) cap_seg * 4));
+        cap_seg          = 0;
+        const uint32_t c = nseg + nseg / 4 + 256;
+        if (!dev_alloc_bytes(seg, (uint64_t) c * 3 * sizeof(HdSeg)) || !dev_alloc(seg_off, c))
+            return false;
+        cap_seg = c;
     }
     if (nblocks + 1 > cap_segb)
     {
-        (void) hipFree(seg_base);
-        (void) hipFree(end_pos);
-        (void) hipFree(flag);
-        cap_segb = nblocks + 64;
-        BRA_HIP_CHECK(hipMalloc(&seg_base, (size_t) cap_segb * 4));
-        BRA_HIP_CHECK(hipMalloc(&end_pos, (size_t) cap_segb * 8));
-        BRA_HIP_CHECK(hipMalloc(&flag, 4));
+        cap_segb         = 0;
+        const uint32_t c = nblocks + 64;
+        if (!dev_alloc(seg_base, c) || !dev_alloc(end_pos, c) || !dev_alloc(flag, 1))
+            return false;
         if (h_flag)
             (void) hipHostFree(h_flag);
-        BRA_HIP_CHECK(hipHostMalloc(&h_flag, (size_t) (cap_segb + 1) * 4, hipHostMallocDefault));
+        h_flag = nullptr;
+        BRA_HIP_CHECK(hipHostMalloc(&h_flag, (size_t) (c + 1) * 4, hipHostMallocDefault));
+        cap_segb = c;
     }
     return true;
 }

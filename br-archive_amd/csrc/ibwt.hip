@@ -253,27 +253,28 @@ bool IbwtWorkspace::reserve(uint64_t n, uint32_t nblocks, uint32_t ntiles)
 {
     if (n > cap_n)
     {
-        (void) hipFree(T);
-        cap_n = n + n / 8 + 4096;
-        BRA_HIP_CHECK(hipMalloc(&T, cap_n * 4));
+        cap_n            = 0;
+        const uint64_t c = n + n / 8 + 4096;
+        if (!dev_alloc(T, c))
+            return false;
+        cap_n = c;
     }
     if (ntiles > cap_t)
     {
-        (void) hipFree(th);
-        cap_t = ntiles + ntiles / 4 + 64;
-        BRA_HIP_CHECK(hipMalloc(&th, (size_t) cap_t * 256 * 4));
+        cap_t            = 0;
+        const uint32_t c = ntiles + ntiles / 4 + 64;
+        if (!dev_alloc(th, (uint64_t) c * 256))
+            return false;
+        cap_t = c;
     }
     if (nblocks > cap_b)
     {
-        (void) hipFree(hop_next);
-        (void) hipFree(hop_len);
-        (void) hipFree(start);
-        (void) hipFree(cyc);
-        cap_b = nblocks + 8;
-        BRA_HIP_CHECK(hipMalloc(&hop_next, (size_t) cap_b * (MAX_SPLIT + 1) * 4));
-        BRA_HIP_CHECK(hipMalloc(&hop_len, (size_t) cap_b * (MAX_SPLIT + 1) * 4));
-        BRA_HIP_CHECK(hipMalloc(&start, (size_t) cap_b * (MAX_SPLIT + 1) * 4));
-        BRA_HIP_CHECK(hipMalloc(&cyc, (size_t) cap_b * 4));
+        cap_b            = 0;
+        const uint32_t c = nblocks + 8;
+        if (!dev_alloc(hop_next, (uint64_t) c * (MAX_SPLIT + 1)) || !dev_alloc(hop_len, (uint64_t) c * (MAX_SPLIT + 1)) ||
+            !dev_alloc(start, (uint64_t) c * (MAX_SPLIT + 1)) || !dev_alloc(cyc, c))
+            return false;
+        cap_b = c;
     }
     return true;
 }

@@ -48,19 +48,22 @@ struct Tiling
             h_count[b] = (uint32_t) h_pieces.size() - h_first[b];
         }
         n = (uint32_t) h_pieces.size();
+        key.clear();  // the cached geometry is valid only once the copies below have been issued
         if (n > cap_p)
         {
-            (void) hipFree(d_pieces);
-            cap_p = n + n / 4 + 16;
-            BRA_HIP_CHECK(hipMalloc(&d_pieces, cap_p * sizeof(Piece)));
+            cap_p          = 0;
+            const size_t c = n + n / 4 + 16;
+            if (!dev_alloc(d_pieces, c))
+                return false;
+            cap_p = c;
         }
         if (nblocks > cap_b)
         {
-            (void) hipFree(d_first);
-            (void) hipFree(d_count);
-            cap_b = nblocks + 16;
-            BRA_HIP_CHECK(hipMalloc(&d_first, cap_b * 4));
-            BRA_HIP_CHECK(hipMalloc(&d_count, cap_b * 4));
+            cap_b          = 0;
+            const size_t c = nblocks + 16;
+            if (!dev_alloc(d_first, c) || !dev_alloc(d_count, c))
+                return false;
+            cap_b = c;
         }
         BRA_HIP_CHECK(hipMemcpyAsync(d_pieces, h_pieces.data(), n * sizeof(Piece), hipMemcpyHostToDevice, s));
         BRA_HIP_CHECK(hipMemcpyAsync(d_first, h_first.data(), nblocks * 4, hipMemcpyHostToDevice, s));
@@ -92,9 +95,11 @@ struct MtfWorkspace
     {
         if (bytes <= cap_state)
             return true;
-        (void) hipFree(state);
-        cap_state = bytes + bytes / 4 + 4096;
-        BRA_HIP_CHECK(hipMalloc(&state, cap_state));
+        cap_state      = 0;
+        const size_t c = bytes + bytes / 4 + 4096;
+        if (!dev_alloc_bytes(state, c))
+            return false;
+        cap_state = c;
         return true;
     }
     void release()

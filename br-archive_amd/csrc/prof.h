@@ -37,7 +37,9 @@ struct Prof
     ~Prof();
 };
 
-extern Prof* g_prof;  // set by the C-ABI for the duration of a call
+// Set by the C-ABI for the duration of a call, per calling thread: contexts used from several
+// threads (or on several devices) each time only their own launches.
+extern thread_local Prof* g_prof;
 
 // Attribute algorithmic bytes ("algorithmic bytes") to a slot's timed launches.
 inline void prof_bytes(int slot, double b)

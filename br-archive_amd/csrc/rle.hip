@@ -534,15 +534,11 @@ bool RleWorkspace::reserve(uint32_t ntiles)
 {
     if (ntiles <= cap)
         return true;
-    (void) hipFree(runs);
-    (void) hipFree(link);
-    (void) hipFree(gaps);
-    (void) hipFree(offs);
-    cap = ntiles + ntiles / 4 + 64;
-    BRA_HIP_CHECK(hipMalloc(&runs, cap * 16));
-    BRA_HIP_CHECK(hipMalloc(&link, cap * 8));
-    BRA_HIP_CHECK(hipMalloc(&gaps, cap * 16));
-    BRA_HIP_CHECK(hipMalloc(&offs, cap * 16));
+    cap              = 0;
+    const uint64_t c = ntiles + ntiles / 4 + 64;
+    if (!dev_alloc_bytes(runs, c * 16) || !dev_alloc_bytes(link, c * 8) || !dev_alloc_bytes(gaps, c * 16) || !dev_alloc_bytes(offs, c * 16))
+        return false;
+    cap = (uint32_t) c;
     return true;
 }
 

@@ -1,53 +1,87 @@
-"""Multi-GPU sharding of the block codec (SURVEY.md 8.1 row e).
+"""Multi-GPU sharding of the block codec (SURVEY.md 8.1 row e; BASELINE configs[3]).
 
-Blocks are independent, so ranks never talk while they encode: rank r owns the contiguous block
-range `shard_blocks(...)` of the global stream (weak scaling: every rank encodes the same number of
-blocks).  The one exchange step gathers the compressed chunks to rank 0 in global block order:
+Blocks are independent, so ranks never talk while they encode.  Global block b of the input stream
+is encoded by rank b mod G (round robin, as configs[3] states); a rank's blocks sit back to back in
+its own HBM in ascending global order.  The one exchange step gathers the compressed chunks to
+rank 0:
 
   1. all_gather of each rank's payload byte count (one int64 per rank),
-  2. per peer one send/recv of its chunk headers (nblocks x 268 B, `bra_io_chunk_header_t`) and
-     one of its payload bytes, posted together with batch_isend_irecv.
+  2. per peer one send/recv of its chunk headers (nblocks x 268 B, `bra_io_chunk_header_t`), its
+     payload offsets, its payload bytes and its 4-byte share of the chunk-stream CRC, posted
+     together with batch_isend_irecv,
+  3. on rank 0, `BlockCodec.assemble_shards` interleaves the parts back into global block order on
+     the device, and the CRC shares XOR to the CRC32C of the whole chunk stream (every rank computed
+     its share with `chunks_crc32c_shard`, positions taken in the global stream).
 
 With the "nccl" backend (RCCL on ROCm) the tensors are device tensors and the copies run over
-xGMI; the same code runs with "gloo" on CPU tensors (tests/test_dist.py).
+xGMI; the same gather runs with "gloo" on CPU tensors (tests/test_dist.py), where
+`assemble_host` is the host-side interleave used to check it.
 """
 from __future__ import annotations
 
 HEADER_BYTES = 268
 
 
-def shard_blocks(nblocks_per_rank: int, rank: int) -> tuple[int, int]:
-    """Global block range [first, first + n) that `rank` encodes."""
-    return rank * nblocks_per_rank, nblocks_per_rank
+def num_blocks(total: int, block_size: int) -> int:
+    return (total + block_size - 1) // block_size
+
+
+def shard_blocks(nblocks: int, rank: int, world: int) -> list[int]:
+    """Global block indices rank `rank` encodes (round robin: b -> b mod world), ascending."""
+    return list(range(rank, nblocks, world))
+
+
+def shard_bytes(total: int, block_size: int, rank: int, world: int) -> int:
+    """Bytes of input rank `rank` holds: its blocks, only the global last one may be short."""
+    nb = num_blocks(total, block_size)
+    mine = shard_blocks(nb, rank, world)
+    if not mine:
+        return 0
+    last = mine[-1]
+    return (len(mine) - 1) * block_size + min(block_size, total - last * block_size)
 
 
 class ChunkGather:
-    """Gathers (headers, payload) of every rank to rank 0; receive buffers are kept between calls."""
+    """Gathers (headers, offsets, payload, crc share) of every rank to rank 0; receive buffers are
+    kept between calls."""
 
     def __init__(self, dist, rank: int, world: int):
         self.dist, self.rank, self.world = dist, rank, world
         self.bufs: dict[int, tuple] = {}
 
-    def __call__(self, hdr, payload_bytes, pay):
-        """hdr: uint8 [nb, 268]; payload_bytes: int64 tensor [1] (this rank's payload size);
-        pay: uint8 payload buffer.  Returns on rank 0 a list over ranks of (hdr, payload view);
-        None elsewhere."""
+    def __call__(self, hdr, off, pay, crc):
+        """hdr: uint8 [nb, 268]; off: int64 [nb + 1] (off[nb] = this rank's payload bytes); pay: uint8
+        payload buffer; crc: int32 [1] CRC share.  Returns on rank 0 a list over ranks of
+        (hdr, off, payload view, crc share); None elsewhere."""
         import torch
 
         dist, rank, world = self.dist, self.rank, self.world
-        sizes = [torch.empty_like(payload_bytes) for _ in range(world)]
-        dist.all_gather(sizes, payload_bytes)
-        sizes = [int(s.item()) for s in sizes]
+        # (payload bytes, block count) of every rank in one small all_gather
+        meta = torch.cat([off[-1:], torch.full((1,), hdr.shape[0], dtype=torch.int64, device=off.device)])
+        metas = [torch.empty_like(meta) for _ in range(world)]
+        dist.all_gather(metas, meta)
+        metas = [m.tolist() for m in metas]
+        sizes = [int(m[0]) for m in metas]
+        nbs = [int(m[1]) for m in metas]
         ops = []
         if rank == 0:
             for r in range(1, world):
-                if r not in self.bufs or self.bufs[r][1].numel() < sizes[r] or self.bufs[r][0].shape != hdr.shape:
-                    self.bufs[r] = (torch.empty_like(hdr), torch.empty((int(sizes[r] * 1.1) + 4096,), dtype=torch.uint8, device=pay.device))
-                ops.append(dist.P2POp(dist.irecv, self.bufs[r][0], r))
+                b = self.bufs.get(r)
+                if b is None or b[2].numel() < sizes[r] or b[0].shape[0] != nbs[r]:
+                    b = (torch.empty((nbs[r], HEADER_BYTES), dtype=torch.uint8, device=hdr.device),
+                         torch.empty((nbs[r] + 1,), dtype=torch.int64, device=hdr.device),
+                         torch.empty((int(sizes[r] * 1.1) + 4096,), dtype=torch.uint8, device=pay.device),
+                         torch.empty((1,), dtype=torch.int32, device=hdr.device))
+                    self.bufs[r] = b
+                ops.append(dist.P2POp(dist.irecv, b[0], r))
+                ops.append(dist.P2POp(dist.irecv, b[1], r))
+                ops.append(dist.P2POp(dist.irecv, b[3], r))
                 if sizes[r]:
-                    ops.append(dist.P2POp(dist.irecv, self.bufs[r][1][: sizes[r]], r))
+                    ops.append(dist.P2POp(dist.irecv, b[2][: sizes[r]], r))
         else:
             ops.append(dist.P2POp(dist.isend, hdr, 0))
+            ops.append(dist.P2POp(dist.isend, off, 0))
+            ops.append(dist.P2POp(dist.isend, crc, 0))
             if sizes[rank]:
                 ops.append(dist.P2POp(dist.isend, pay[: sizes[rank]], 0))
         if ops:
@@ -55,19 +89,48 @@ class ChunkGather:
                 w.wait()
         if rank != 0:
             return None
-        parts = [(hdr, pay[: sizes[0]])]
+        parts = [(hdr, off, pay[: sizes[0]], crc)]
         for r in range(1, world):
-            parts.append((self.bufs[r][0], self.bufs[r][1][: sizes[r]]))
+            b = self.bufs[r]
+            parts.append((b[0], b[1], b[2][: sizes[r]], b[3]))
         return parts
 
 
-def assemble(parts):
-    """Concatenate gathered parts in global block order: (headers [N, 268], payload, offsets [N+1])."""
+def merge_crc(parts) -> int:
+    """CRC32C of the global chunk stream from the ranks' shares (XOR; see chunks_crc32c_shard)."""
+    v = 0
+    for p in parts:
+        v ^= int(p[3].item()) & 0xFFFFFFFF
+    return v
+
+
+def assemble(codec, parts, round_robin: bool = True):
+    """Device assembly on rank 0: (headers [N, 268], offsets [N + 1], payload) in global block order."""
+    return codec.assemble_shards([(h, o, p) for h, o, p, _ in parts], round_robin=round_robin)
+
+
+def assemble_host(parts, round_robin: bool = True):
+    """Host restatement of the same interleave for CPU tensors (the gloo test checks the gather with it)."""
     import torch
 
-    hdrs = torch.cat([h for h, _ in parts], 0)
-    pays = torch.cat([p for _, p in parts], 0)
-    sizes = hdrs[:, 264:268].contiguous().view(torch.int32).to(torch.int64).flatten()  # encoded_size field
-    offs = torch.zeros(hdrs.shape[0] + 1, dtype=torch.int64, device=hdrs.device)
+    world = len(parts)
+    nbs = [int(h.shape[0]) for h, _, _, _ in parts]
+    nb = sum(nbs)
+    order = []
+    for g in range(nb):
+        if round_robin:
+            order.append((g % world, g // world))
+        else:
+            r, first = 0, 0
+            while g >= first + nbs[r]:
+                first += nbs[r]
+                r += 1
+            order.append((r, g - first))
+    hdrs = torch.stack([parts[r][0][i] for r, i in order]) if nb else torch.empty((0, HEADER_BYTES), dtype=torch.uint8)
+    pays = [parts[r][2][int(parts[r][1][i]): int(parts[r][1][i]) + int.from_bytes(parts[r][0][i, 264:268].numpy().tobytes(), "little")]
+            for r, i in order]
+    pay = torch.cat(pays) if pays else torch.empty((0,), dtype=torch.uint8)
+    sizes = torch.tensor([p.numel() for p in pays], dtype=torch.int64)
+    offs = torch.zeros(nb + 1, dtype=torch.int64)
     offs[1:] = torch.cumsum(sizes, 0)
-    return hdrs, pays, offs
+    return hdrs, offs, pay

@@ -189,6 +189,33 @@ int bra_gpu_compress_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_in, uint64_t da
 int bra_gpu_decompress_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
                               uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream);
 
+/* ---- Part 4: blocks sharded over several GPUs (SURVEY 8.1 row e) ----------------------------- */
+
+/*
+ * One shard's share of bra_gpu_chunks_crc32c over a stream whose chunks are spread over devices:
+ * this device holds global chunks first_chunk, first_chunk + chunk_stride, ... back to back in
+ * d_data[0, total) with their headers in d_headers (every chunk block_size bytes except the global
+ * last, which must then be this shard's last).  The XOR of all shards' *d_crc words is the CRC32C of
+ * the whole global_total-byte chunk stream chained from prev, when exactly one shard passes
+ * with_init != 0.  Round-robin sharding over G ranks: first_chunk = rank, chunk_stride = G.
+ */
+int bra_gpu_chunks_crc32c_shard(bra_gpu_ctx_t* ctx, const uint8_t* d_data, uint64_t total, uint32_t block_size,
+                                const bra_io_chunk_header_t* d_headers, uint64_t first_chunk, uint64_t chunk_stride, uint64_t global_total,
+                                uint32_t prev, int with_init, uint32_t* d_crc, void* stream);
+
+/*
+ * Assemble the bra_gpu_encode_blocks outputs of nparts (<= 16) shards, all resident on this
+ * context's device, into global block order: headers, payload offsets (N + 1 entries, N = sum of
+ * nblocks[]) and payloads back to back.  round_robin != 0: global block g is shard g % nparts's
+ * block g / nparts; otherwise shard p holds the next nblocks[p] blocks.  Returns 0, -2 when the
+ * payloads need more than payload_cap bytes (the need is in d_payload_off_out[N]), -1 on error.
+ * Completes before returning.
+ */
+int bra_gpu_assemble_shards(bra_gpu_ctx_t* ctx, uint32_t nparts, const bra_io_chunk_header_t* const* d_headers,
+                            const uint64_t* const* d_payload_off, const uint8_t* const* d_payload, const uint32_t* nblocks, int round_robin,
+                            bra_io_chunk_header_t* d_headers_out, uint64_t* d_payload_off_out, uint8_t* d_payload_out, uint64_t payload_cap,
+                            void* stream);
+
 /*
  * Device pointers to the intermediate stage outputs of the last bra_gpu_encode_blocks call (for
  * parity tests): 0 = BWT last column (total bytes), 1 = MTF (total bytes), 2 = RLE output (block b

@@ -210,3 +210,30 @@ def test_full_size_chunk_stream(bra, codec):
     out, dcrc = codec.decompress_chunks(stream, CS, out_cap=total)
     assert torch.equal(out, d)
     assert dcrc == crc
+
+
+@pytest.mark.parametrize("world,nblocks,tail", [(3, 10, 777), (8, 16, 0), (2, 3, CS - 1)])
+def test_round_robin_shards_assemble_and_crc(bra, codec, world, nblocks, tail):
+    """configs[3] on one GPU: global block b encoded by "rank" b mod G, CRC shares computed in the
+    global stream, parts assembled in global order == one encode of the whole stream + its chunk CRC."""
+    import torch
+
+    dmod = importlib.import_module("br-archive_amd.dist")
+    total = (nblocks - 1) * CS + (tail or CS)
+    d_all = torch.from_numpy(bra.synth_fill(0, total, CS)).cuda()
+    H, O, P = codec.encode(d_all, CS)
+    want_crc = codec.chunks_crc32c(d_all, H, CS)
+    parts = []
+    for r in range(world):
+        nbytes = dmod.shard_bytes(total, CS, r, world)
+        d = torch.from_numpy(bra.synth_fill(0, nbytes, CS, first_block=r, stride=world)).cuda()
+        h, o, p = codec.encode(d, CS)
+        c = codec.chunks_crc32c_shard(d, h, CS, r, world, total, r == 0)
+        parts.append((h, o, p[: int(o[-1].item())], c))
+    h2, o2, p2 = dmod.assemble(codec, parts, round_robin=True)
+    assert torch.equal(h2, H) and torch.equal(o2, O[: nblocks + 1])
+    assert torch.equal(p2[: int(O[nblocks].item())], P[: int(O[nblocks].item())])
+    assert dmod.merge_crc(parts) == want_crc
+    # too small a payload buffer is reported, not overrun
+    with pytest.raises(RuntimeError):
+        codec.assemble_shards([(h, o, p) for h, o, p, _ in parts], payload=torch.empty((16,), dtype=torch.uint8, device="cuda"))
