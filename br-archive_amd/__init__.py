@@ -38,6 +38,7 @@ ABI_SYMBOLS = (
     "bra_gpu_prof_enable", "bra_gpu_prof_reset", "bra_gpu_prof_read",
     "bra_gpu_crc32c", "bra_gpu_chunks_crc32c", "bra_gpu_crc32c_combine", "bra_gpu_entry_crc32c", "bra_gpu_chunks_bound",
     "bra_gpu_frame_chunks", "bra_gpu_unframe_chunks", "bra_gpu_compress_chunks", "bra_gpu_decompress_chunks",
+    "bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host",
     "bra_gpu_chunks_crc32c_shard", "bra_gpu_assemble_shards",
 )
 MAX_CHUNK_SIZE = 256 * 1024  # BRA_MAX_CHUNK_SIZE (src/lib_bra_defs.h:93): the .BRa chunk size

@@ -193,16 +193,48 @@ __device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ blk, uint
     return (k & 0xFFFFFFFFFF000000ull) | idx;
 }
 
-// Start of an MSD level.
-// Counters a level's kernels accumulate from zero.  Nothing reads a counter on the device in a
-// later kernel: the host passes the counts (the tile count of a level, say) as kernel arguments,
-// because a plain load in the next kernel can return a stale copy of an atomically updated line.
-__global__ void k_level_start(Counters* ctr)
+// Counters of one call: slot 0 holds the call-wide lists (jobs, workgroup jobs, fallback groups,
+// overflow); slot k >= 1 holds what the scan of MSD level k - 1 appended for level k (n_big,
+// n_tiles_next, and the byte-accounting counts).  Every slot is zeroed once, by k_ctr_init at the
+// start of the call (or of a fallback round), so no kernel ever resets a counter a later kernel
+// reads, and the host never has to copy a level's counts back before it launches the next level.
+constexpr uint32_t MAX_LEVELS = DCAP_BIG + 2;  // slot 0 + one per STRING level (depth <= DCAP_BIG)
+
+__global__ void k_ctr_init(Counters* ctr, uint32_t nslots)
 {
-    ctr->n_tiles_next = 0;
-    ctr->n_elems_next = 0;
-    ctr->n_big        = 0;
-    ctr->n_moved      = 0;
+    uint32_t* w = reinterpret_cast<uint32_t*>(ctr);
+    for (uint32_t i = threadIdx.x; i < nslots * (uint32_t) (sizeof(Counters) / 4); i += blockDim.x)
+        w[i] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        ctr[0].hmin = 0xFFFFFFFFu;
+}
+
+// A count an earlier kernel of the call accumulated with device-scope atomics.  Read with an
+// agent-scope atomic load (global_load sc1: never served from a CU's L1 or the scalar cache) instead
+// of a plain load, which the compiler may turn into a scalar load through the non-coherent K$.
+__device__ __forceinline__ uint32_t dev_count(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Host mailbox record: a level's counts, written by k_publish into pinned host memory so the host
+// can follow the level loop without a copy or a stream synchronisation.  `seq` is stored last.
+struct Mail
+{
+    uint32_t n_big, n_tiles, overflow, n_groups, hmin, n_jobs, n_mjobs, seq;
+};
+
+__global__ void k_publish(const Counters* __restrict__ g, const Counters* __restrict__ lv, Mail* __restrict__ mail, uint32_t seq)
+{
+    if (threadIdx.x != 0)
+        return;
+    const uint32_t v[7] = {lv ? dev_count(&lv->n_big) : 0u, lv ? dev_count(&lv->n_tiles_next) : 0u, dev_count(&g->overflow), dev_count(&g->n_groups),
+                           dev_count(&g->hmin),  dev_count(&g->n_jobs),  dev_count(&g->n_mjobs)};
+    uint32_t* m = reinterpret_cast<uint32_t*>(mail);
+    for (int i = 0; i < 7; ++i)
+        __hip_atomic_store(m + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mail->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -269,9 +301,10 @@ template <uint32_t MODE>
 __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
                                               const uint64_t* __restrict__ key0, const uint64_t* __restrict__ key1,
                                               const uint32_t* __restrict__ pay0, const uint32_t* __restrict__ pay1,
-                                              uint32_t* __restrict__ tile_hist, uint32_t ntiles, TileOrder to,
+                                              uint32_t* __restrict__ tile_hist, const Counters* __restrict__ lv, TileOrder to,
                                               const uint8_t* __restrict__ dig0, const uint8_t* __restrict__ dig1)
 {
+    const uint32_t ntiles = dev_count(&lv->n_tiles_next);
     __shared__ uint32_t h[256];
     __shared__ uint32_t hc[SCATTER_NC * CSTRIDE];  // per-copy counters (copy = lane & (NC - 1), see TileStagePN)
     if (MODE == MODE_STRING && BRA_HIST_PIPE)
@@ -401,10 +434,12 @@ struct ScanArgs
     uint32_t        cap_mjobs;
     Group*          groups;
     uint32_t        cap_groups;
-    Counters*       ctr;
+    Counters*       ctr;       // call-wide lists (slot 0)
     uint32_t        dcap;      // STRING: depth cap for big buckets
     uint32_t        account;   // keep the byte-accounting counters (profiling)
     uint32_t        mjob_max;  // largest workgroup job (256 * waves; JOB_MAX = no workgroup jobs)
+    const Counters* lin;       // this level's bucket count (n_big); null: nbuckets (level 0)
+    Counters*       lout;      // the next level's buckets / tiles / byte accounting
 };
 
 constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into one wave job
@@ -437,10 +472,11 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
     __shared__ ScanWaveCounts cnt_s[SCAN_WAVES];
     __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
     const int                 lane = lane_id(), w = threadIdx.x >> 6;
-    for (uint32_t b0 = blockIdx.x * SCAN_WAVES; b0 < a.nbuckets; b0 += gridDim.x * SCAN_WAVES)
+    const uint32_t            nbuckets = a.lin ? dev_count(&a.lin->n_big) : a.nbuckets;
+    for (uint32_t b0 = blockIdx.x * SCAN_WAVES; b0 < nbuckets; b0 += gridDim.x * SCAN_WAVES)
     {
         const uint32_t bi     = b0 + w;
-        const bool     active = bi < a.nbuckets;
+        const bool     active = bi < nbuckets;
         Bucket         B{};
         if (active)
             B = a.buckets[bi];
@@ -650,7 +686,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
             if (tb)
             {
                 const unsigned long long old =
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_big), ((unsigned long long) tt << 32) | tb);
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.lout->n_big), ((unsigned long long) tt << 32) | tb);
                 pre[2] = (uint32_t) old;
                 pre[3] = (uint32_t) (old >> 32);
             }
@@ -663,11 +699,11 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
             if (a.account)
             {
                 if (T.moved)
-                    atomicAdd(&a.ctr->n_moved, T.moved);
+                    atomicAdd(&a.lout->n_moved, T.moved);
                 if (T.melems)
                     atomicAdd(&a.ctr->n_melems, T.melems);
                 if (T.elems_next)
-                    atomicAdd(&a.ctr->n_elems_next, T.elems_next);
+                    atomicAdd(&a.lout->n_elems_next, T.elems_next);
             }
             for (int v = 0; v < SCAN_WAVES; ++v)
                 for (int q = 0; q < 5; ++q)
@@ -942,11 +978,12 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
 // payloads are re-gathered in place.
 __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ pay0,
-                                                   uint64_t* __restrict__ pay1, uint32_t ntiles, TileOrder to, uint8_t* __restrict__ dig0,
-                                                   uint8_t* __restrict__ dig1)
+                                                   uint64_t* __restrict__ pay1, const Counters* __restrict__ lv, TileOrder to,
+                                                   uint8_t* __restrict__ dig0, uint8_t* __restrict__ dig1)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStageS& S = *reinterpret_cast<TileStageS*>(smem);
+    TileStageS&    S      = *reinterpret_cast<TileStageS*>(smem);
+    const uint32_t ntiles = dev_count(&lv->n_tiles_next);
     for (uint32_t it = 0;; ++it)
     {
         const uint32_t p = tile_pos(to, it, ntiles);
@@ -1049,13 +1086,14 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
 
 // RANK-mode MSD scatter (fallback rounds): 8-byte keys + payloads.
 __global__ void __launch_bounds__(TPB) k_scatter(const Bucket* __restrict__ buckets, const uint8_t* __restrict__ nomove,
-                                                 const uint32_t* __restrict__ tile_bucket, const Counters* __restrict__ ctr,
+                                                 const uint32_t* __restrict__ tile_bucket, const Counters* __restrict__ lv,
                                                  const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ key0,
                                                  uint64_t* __restrict__ key1, uint32_t* __restrict__ pay0, uint32_t* __restrict__ pay1,
-                                                 uint32_t mode, uint32_t ntiles)
+                                                 uint32_t mode)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStage& S = *reinterpret_cast<TileStage*>(smem);
+    TileStage&     S      = *reinterpret_cast<TileStage*>(smem);
+    const uint32_t ntiles = dev_count(&lv->n_tiles_next);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const uint32_t bi = tile_bucket[t];
@@ -1126,6 +1164,7 @@ struct JobArgs
     uint32_t         hstep;    // RANK mode: depth added to a subgroup (min depth of the round)
     uint32_t         xcd_major;  // jobs ordered by job_order(): XCD x works on jobs [xseg[x], xseg[x+1])
     uint32_t         xseg[9];
+    const uint32_t*  dxseg;    // non-null: the per-XCD list ranges live in device memory (k_job_prefix), not in xseg
     uint32_t*        jq;       // dynamic order (xcd_major only): per-XCD claim counters, 32 dwords apart; null = static ranges
     uint32_t         jq_chunk; // jobs a wave claims at once
 };
@@ -1151,11 +1190,11 @@ struct JobClaim
 };
 
 // Called by a whole wave (wave-uniform control flow; lane 0 performs the atomic).
-__device__ __forceinline__ bool job_claim(const JobArgs& a, JobClaim& c, uint32_t chunk, uint32_t& first, uint32_t& end)
+__device__ __forceinline__ bool job_claim(const JobArgs& a, const uint32_t* xs, JobClaim& c, uint32_t chunk, uint32_t& first, uint32_t& end)
 {
     while (c.t < 8)
     {
-        const uint32_t x = (c.x0 + c.t) & 7u, lo = a.xseg[x], hi = a.xseg[x + 1];
+        const uint32_t x = (c.x0 + c.t) & 7u, lo = xs[x], hi = xs[x + 1];
         uint32_t       b = 0;
         if (lane_id() == 0)
             b = atomicAdd(&a.jq[x * 32], chunk);
@@ -1171,6 +1210,15 @@ __device__ __forceinline__ bool job_claim(const JobArgs& a, JobClaim& c, uint32_
     return false;
 }
 
+// The per-XCD list ranges into LDS (from device memory when k_job_prefix computed them, else from
+// the kernel arguments); every thread of the workgroup calls it.
+__device__ __forceinline__ void load_xseg(const JobArgs& a, uint32_t* xs)
+{
+    if (threadIdx.x < 9)
+        xs[threadIdx.x] = a.dxseg ? dev_count(a.dxseg + threadIdx.x) : a.xseg[threadIdx.x];
+    __syncthreads();
+}
+
 // Job index ranges per workgroup.  With xcd_major, workgroup w runs on XCD w % 8 (the dispatcher's
 // round-robin; only speed depends on it) and walks that XCD's list, where the jobs of the blocks
 // b = x (mod 8) are stored in block order: the workgroups of one XCD then gather from the same one
@@ -1180,12 +1228,12 @@ struct JobRange
     uint32_t first, end, step;
 };
 
-__device__ __forceinline__ JobRange job_range(const JobArgs& a, uint32_t unit, uint32_t units_per_wg)
+__device__ __forceinline__ JobRange job_range(const JobArgs& a, const uint32_t* xs, uint32_t unit, uint32_t units_per_wg)
 {
     if (a.xcd_major)
     {
         const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, g = gridDim.x >> 3;
-        return JobRange{a.xseg[x] + l * units_per_wg + unit, a.xseg[x + 1], g * units_per_wg};
+        return JobRange{xs[x] + l * units_per_wg + unit, xs[x + 1], g * units_per_wg};
     }
     return JobRange{blockIdx.x * units_per_wg + unit, a.njobs, gridDim.x * units_per_wg};
 }
@@ -1821,9 +1869,11 @@ template <uint32_t MODE>
 __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
 {
     __shared__ JobLds<1> lds[4];
+    __shared__ uint32_t  xs[9];
+    load_xseg(a, xs);
     const int      wl  = threadIdx.x >> 6;
     const bool     dyn = a.xcd_major && a.jq;
-    const JobRange R   = job_range(a, wl, 4);
+    const JobRange R   = job_range(a, xs, wl, 4);
     JobClaim       c{xcc_id(), 0};
     uint32_t       end = 0;
     // one call site of job_run, in a plain while loop (other loop shapes raised the register
@@ -1834,7 +1884,7 @@ __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
         if (j + 1 < end)
             return j + 1;
         uint32_t first = 0;
-        return job_claim(a, c, a.jq_chunk, first, end) ? first : ~0u;
+        return job_claim(a, xs, c, a.jq_chunk, first, end) ? first : ~0u;
     };
     uint32_t j = dyn ? next(~0u) : (R.first < R.end ? R.first : ~0u);
     while (j != ~0u)
@@ -1850,8 +1900,10 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     JobLds<W>&     S   = *reinterpret_cast<JobLds<W>*>(smem);
     uint32_t*      claim = reinterpret_cast<uint32_t*>(smem + sizeof(JobLds<W>));  // 2 own LDS words (launch adds 16 bytes)
+    __shared__ uint32_t xs[9];
+    load_xseg(a, xs);
     const bool     dyn   = a.xcd_major && a.jq;
-    const JobRange R     = job_range(a, 0, 1);
+    const JobRange R     = job_range(a, xs, 0, 1);
     JobClaim       c{xcc_id(), 0};
     uint32_t       k = 0;
     // Dynamic order: wave 0 claims the next job into claim[k & 1] and one barrier publishes it (the
@@ -1865,7 +1917,7 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
         if (__builtin_amdgcn_readfirstlane(threadIdx.x) == 0)  // wave 0
         {
             uint32_t first = 0, end = 0;
-            const bool ok = job_claim(a, c, 1, first, end);
+            const bool ok = job_claim(a, xs, c, 1, first, end);
             if (lane_id() == 0)
                 claim[k & 1] = ok ? first : ~0u;
         }
@@ -1895,10 +1947,11 @@ constexpr uint32_t JOB_CHUNK = 4096;  // jobs per workgroup of the ordering kern
 // Per-key job counts.  Each workgroup counts a chunk of the list in LDS and adds its nonzero counts
 // to the global ones (one atomic per key and workgroup instead of one per job: thousands of jobs of
 // one block share a key, and same-address device atomics serialise).  nkeys <= lds capacity.
-__global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs, uint32_t n, uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys,
-                                                   uint32_t* __restrict__ cnt)
+__global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q,
+                                                   uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cnt)
 {
     extern __shared__ uint32_t h[];
+    const uint32_t n = dev_count(pn);
     for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
         for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
@@ -1917,10 +1970,11 @@ __global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs,
 
 // Scatter into key order: per chunk, local ranks from LDS atomics, one global cursor reservation per
 // nonzero key and workgroup.  (Job order within a key only affects speed.)
-__global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in, uint32_t n, uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys,
-                                                     uint32_t* __restrict__ cursor, Job* __restrict__ out)
+__global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in, const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q,
+                                                     uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cursor, Job* __restrict__ out)
 {
     extern __shared__ uint32_t h[];
+    const uint32_t n = dev_count(pn);
     constexpr int PT = JOB_CHUNK / 256;
     for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
@@ -1960,10 +2014,11 @@ __global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in,
 // order, so the digit gathers of the scatter hit the one or two blocks its XCD's L2 holds.
 __device__ __forceinline__ uint32_t tile_key(uint32_t block, uint32_t kb, uint32_t q) { return (block & 7u) * kb + (block >> 3) / q; }
 
-__global__ void __launch_bounds__(256) k_tile_count(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket, uint32_t n,
-                                                    uint32_t kb, uint32_t q, uint32_t nkeys, uint32_t* __restrict__ cnt)
+__global__ void __launch_bounds__(256) k_tile_count(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
+                                                    const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q, uint32_t nkeys, uint32_t* __restrict__ cnt)
 {
     extern __shared__ uint32_t h[];
+    const uint32_t n = dev_count(pn);
     for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
         for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
@@ -2010,12 +2065,57 @@ __global__ void __launch_bounds__(256) k_tile_prefix(const uint32_t* __restrict_
         xseg[8] = carry;
 }
 
-__global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket, uint32_t n,
-                                                      uint32_t kb, uint32_t q, uint32_t nkeys, uint32_t* __restrict__ cursor,
-                                                      const BlockDesc* __restrict__ blocks, const TileDesc* __restrict__ nat,
-                                                      TileDesc* __restrict__ order)
+// One workgroup: the job lists' key counts cnt[list][class][nkeys] (k_job_count) -> cursors of the same
+// layout and the per-XCD ranges of the three job launches, seg[16 * k + x] (x = 0..8): k = 0 the
+// wave jobs, k = 1 / 2 the workgroup jobs of the small / large size class.  The two classes of a
+// list are stored one after the other (class 1 after class 0).
+__global__ void __launch_bounds__(256) k_job_prefix(const uint32_t* __restrict__ cnt, uint32_t nkeys, uint32_t kb, uint32_t* __restrict__ cursor,
+                                                    uint32_t* __restrict__ seg)
+{
+    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t carry;
+    for (uint32_t l = 0; l < 2; ++l)
+    {
+        if (threadIdx.x == 0)
+            carry = 0;
+        __syncthreads();
+        for (uint32_t c = 0; c < 2; ++c)
+        {
+            const bool      used = (l == 1 || c == 0);
+            uint32_t*       xs   = seg + 16 * (l == 0 ? 0 : 1 + c);
+            const uint32_t* hc   = cnt + ((size_t) l * 2 + c) * nkeys;
+            uint32_t*       hu   = cursor + ((size_t) l * 2 + c) * nkeys;
+            for (uint32_t k0 = 0; k0 < nkeys; k0 += 256)
+            {
+                const uint32_t k = k0 + threadIdx.x;
+                const uint32_t v = k < nkeys ? hc[k] : 0u;
+                uint32_t       tot;
+                const uint32_t ex = block256_exclusive_sum(v, tmp, &tot) + carry;
+                if (k < nkeys)
+                {
+                    hu[k] = ex;
+                    if (used && k % kb == 0)
+                        xs[k / kb] = ex;
+                }
+                __syncthreads();
+                if (threadIdx.x == 0)
+                    carry += tot;
+                __syncthreads();
+            }
+            if (used && threadIdx.x == 0)
+                xs[8] = carry;
+            __syncthreads();
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
+                                                      const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q, uint32_t nkeys,
+                                                      uint32_t* __restrict__ cursor, const BlockDesc* __restrict__ blocks,
+                                                      const TileDesc* __restrict__ nat, TileDesc* __restrict__ order)
 {
     extern __shared__ uint32_t h[];
+    const uint32_t n = dev_count(pn);
     constexpr int PT = JOB_CHUNK / 256;
     for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
@@ -2144,7 +2244,8 @@ __global__ void k_rank_keys(const Group* __restrict__ groups, uint32_t ng, const
 // group, one wave job per small group.
 __global__ void k_groups_to_work(const Group* __restrict__ groups, uint32_t ng, Bucket* __restrict__ big, uint32_t cap_big,
                                  uint32_t* __restrict__ tile_bucket, uint32_t cap_tiles, Job* __restrict__ jobs, uint32_t cap_jobs,
-                                 Job* __restrict__ mjobs, uint32_t cap_mjobs, uint32_t mjob_max, Counters* __restrict__ ctr)
+                                 Job* __restrict__ mjobs, uint32_t cap_mjobs, uint32_t mjob_max, Counters* __restrict__ ctr,
+                                 Counters* __restrict__ lout)
 {
     for (uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x; gi < ng; gi += gridDim.x * blockDim.x)
     {
@@ -2154,7 +2255,7 @@ __global__ void k_groups_to_work(const Group* __restrict__ groups, uint32_t ng, 
         {
             const uint32_t ntl = div_up(G.len, TILE);
             const unsigned long long old =
-                atomicAdd(reinterpret_cast<unsigned long long*>(&ctr->n_big), ((unsigned long long) ntl << 32) | 1ull);
+                atomicAdd(reinterpret_cast<unsigned long long*>(&lout->n_big), ((unsigned long long) ntl << 32) | 1ull);
             const uint32_t s = (uint32_t) old, t0 = (uint32_t) (old >> 32);
             if (s < cap_big && t0 + ntl <= cap_tiles)
             {
@@ -2239,22 +2340,29 @@ struct BwtWorkspace
     uint8_t*  nomove         = nullptr;
     uint8_t*  flag           = nullptr;
     Bucket*   big[2]         = {nullptr, nullptr};
+    Bucket*   l0b            = nullptr;  // level-0 buckets (one per block), kept for the cached geometry
     Job*      jobs           = nullptr;
     Job*      mjobs          = nullptr;
     Job*      jobs_sorted    = nullptr;  // block-major, XCD-major copies (order_jobs)
     Job*      mjobs_sorted   = nullptr;
     uint32_t* job_cnt        = nullptr;  // 2 lists x 2 size classes x 8 * ceil(blocks / 8) keys, then the cursors
-    uint32_t* h_job_cnt      = nullptr;  // pinned: counts back, cursors out
+    uint32_t* jseg           = nullptr;  // per-XCD ranges of the three job launches (k_job_prefix), 3 x 16 dwords
     uint32_t* tile_cnt       = nullptr;  // MSD tile order: key counts, cursors, xseg[9]
     TileDesc* tile_order     = nullptr;
-    TileDesc* tdesc[2]       = {nullptr, nullptr};
-    uint8_t*  dig[2]         = {nullptr, nullptr};  // STRING: digit of the current level beside each payload of key[b]  // STRING: tile-order descriptors written by the scan (per level, ping-pong)
+    TileDesc* tdesc[2]       = {nullptr, nullptr};  // STRING: tile-order descriptors written by the scan (per level, ping-pong)
+    uint8_t*  dig[2]         = {nullptr, nullptr};  // STRING: digit of the current level beside each payload of key[b]
     Group*    groups[2]      = {nullptr, nullptr};
-    Counters* ctr            = nullptr;
-    Counters* h_ctr          = nullptr;  // pinned
+    Counters* ctr            = nullptr;  // MAX_LEVELS slots: [0] call-wide lists, [k] level k's buckets
+    Counters* h_ctr          = nullptr;  // pinned copy (byte accounting when profiling)
+    Mail*     h_mail         = nullptr;  // pinned, device-written mailbox records (one per level slot)
+    uint32_t  mail_seq       = 0;
     L0Tile*   l0tiles        = nullptr;
+    std::vector<BlockDesc> geo;          // block geometry the level-0 tiles / buckets on the device were built for
+    uint32_t  nt0 = 0;
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
     int       grid = 16384;  // workgroups of the MSD / level-0 tile kernels (env BRA_GRID; 2048: 11.9, 8192: 12.3, 16384: 12.5 GB/s)
+    uint32_t  scan_grid = 4096;         // workgroups of a level's scan (4 buckets each per pass; env BRA_SCAN_GRID)
+    uint32_t  lookahead = 2;            // MSD levels enqueued before the host has seen the bucket count they consume (env BRA_LOOKAHEAD)
     int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
     uint32_t  jobs_grid = 2048;         // workgroups of the wave-job launch (env BRA_JOBS_GRID): about the resident
                                         // capacity (6 waves/SIMD = 1536 four-wave groups); with the dynamic job
@@ -2264,70 +2372,105 @@ struct BwtWorkspace
     int       tile_order_mode = 1;      // MSD tile order: 0 scan order, 1 XCD-major on re-gather levels, 2 always (env BRA_TILE_ORDER)
     uint32_t  jobq_chunk = 2;           // wave jobs claimed at once (env BRA_JOBQ_CH)
     uint32_t  nblocks   = 0;            // blocks of the current call
+    uint32_t  levels    = 0;            // MSD levels enqueued by the last STRING level loop
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
-// Reorder the wave-job and workgroup-job lists block-major per XCD (see job_range): count jobs per
-// key on the device, prefix on the host (the counts come back with one small copy), scatter.  The
-// workgroup jobs are also split into two size classes (<= half the workgroup-job size, larger):
-// out[0] wave jobs, out[1] small workgroup jobs, out[2] large ones.
+// ---- host mailbox ----
+// k_publish writes the call counters and one level slot into a pinned record; the host spins on the
+// record's sequence number.  Nothing is copied and the stream is not synchronised, so the device
+// keeps running the levels enqueued ahead while the host reads.
+static uint32_t post(BwtWorkspace& w, uint32_t slot, hipStream_t s)
+{
+    if (++w.mail_seq == 0)
+        w.mail_seq = 1;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, w.ctr, slot ? w.ctr + slot : nullptr, w.h_mail + slot, w.mail_seq);
+    return w.mail_seq;
+}
+
+static bool wait_mail(BwtWorkspace& w, uint32_t slot, uint32_t seq, hipStream_t s, Mail& out)
+{
+    Mail* m = w.h_mail + slot;
+    for (uint32_t i = 1;; ++i)
+    {
+        if (__atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) == seq)
+        {
+            out.n_big    = __atomic_load_n(&m->n_big, __ATOMIC_RELAXED);
+            out.n_tiles  = __atomic_load_n(&m->n_tiles, __ATOMIC_RELAXED);
+            out.overflow = __atomic_load_n(&m->overflow, __ATOMIC_RELAXED);
+            out.n_groups = __atomic_load_n(&m->n_groups, __ATOMIC_RELAXED);
+            out.hmin     = __atomic_load_n(&m->hmin, __ATOMIC_RELAXED);
+            out.n_jobs   = __atomic_load_n(&m->n_jobs, __ATOMIC_RELAXED);
+            out.n_mjobs  = __atomic_load_n(&m->n_mjobs, __ATOMIC_RELAXED);
+            out.seq      = seq;
+            if (out.overflow)
+            {
+                bra_hip_report("bwt: work list overflow");
+                return false;
+            }
+            return true;
+        }
+        if ((i & 255) == 0)
+        {
+            // a launch failed or the stream drained without the record: report instead of spinning forever
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess && __atomic_load_n(&m->seq, __ATOMIC_ACQUIRE) != seq)
+            {
+                bra_hip_report("bwt: mailbox record %u never arrived", slot);
+                return false;
+            }
+            if (q != hipSuccess && q != hipErrorNotReady)
+            {
+                bra_hip_report("bwt: stream error while waiting for level counts: %s", hipGetErrorString(q));
+                return false;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+static bool post_wait(BwtWorkspace& w, uint32_t slot, hipStream_t s, Mail& out)
+{
+    const uint32_t seq = post(w, slot, s);
+    return wait_mail(w, slot, seq, s, out);
+}
+
+// Reorder the wave-job and workgroup-job lists block-major per XCD (see job_range), all on the
+// device: count jobs per key, k_job_prefix (cursors + the three launches' per-XCD ranges), scatter.
+// The workgroup jobs are also split into two size classes (<= half the workgroup-job size, larger):
+// out[0] wave jobs, out[1] small workgroup jobs, out[2] large ones.  The job counts are read on the
+// device (counters slot 0), so the host never waits for them.
 static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[3], hipStream_t s)
 {
-    const uint32_t kb0 = div_up(nblocks, 8), q = div_up(kb0, 1024u);
-    const uint32_t kb = div_up(kb0, q), nk = 8 * kb;  // keys per size class (<= 8192)
-    const uint32_t n[2]     = {ja.njobs, jm.njobs};
-    const uint32_t split[2] = {0, w.mjob_max() / 2};
-    const Job*     src[2]   = {w.jobs, w.mjobs};
-    Job*           dst[2]   = {w.jobs_sorted, w.mjobs_sorted};
-    uint32_t*      dcnt     = w.job_cnt;                    // [list][class][nk] counts
-    uint32_t*      dcur     = w.job_cnt + 4 * (size_t) nk;  // cursors, same layout
+    const uint32_t  kb0 = div_up(nblocks, 8), q = div_up(kb0, 1024u);
+    const uint32_t  kb = div_up(kb0, q), nk = 8 * kb;  // keys per size class (<= 8192)
+    const uint32_t  split[2] = {0, w.mjob_max() / 2};
+    const Job*      src[2]   = {w.jobs, w.mjobs};
+    Job*            dst[2]   = {w.jobs_sorted, w.mjobs_sorted};
+    const uint32_t* pn[2]    = {&w.ctr[0].n_jobs, &w.ctr[0].n_mjobs};
+    uint32_t*       dcnt     = w.job_cnt;                    // [list][class][nk] counts
+    uint32_t*       dcur     = w.job_cnt + 4 * (size_t) nk;  // cursors, same layout
+    const dim3      g(1024);
     BRA_HIP_CHECK(hipMemsetAsync(dcnt, 0, 4 * (size_t) nk * 4, s));
     for (int l = 0; l < 2; ++l)
-        if (n[l])
-        {
-            hipLaunchKernelGGL(k_job_count, dim3(std::min<uint32_t>(div_up(n[l], JOB_CHUNK), 2048u)), dim3(256), 2 * nk * 4, s, src[l], n[l], kb,
-                               q, split[l], 2 * nk, dcnt + (size_t) l * 2 * nk);
-            BRA_DSYNC(s);
-        }
-    BRA_HIP_CHECK(hipMemcpyAsync(w.h_job_cnt, dcnt, 4 * (size_t) nk * 4, hipMemcpyDeviceToHost, s));
-    BRA_HIP_CHECK(hipStreamSynchronize(s));
-    uint32_t* cur = w.h_job_cnt + 4 * (size_t) nk;
-    out[0]        = ja;
-    out[1]        = jm;
-    out[2]        = jm;
+    {
+        hipLaunchKernelGGL(k_job_count, g, dim3(256), 2 * nk * 4, s, src[l], pn[l], kb, q, split[l], 2 * nk, dcnt + (size_t) l * 2 * nk);
+        BRA_DSYNC(s);
+    }
+    hipLaunchKernelGGL(k_job_prefix, dim3(1), dim3(256), 0, s, dcnt, nk, kb, dcur, w.jseg); BRA_DSYNC(s);
     for (int l = 0; l < 2; ++l)
     {
-        uint32_t run = 0;
-        for (uint32_t c = 0; c < 2; ++c)
-        {
-            const bool used = (l == 1 || c == 0);
-            JobArgs&   A    = out[l == 0 ? 0 : 1 + c];
-            uint32_t*  hc   = w.h_job_cnt + ((size_t) l * 2 + c) * nk;
-            uint32_t*  hu   = cur + ((size_t) l * 2 + c) * nk;
-            for (uint32_t k = 0; k < nk; ++k)
-            {
-                if (used && k % kb == 0)
-                    A.xseg[k / kb] = run;
-                hu[k] = run;
-                run += hc[k];
-            }
-            if (used)
-            {
-                A.xseg[8]   = run;
-                A.xcd_major = 1;
-                A.jobs      = dst[l];
-                A.njobs     = run - A.xseg[0];
-            }
-        }
+        hipLaunchKernelGGL(k_job_scatter, g, dim3(256), 2 * nk * 4, s, src[l], pn[l], kb, q, split[l], 2 * nk, dcur + (size_t) l * 2 * nk, dst[l]);
+        BRA_DSYNC(s);
     }
-    BRA_HIP_CHECK(hipMemcpyAsync(dcur, cur, 4 * (size_t) nk * 4, hipMemcpyHostToDevice, s));
-    for (int l = 0; l < 2; ++l)
-        if (n[l])
-        {
-            hipLaunchKernelGGL(k_job_scatter, dim3(std::min<uint32_t>(div_up(n[l], JOB_CHUNK), 2048u)), dim3(256), 2 * nk * 4, s, src[l], n[l], kb,
-                               q, split[l], 2 * nk, dcur + (size_t) l * 2 * nk, dst[l]);
-            BRA_DSYNC(s);
-        }
+    for (int k = 0; k < 3; ++k)
+    {
+        out[k]           = k == 0 ? ja : jm;
+        out[k].jobs      = k == 0 ? dst[0] : dst[1];
+        out[k].xcd_major = 1;
+        out[k].dxseg     = w.jseg + 16 * k;
+        out[k].njobs     = 0;  // unknown on the host; the launches read the ranges from dxseg
+    }
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }
@@ -2365,30 +2508,17 @@ static void ws_free(BwtWorkspace& w)
         (void) hipFree(w.big[i]);
         (void) hipFree(w.groups[i]);
         (void) hipFree(w.tile_bucket[i]);
+        (void) hipFree(w.tdesc[i]);
+        (void) hipFree(w.dig[i]);
     }
-    (void) hipFree(w.fsa);
-    (void) hipFree(w.isa);
-    (void) hipFree(w.tile_hist);
-    (void) hipFree(w.tile_off);
-    (void) hipFree(w.nomove);
-    (void) hipFree(w.flag);
-    (void) hipFree(w.jobs);
-    (void) hipFree(w.jobs_sorted);
-    (void) hipFree(w.mjobs_sorted);
-    (void) hipFree(w.job_cnt);
-    (void) hipFree(w.tile_cnt);
-    (void) hipFree(w.tile_order);
-    (void) hipFree(w.tdesc[0]);
-    (void) hipFree(w.dig[0]);
-    (void) hipFree(w.dig[1]);
-    (void) hipFree(w.tdesc[1]);
-    (void) hipHostFree(w.h_job_cnt);
-    (void) hipFree(w.mjobs);
-    (void) hipFree(w.ctr);
-    (void) hipFree(w.jobq);
-    (void) hipFree(w.l0tiles);
+    void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
+                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b};
+    for (void* p : dev)
+        (void) hipFree(p);
     if (w.h_ctr)
         (void) hipHostFree(w.h_ctr);
+    if (w.h_mail)
+        (void) hipHostFree(w.h_mail);
     w = BwtWorkspace{};
 }
 
@@ -2418,6 +2548,10 @@ static void ws_env(BwtWorkspace& w)
         w.jobq_on = atoi(e) != 0;
     if (const char* e = getenv("BRA_GRID"))  // workgroups of the MSD / level-0 tile kernels
         w.grid = std::max(8, atoi(e));
+    if (const char* e = getenv("BRA_SCAN_GRID"))
+        w.scan_grid = (uint32_t) std::max(8, atoi(e));
+    if (const char* e = getenv("BRA_LOOKAHEAD"))
+        w.lookahead = (uint32_t) std::max(1, atoi(e));
     if (const char* e = getenv("BRA_TILE_ORDER"))
         w.tile_order_mode = atoi(e);
     if (const char* e = getenv("BRA_JOBQ_CH"))
@@ -2426,7 +2560,6 @@ static void ws_env(BwtWorkspace& w)
 
 static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
 {
-    ws_env(w);
     if (n <= w.cap_n && nblocks <= w.cap_blocks)
         return true;
     ws_free(w);
@@ -2448,131 +2581,148 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     bool ok = true;
     for (int i = 0; i < 2 && ok; ++i)
         ok = dev_alloc(w.key[i], N) && dev_alloc(w.pay[i], N) && dev_alloc(w.big[i], w.cap_big) && dev_alloc(w.groups[i], w.cap_groups) &&
-             dev_alloc(w.tile_bucket[i], w.cap_tiles);
+             dev_alloc(w.tile_bucket[i], w.cap_tiles) && dev_alloc(w.tdesc[i], w.cap_tiles) && dev_alloc(w.dig[i], N + 16);
     const uint32_t tmax  = std::max(w.cap_tiles, w.cap_l0);
     const size_t   nkeys = 8 * (size_t) div_up(B, 8);
     ok = ok && dev_alloc(w.fsa, N) && dev_alloc(w.isa, N) && dev_alloc(w.tile_hist, (uint64_t) tmax * 256) &&
          dev_alloc(w.tile_off, (uint64_t) tmax * 256) && dev_alloc(w.nomove, std::max<uint32_t>(w.cap_big, B)) && dev_alloc(w.flag, B) &&
          dev_alloc(w.jobs, w.cap_jobs) && dev_alloc(w.mjobs, w.cap_mjobs) && dev_alloc(w.jobs_sorted, cap_sorted) &&
-         dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 8 * nkeys) && dev_alloc(w.tile_cnt, 2 * nkeys + 16) &&
-         dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.tdesc[0], w.cap_tiles) && dev_alloc(w.tdesc[1], w.cap_tiles) &&
-         dev_alloc(w.dig[0], N + 16) && dev_alloc(w.dig[1], N + 16) && dev_alloc(w.ctr, 1) && dev_alloc(w.jobq, 3 * 8 * 32) &&
-         dev_alloc(w.l0tiles, w.cap_l0);
-    if (ok && hipHostMalloc(&w.h_job_cnt, 8 * nkeys * 4, hipHostMallocDefault) != hipSuccess)
-        w.h_job_cnt = nullptr, ok = false;
-    if (ok && hipHostMalloc(&w.h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
+         dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 8 * nkeys) && dev_alloc(w.jseg, 3 * 16) &&
+         dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
+         dev_alloc(w.jobq, 3 * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B);
+    if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
+    if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+        w.h_mail = nullptr, ok = false;
     if (!ok)
     {
+        (void) hipGetLastError();
         bra_hip_report("bwt: workspace allocation for %llu elements failed", (unsigned long long) N);
         ws_free(w);  // capacities back to zero: the next call retries the allocation
         ws_env(w);
         return false;
     }
+    std::memset(w.h_mail, 0, MAX_LEVELS * sizeof(Mail));
     w.cap_n      = N;
     w.cap_blocks = B;
     return true;
 }
 
-static bool read_ctr(BwtWorkspace& w, hipStream_t s)
-{
-    BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    BRA_HIP_CHECK(hipStreamSynchronize(s));
-    if (w.h_ctr->overflow)
-    {
-        bra_hip_report("bwt: work list overflow");
-        return false;
-    }
-    return true;
-}
-
-static bool reset_ctr(BwtWorkspace& w, hipStream_t s)
-{
-    Counters z{};
-    z.hmin   = 0xFFFFFFFFu;
-    *w.h_ctr = z;  // pinned staging; the copy is ordered before any kernel of this call
-    BRA_HIP_CHECK(hipMemcpyAsync(w.ctr, w.h_ctr, sizeof(Counters), hipMemcpyHostToDevice, s));
-    return true;
-}
-
 static size_t tile_stage_bytes() { return sizeof(TileStage); }
 
-// MSD levels for the buckets in w.big[cur] (tiles already reserved in w.tile_bucket[cur] and
-// ctr->n_tiles_next).  Sub-buckets become jobs / fallback groups (appended to the queues).
+// MSD levels for the buckets listed in counters slot 1 (w.big[cur], tiles in w.tile_bucket[cur]);
+// the caller has posted slot 1's mailbox record.  Level k (k >= 1) consumes slot k and fills slot
+// k + 1.  Every level's kernels read their counts on the device, so the host only decides when to
+// stop: it enqueues up to `lookahead` levels beyond the last slot it has read; once a read slot is
+// empty, the levels already enqueued after it find nothing to do and return at once.
+// Sub-buckets become jobs / fallback groups (appended to the call-wide lists, slot 0).
 template <uint32_t MODE>
-static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, uint32_t nbig, uint32_t ntiles, int cur,
-                       Group* groups_out, hipStream_t s)
+static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, int cur, Group* groups_out, hipStream_t s,
+                       uint32_t first_seq)
 {
-    uint32_t nelems = w.h_ctr->n_elems_next;
-    const size_t lds  = tile_stage_bytes();
-    const int    grid = w.grid;
+    const size_t   lds    = tile_stage_bytes();
+    const int      grid   = w.grid;
+    const uint32_t max_lv = (MODE == MODE_STRING) ? DCAP_BIG : RANK_KEYBYTES;  // the scans emit no bucket deeper than this
+    uint32_t       seqs[MAX_LEVELS + 1] = {};
+    seqs[1]                             = first_seq;
     // STRING levels start at depth 1 with payloads carrying digits [1, 1 + CARRY); a level whose
     // scatter re-gathers digits (once per CARRY levels) lists its tiles XCD-major and block-major
     // (the gathers then stay in the XCD's L2); the other levels only stream payloads and take the
     // scan's tile-order descriptors as they are (no ordering kernels).
-    uint32_t lvl_d = 1, lvl_kd = 1;
-    while (nbig > 0)
+    uint32_t lvl_kd = 1;
+    uint32_t k = 1, known = 0, nb_known = 1;
+    while (true)
     {
-        hipLaunchKernelGGL(k_level_start, dim3(1), dim3(1), 0, s, w.ctr); BRA_DSYNC(s);
-        TileOrder  to{nullptr, nullptr, 0};
-        const bool rg      = lvl_d + 1 - lvl_kd >= CARRY;
-        const bool ordered = w.tile_order_mode == 2 || (w.tile_order_mode == 1 && rg);
-        if (MODE == MODE_STRING && !ordered)
-            to = TileOrder{w.tdesc[cur], nullptr, 1};
-        else if (MODE == MODE_STRING)
+        if (known > 0 && nb_known == 0)
+            break;  // slot `known` is empty: level `known` and every later one have nothing to do
+        if (k <= max_lv && k <= known + w.lookahead)
         {
-            // XCD-major, block-major tile list (the scatter's digit gathers stay in the XCD's L2)
-            const uint32_t kb0 = div_up(w.nblocks, 8), q = div_up(kb0, 1024u), kb = div_up(kb0, q), nk = 8 * kb;
-            uint32_t*      cnt = w.tile_cnt, *cur_ = w.tile_cnt + nk, *xs = w.tile_cnt + 2 * nk;
-            const dim3     g(std::min<uint32_t>(div_up(ntiles, JOB_CHUNK), 1024u));
-            BRA_HIP_CHECK(hipMemsetAsync(cnt, 0, nk * 4, s));
-            hipLaunchKernelGGL(k_tile_count, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cnt); BRA_DSYNC(s);
-            hipLaunchKernelGGL(k_tile_prefix, dim3(1), dim3(256), 0, s, cnt, nk, kb, cur_, xs); BRA_DSYNC(s);
-            hipLaunchKernelGGL(k_tile_scatter, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], ntiles, kb, q, nk, cur_, d_blocks,
-                               w.tdesc[cur], w.tile_order);
-            BRA_DSYNC(s);
-            to = TileOrder{w.tile_order, xs, 0};
+            const uint32_t  lvl_d   = k;
+            const bool      rg      = lvl_d + 1 - lvl_kd >= CARRY;
+            const bool      ordered = w.tile_order_mode == 2 || (w.tile_order_mode == 1 && rg);
+            const Counters* lin     = w.ctr + k;
+            Counters*       lout    = w.ctr + k + 1;
+            TileOrder       to{nullptr, nullptr, 0};
+            if (MODE == MODE_STRING && !ordered)
+                to = TileOrder{w.tdesc[cur], nullptr, 1};
+            else if (MODE == MODE_STRING)
+            {
+                // XCD-major, block-major tile list (the scatter's digit gathers stay in the XCD's L2)
+                const uint32_t kb0 = div_up(w.nblocks, 8), q = div_up(kb0, 1024u), kb = div_up(kb0, q), nk = 8 * kb;
+                uint32_t*      cnt = w.tile_cnt, *cur_ = w.tile_cnt + nk, *xs = w.tile_cnt + 2 * nk;
+                const dim3     g(1024);
+                BRA_HIP_CHECK(hipMemsetAsync(cnt, 0, nk * 4, s));
+                hipLaunchKernelGGL(k_tile_count, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], &lin->n_tiles_next, kb, q, nk, cnt);
+                BRA_DSYNC(s);
+                hipLaunchKernelGGL(k_tile_prefix, dim3(1), dim3(256), 0, s, cnt, nk, kb, cur_, xs); BRA_DSYNC(s);
+                hipLaunchKernelGGL(k_tile_scatter, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], &lin->n_tiles_next, kb, q, nk, cur_,
+                                   d_blocks, w.tdesc[cur], w.tile_order);
+                BRA_DSYNC(s);
+                to = TileOrder{w.tile_order, xs, 0};
+            }
+            {
+                BRA_PROF(P_BWT_HIST, s);
+                hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
+                                   w.pay[1], w.tile_hist, lin, to, w.dig[0], w.dig[1]); BRA_DSYNC(s);
+            }
+            ScanArgs a{d_blocks, w.big[cur],  0,           w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
+                       w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
+                       w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
+                       (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout};
+            {
+                BRA_PROF(P_BWT_SCAN, s);
+                hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
+            }
+            {
+                BRA_PROF(P_BWT_SCATTER, s);
+                if (MODE == MODE_STRING)
+                    hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
+                                       lin, to, w.dig[0], w.dig[1]);
+                else
+                    hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], lin, w.tile_off,
+                                       w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
+                BRA_DSYNC(s);
+            }
+            BRA_HIP_CHECK(hipGetLastError());
+            seqs[k + 1] = post(w, k + 1, s);
+            cur ^= 1;
+            if (rg)
+                lvl_kd = lvl_d + 1;
+            ++k;
+            continue;
         }
-        {
-            BRA_PROF(P_BWT_HIST, s);
-            hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
-                               w.pay[1], w.tile_hist, ntiles, to, w.dig[0], w.dig[1]); BRA_DSYNC(s);
-        }
-        ScanArgs a{d_blocks, w.big[cur],  nbig,        w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
-                   w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
-                   w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
-                   (uint32_t) (g_prof != nullptr), w.mjob_max()};
-        {
-            BRA_PROF(P_BWT_SCAN, s);
-            hipLaunchKernelGGL(k_scan<MODE>, dim3(std::min<uint32_t>(div_up(nbig, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
-        }
-        {
-            BRA_PROF(P_BWT_SCATTER, s);
-            if (MODE == MODE_STRING)
-                hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
-                                   ntiles, to, w.dig[0], w.dig[1]);
-            else
-                hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], w.ctr, w.tile_off,
-                                   w.key[0], w.key[1], w.pay[0], w.pay[1], MODE, ntiles);
-            BRA_DSYNC(s);
-        }
-        BRA_HIP_CHECK(hipGetLastError());
-        if (!read_ctr(w, s))
+        Mail m{};
+        if (!wait_mail(w, known + 1, seqs[known + 1], s, m))
             return false;
-        // algorithmic bytes: keys read by the histogram, tile histograms, KV moved by the scatter
-        const double nt = ntiles, ne = nelems, nm = w.h_ctr->n_moved;
-        nelems          = w.h_ctr->n_elems_next;
-        // STRING: 4-byte payloads (+ the next digit gathered for elements that stay in big buckets)
-        const double eb = 8.0, mb = (MODE == MODE_STRING) ? 16.0 + 8.0 / CARRY : 24.0;
+        ++known;
+        nb_known = m.n_big;
+        if (known > max_lv)
+            break;
+    }
+    w.levels = k - 1;
+    return true;
+}
+
+// Algorithmic bytes of the MSD levels (profiling only: one copy of the level counters).
+template <uint32_t MODE>
+static bool account_levels(BwtWorkspace& w, hipStream_t s)
+{
+    if (!g_prof || !(g_prof->mask >> P_BWT_HIST & 1 || g_prof->mask >> P_BWT_SCAN & 1 || g_prof->mask >> P_BWT_SCATTER & 1))
+        return true;
+    const uint32_t ns = std::min<uint32_t>(w.levels + 2, MAX_LEVELS);
+    BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, ns * sizeof(Counters), hipMemcpyDeviceToHost, s));
+    BRA_HIP_CHECK(hipStreamSynchronize(s));
+    // STRING: 8-byte payloads moved (+ the next digit gathered for elements that stay in big buckets)
+    const double eb = 8.0, mb = (MODE == MODE_STRING) ? 16.0 + 8.0 / CARRY : 24.0;
+    for (uint32_t k = 1; k + 1 < ns; ++k)
+    {
+        const Counters& c  = w.h_ctr[k];
+        const double    nt = c.n_tiles_next, ne = c.n_elems_next, nm = w.h_ctr[k + 1].n_moved;
+        if (c.n_big == 0)
+            break;
         prof_bytes(P_BWT_HIST, eb * ne + 1024.0 * nt);
-        prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * nbig);
+        prof_bytes(P_BWT_SCAN, 3072.0 * nt + 32.0 * c.n_big);
         prof_bytes(P_BWT_SCATTER, mb * nm + 1024.0 * nt);
-        nbig   = w.h_ctr->n_big;
-        ntiles = w.h_ctr->n_tiles_next;
-        cur ^= 1;
-        if (rg)
-            lvl_kd = lvl_d + 1;
-        ++lvl_d;
     }
     return true;
 }
@@ -2637,27 +2787,34 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     const int grid = w.grid;
 
     // ---- level 0 (buckets = blocks, elements read straight from the input) ----
-    std::vector<L0Tile> tiles;
-    std::vector<Bucket> l0b(nblocks);
-    for (uint32_t b = 0; b < nblocks; ++b)
+    // The tile list and the per-block buckets depend only on the geometry: uploaded once per geometry.
+    if (w.geo.size() != nblocks || std::memcmp(w.geo.data(), h_blocks, nblocks * sizeof(BlockDesc)) != 0)
     {
-        l0b[b] = Bucket{(uint32_t) h_blocks[b].off, h_blocks[b].len, 0, 0, b, 2u, 0, (uint32_t) tiles.size()};
-        for (uint32_t st = 0; st < h_blocks[b].len; st += TILE)
-            tiles.push_back(L0Tile{b, st});
+        std::vector<L0Tile> tiles;
+        std::vector<Bucket> l0b(nblocks);
+        for (uint32_t b = 0; b < nblocks; ++b)
+        {
+            l0b[b] = Bucket{(uint32_t) h_blocks[b].off, h_blocks[b].len, 0, 0, b, 2u, 0, (uint32_t) tiles.size()};
+            for (uint32_t st = 0; st < h_blocks[b].len; st += TILE)
+                tiles.push_back(L0Tile{b, st});
+        }
+        w.geo.clear();
+        w.nt0 = (uint32_t) tiles.size();
+        BRA_HIP_CHECK(hipMemcpyAsync(w.l0tiles, tiles.data(), w.nt0 * sizeof(L0Tile), hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipMemcpyAsync(w.l0b, l0b.data(), nblocks * sizeof(Bucket), hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));  // the host vectors are the copies' sources
+        w.geo.assign(h_blocks, h_blocks + nblocks);
     }
-    const uint32_t nt0 = (uint32_t) tiles.size();
-    BRA_HIP_CHECK(hipMemcpyAsync(w.l0tiles, tiles.data(), nt0 * sizeof(L0Tile), hipMemcpyHostToDevice, s));
-    BRA_HIP_CHECK(hipMemcpyAsync(w.big[1], l0b.data(), nblocks * sizeof(Bucket), hipMemcpyHostToDevice, s));
-    if (!reset_ctr(w, s))
-        return false;
+    const uint32_t nt0 = w.nt0;
+    hipLaunchKernelGGL(k_ctr_init, dim3(1), dim3(1024), 0, s, w.ctr, MAX_LEVELS);
     BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, nblocks, s));
     {
         BRA_PROF(P_BWT_L0HIST, s);
         hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist); BRA_DSYNC(s);
     }
-    ScanArgs a0{d_blocks, w.big[1],  nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
+    ScanArgs a0{d_blocks, w.l0b,     nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
-                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max()};
+                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1};
     {
         BRA_PROF(P_BWT_SCAN, s);
         hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(div_up(nblocks, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a0); BRA_DSYNC(s);
@@ -2668,23 +2825,18 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
                            w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
-    if (!read_ctr(w, s))
-        return false;
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
     prof_bytes(P_BWT_L0SCATTER, 9.0 * N + 1024.0 * nt0);  // window in, payload out
     // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]
-    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, w.h_ctr->n_big, w.h_ctr->n_tiles_next, 0, w.groups[0], s))
+    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s)))
         return false;
 
-    // ---- wave jobs ----
-    const uint32_t njobs = w.h_ctr->n_jobs;
-    JobArgs ja{w.jobs,  njobs,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
-               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}};
-    const uint32_t nmjobs = w.h_ctr->n_mjobs;
-    JobArgs        jm     = ja;
-    jm.jobs               = w.mjobs;
-    jm.njobs              = nmjobs;
+    // ---- jobs (counts and list ranges stay on the device) ----
+    JobArgs ja{w.jobs,  0,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
+               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0};
+    JobArgs jm = ja;
+    jm.jobs    = w.mjobs;
     JobArgs ord[3];
     if (!order_jobs(w, nblocks, ja, jm, ord, s))
         return false;
@@ -2697,24 +2849,26 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
             ord[k].jq_chunk = w.jobq_chunk;
         }
     }
-    if (njobs)
     {
         BRA_PROF(P_BWT_JOBS, s);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::min<uint32_t>(div_up(njobs, 4), w.jobs_grid))), dim3(256), 0, s, ord[0]);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, s, ord[0]);
         BRA_DSYNC(s);
     }
-    if (nmjobs)
     {
         // workgroup jobs of at most half the size run on half the waves
         BRA_PROF(P_BWT_MJOBS, s);
         const int half = w.mj_waves / 2;
-        if (ord[1].njobs)
-            launch_mjobs<MODE_STRING>(half >= 2 ? half : w.mj_waves, ord[1].njobs, ord[1], s);
-        if (ord[2].njobs)
-            launch_mjobs<MODE_STRING>(w.mj_waves, ord[2].njobs, ord[2], s);
+        if (w.mj_waves)
+        {
+            launch_mjobs<MODE_STRING>(half >= 2 ? half : w.mj_waves, ~0u, ord[1], s);
+            launch_mjobs<MODE_STRING>(w.mj_waves, ~0u, ord[2], s);
+        }
     }
     BRA_HIP_CHECK(hipGetLastError());
-    if (!read_ctr(w, s))
+    if (!account_levels<MODE_STRING>(w, s))
+        return false;
+    Mail mc{};
+    if (!post_wait(w, 0, s, mc))
         return false;
 #ifdef BRA_PHASES
     {
@@ -2727,13 +2881,18 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof ph));
     }
 #endif
-    // payload in, SA entry + L byte out, 16 key bytes + the previous byte gathered (split by the
-    // elements each kind of job covers)
-    prof_bytes(P_BWT_JOBS, 26.0 * ((double) N - (double) w.h_ctr->n_melems));
-    prof_bytes(P_BWT_MJOBS, 26.0 * (double) w.h_ctr->n_melems);
+    // SURVEY 8.1(d) BWT model: 11 algorithmic bytes per element (input read, SA written and
+    // re-read, L gathered and written), charged to the job kernels by the elements each kind covers
+    if (g_prof && (g_prof->mask >> P_BWT_JOBS & 1 || g_prof->mask >> P_BWT_MJOBS & 1))
+    {
+        BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));
+        prof_bytes(P_BWT_JOBS, 11.0 * ((double) N - (double) w.h_ctr->n_melems));
+        prof_bytes(P_BWT_MJOBS, 11.0 * (double) w.h_ctr->n_melems);
+    }
 
     // ---- fallback: prefix doubling on the groups still tied ----
-    uint32_t ng = w.h_ctr->n_groups;
+    uint32_t ng = mc.n_groups;
     if (ng == 0)
         return true;
     BRA_PROF(P_BWT_FALLBACK, s);
@@ -2745,44 +2904,46 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     hipLaunchKernelGGL(k_isa_init, dim3(64, std::min<uint32_t>(nblocks, 65535u)), dim3(256), 0, s, d_blocks, w.flag, nblocks, w.fsa, w.isa); BRA_DSYNC(s);
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
                        w.flag); BRA_DSYNC(s);
-    uint32_t hmin    = w.h_ctr->hmin;
+    uint32_t hmin    = mc.hmin;
     for (int round = 0; round < 64 && ng > 0; ++round)
     {
         // keys for this round (every read of isa happens here, before any rank update)
         hipLaunchKernelGGL(k_rank_keys, dim3(std::min<uint32_t>(ng, 8192u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, d_in, w.fsa,
                            w.isa, w.key[0], w.pay[0]); BRA_DSYNC(s);
-        if (!reset_ctr(w, s))
-            return false;
+        hipLaunchKernelGGL(k_ctr_init, dim3(1), dim3(1024), 0, s, w.ctr, MAX_LEVELS);
         hipLaunchKernelGGL(k_groups_to_work, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng,
-                           w.big[0], w.cap_big, w.tile_bucket[0], w.cap_tiles, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs, w.mjob_max(), w.ctr); BRA_DSYNC(s);
-        if (!read_ctr(w, s))
-            return false;
+                           w.big[0], w.cap_big, w.tile_bucket[0], w.cap_tiles, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs, w.mjob_max(), w.ctr,
+                           w.ctr + 1); BRA_DSYNC(s);
         Group* gnext = w.groups[gcur ^ 1];
         // sort the groups by rank key: MSD levels over the 4 key bytes; equal-key sub-buckets larger
         // than a job become next-round groups directly (emitted with the parent's depth)
-        if (!run_levels<MODE_RANK>(w, d_in, d_blocks, w.h_ctr->n_big, w.h_ctr->n_tiles_next, 0, gnext, s))
+        if (!run_levels<MODE_RANK>(w, d_in, d_blocks, 0, gnext, s, post(w, 1, s)))
             return false;
-        const uint32_t ng_big = w.h_ctr->n_groups;
-        const uint32_t nj     = w.h_ctr->n_jobs;
+        Mail mr{};
+        if (!post_wait(w, 0, s, mr))
+            return false;
+        const uint32_t ng_big = mr.n_groups;
+        const uint32_t nj     = mr.n_jobs;
         JobArgs jr{w.jobs, nj, d_in, d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi, w.isa, gnext, w.cap_groups,
-                   w.ctr,  0,  hmin, 0, {}};
+                   w.ctr,  0,  hmin, 0, {}, nullptr, nullptr, 0};
         if (ng_big)
             hipLaunchKernelGGL(k_rank_flush, dim3(std::min<uint32_t>(ng_big, 4096u)), dim3(256), 0, s, gnext, ng_big, d_blocks, w.pay[0],
                                w.pay[1], w.fsa, d_L, w.isa, d_pi); BRA_DSYNC(s);
         if (nj)
             hipLaunchKernelGGL(k_jobs<MODE_RANK>, dim3(std::min<uint32_t>(div_up(nj, 4), 8192u)), dim3(256), 0, s, jr); BRA_DSYNC(s);
-        const uint32_t nmj = w.h_ctr->n_mjobs;
+        const uint32_t nmj = mr.n_mjobs;
         if (nmj)
         {
-            JobArgs jm = jr;
-            jm.jobs    = w.mjobs;
-            jm.njobs   = nmj;
-            launch_mjobs<MODE_RANK>(w.mj_waves, nmj, jm, s);
+            JobArgs jm2 = jr;
+            jm2.jobs    = w.mjobs;
+            jm2.njobs   = nmj;
+            launch_mjobs<MODE_RANK>(w.mj_waves, nmj, jm2, s);
         }
         BRA_HIP_CHECK(hipGetLastError());
-        if (!read_ctr(w, s))
+        Mail me{};
+        if (!post_wait(w, 0, s, me))
             return false;
-        uint32_t ng_new = w.h_ctr->n_groups;
+        uint32_t ng_new = me.n_groups;
         // the big equal-key subgroups were emitted with the parent's depth: add the round's step,
         // mark them flushed, drop groups of identical rotations (depth >= n) and find the new step
         std::vector<Group> all(ng_new);

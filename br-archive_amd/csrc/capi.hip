@@ -210,6 +210,14 @@ struct bra_gpu_ctx_s
     uint32_t       last_nblocks = 0;
     uint32_t*      d_word = nullptr;  // [0] CRC result, [1..2] unframe status
     uint64_t       cap_word = 0;
+    // encode geometry cache (encode_impl)
+    std::vector<BlockDesc> enc_geo;
+    BlockDesc*     d_enc_blocks = nullptr;
+    uint8_t*       d_hin = nullptr;   // host-buffer chunk loops: staged input / output
+    uint8_t*       d_hout = nullptr;
+    uint64_t       cap_hin = 0, cap_hout = 0;
+    uint64_t*      d_enc_rle_base = nullptr;
+    uint64_t       cap_eb = 0, cap_erb = 0;
     Prof           prof;
 };
 
@@ -235,7 +243,7 @@ static void ctx_free(bra_gpu_ctx_s* c)
     c->hist_tiling.release();
     void* ptrs[] = {c->d_L,       c->d_mtf,   c->d_rle,  c->d_tmp,  c->d_blocks, c->d_pi,  c->d_rle_size, c->d_hist, c->d_status, c->d_rle_base,
                     c->d_rle_cap, c->d_aux,   c->d_meta, c->d_recs, c->d_io,     c->d_off, c->d_pay,      c->d_hdr,
-                    c->d_word};
+                    c->d_word,    c->d_enc_blocks, c->d_enc_rle_base, c->d_hin, c->d_hout};
     for (void* p : ptrs)
         (void) hipFree(p);
     if (c->stream)
@@ -277,12 +285,21 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     rle_base[nb] = R;
     if (!ensure_block_arrays(c, nb) || !grow(c->d_L, c->cap_L, N + 16) || !grow(c->d_mtf, c->cap_mtf, N + 16) || !grow(c->d_rle, c->cap_rle, R + 16))
         return -1;
-    if (hipMemcpyAsync(c->d_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(c->d_rle_base, rle_base.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-        return -1;
+    // the block descriptors and RLE bases depend only on the geometry: uploaded once per geometry
+    // (a pageable-source copy stalls the host, and the benchmark encodes one geometry repeatedly)
+    if (c->enc_geo.size() != nb || std::memcmp(c->enc_geo.data(), hb.data(), nb * sizeof(BlockDesc)) != 0)
+    {
+        c->enc_geo.clear();
+        if (!grow(c->d_enc_blocks, c->cap_eb, nb) || !grow(c->d_enc_rle_base, c->cap_erb, nb + 1) ||
+            hipMemcpyAsync(c->d_enc_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(c->d_enc_rle_base, rle_base.data(), (nb + 1) * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -1;
+        c->enc_geo = hb;
+    }
     {
         BRA_PROF(P_STAGE_BWT, s);
-        if (!bwt_encode_device(c->bwt, d_in, c->d_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
+        if (!bwt_encode_device(c->bwt, d_in, c->d_enc_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
             return -1;
     }
     {
@@ -292,7 +309,7 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     }
     {
         BRA_PROF(P_STAGE_RLE, s);
-        if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
+        if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_enc_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
             return -1;
     }
     uint64_t total = 0;
@@ -480,6 +497,8 @@ extern "C" {
 
 bra_gpu_ctx_t* bra_gpu_ctx_create(int device)
 {
+    if (device < 0 && hipGetDevice(&device) != hipSuccess)  // -1: the calling thread's current device
+        return nullptr;
     auto* c = new bra_gpu_ctx_s();
     if (!ctx_init(c, device))
     {
@@ -680,8 +699,20 @@ int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data
     return need < data_size ? 1 : 0;  // 0: not smaller than the input -> STORED (lib_bra_io_file_chunks.c:274-278)
 }
 
+static int decompress_chunks_impl(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
+                                  uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream, bool whole_entry);
+
 int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
                               uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream)
+{
+    return decompress_chunks_impl(c, d_stream, stream_size, block_size, d_out, out_cap, out_size, prev_crc, crc_out, stream, true);
+}
+
+// whole_entry: the stream is a whole file entry, so the reference's final safety check applies
+// (decoded size must exceed the stream size, lib_bra_io_file_chunks.c:423-427); a front end that
+// decodes an entry in several batches checks the total itself.
+static int decompress_chunks_impl(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
+                                  uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream, bool whole_entry)
 {
     if (!c || !d_stream || !block_size || block_size >= (1u << 24) || !d_out)
         return -1;
@@ -710,7 +741,7 @@ int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_
         *out_size = total;
     if (rc != 0)
         return rc;
-    if (total <= stream_size)  // the reference's safety check (:423-427)
+    if (whole_entry && total <= stream_size)  // the reference's safety check (:423-427)
     {
         bra_hip_report("corrupted file entry: %llu decoded bytes from %llu", (unsigned long long) total, (unsigned long long) stream_size);
         return -1;
@@ -740,6 +771,57 @@ int bra_gpu_decompress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_
         }
         *crc_out = crc;
     }
+    return 0;
+}
+
+// ---- host-buffer forms for the C front end (row f1; frontend/bra_io_file_chunks_gpu.c) ----
+// The input is copied into the context's device staging buffer, the device chunk loop runs, and
+// the chunk records come back; everything completes before the call returns.
+int bra_gpu_compress_chunks_host(bra_gpu_ctx_t* c, const uint8_t* h_in, uint64_t data_size, uint32_t block_size, uint8_t* h_out,
+                                 uint64_t out_cap, uint64_t* out_size, uint32_t* chunks_crc)
+{
+    if (!c || !h_in || !data_size || !block_size || block_size >= (1u << 24) || !h_out)
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
+        return -1;
+    const uint64_t bound = bra_gpu_chunks_bound(data_size, block_size);
+    if (!grow(c->d_hin, c->cap_hin, data_size + 16) || !grow(c->d_hout, c->cap_hout, bound + 16) ||
+        hipMemcpyAsync(c->d_hin, h_in, data_size, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return -1;
+    uint64_t  osz = 0;
+    const int rc  = bra_gpu_compress_chunks(c, c->d_hin, data_size, block_size, c->d_hout, c->cap_hout, &osz, chunks_crc, nullptr);
+    if (out_size)
+        *out_size = osz;
+    if (rc < 0)
+        return rc;
+    if (osz > out_cap)
+        return -2;
+    if (hipMemcpy(h_out, c->d_hout, osz, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return rc;
+}
+
+int bra_gpu_decompress_chunks_host(bra_gpu_ctx_t* c, const uint8_t* h_stream, uint64_t stream_size, uint32_t block_size, uint8_t* h_out,
+                                   uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, int whole_entry)
+{
+    if (!c || !h_stream || !stream_size || !block_size || block_size >= (1u << 24) || !h_out)
+        return -1;
+    DevGuard dg(c->device);
+    if (!dg.ok)
+        return -1;
+    if (!grow(c->d_hin, c->cap_hin, stream_size + 16) || !grow(c->d_hout, c->cap_hout, out_cap + 16) ||
+        hipMemcpyAsync(c->d_hin, h_stream, stream_size, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return -1;
+    uint64_t  osz = 0;
+    const int rc  = decompress_chunks_impl(c, c->d_hin, stream_size, block_size, c->d_hout, out_cap, &osz, prev_crc, crc_out, nullptr,
+                                           whole_entry != 0);
+    if (out_size)
+        *out_size = osz;
+    if (rc != 0)
+        return rc;
+    if (hipMemcpy(h_out, c->d_hout, osz, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
     return 0;
 }
 
@@ -810,7 +892,7 @@ const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)
     case 0: return c->d_L;
     case 1: return c->d_mtf;
     case 2: return c->d_rle;
-    case 3: return c->d_rle_base;
+    case 3: return c->d_enc_rle_base;  // RLE output bases of the last batch encode
     case 4: return c->d_rle_size;
     default: return nullptr;
     }

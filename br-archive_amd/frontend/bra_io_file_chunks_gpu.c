@@ -1,0 +1,308 @@
+/*
+ * bra_io_file_chunks_gpu.c -- the batched chunk loop of lib_bra on the MI355X block codec
+ * (SURVEY 8.1 row f1).  A drop-in replacement for the reference's src/io/lib_bra_io_file_chunks.c:
+ * it defines the six functions of src/io/lib_bra_io_file_chunks.h with the same signatures, file
+ * formats, CRC sequence and error behaviour, and is compiled against lib_bra's own headers (the
+ * maintainer's tree; oracle/Makefile target `gpulib` builds it against /root/reference/src).
+ *
+ * Where the reference encodes one 256 KiB chunk at a time through the four encoders
+ * (lib_bra_io_file_chunks.c:199-266), this file reads BATCH_CHUNKS chunks, makes ONE call into
+ * libbra_hip.so (bra_gpu_compress_chunks_host: all chunks encoded, framed and CRC'd on the GPU)
+ * and writes the returned chunk records to the temporary file.  The STORED fallback (:268-278),
+ * the meta entry update (:280-297) and the copy into the archive are the reference's sequence.
+ * Decoding parses the records of a batch on the host, hands them to bra_gpu_decompress_chunks_host
+ * and folds me->crc32 the way the reference does per chunk (:396-397).  There is no CPU encoder
+ * here: without a GPU the calls fail and log, like every other entry point of libbra_hip.so.
+ */
+#include <lib_bra_defs.h>
+#include <lib_bra_private.h>
+#include <lib_bra_types.h>
+
+#include <io/lib_bra_io_file.h>
+#include <io/lib_bra_io_file_chunks.h>
+#include <io/lib_bra_io_file_meta_entries.h>
+#include <log/bra_log.h>
+#include <utils/lib_bra_crc32c.h>
+
+#include <encoders/bra_huffman.h>
+#include <encoders/bra_rle.h>
+
+#define BRA_HIP_NO_TYPES /* the ABI types come from lib_bra_types.h / bra_huffman.h above */
+#include "../../include/bra_hip.h"
+
+#include <assert.h>
+#include <inttypes.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define CHUNK_SIZE   ((uint64_t) BRA_MAX_CHUNK_SIZE)
+#define BATCH_CHUNKS 256u /* 64 MiB of input per device call */
+
+/* One device context for the front end, on the device current when lib_bra first compresses. */
+static bra_gpu_ctx_t* front_ctx(void)
+{
+    static bra_gpu_ctx_t* ctx = NULL;
+    if (ctx == NULL)
+    {
+        ctx = bra_gpu_ctx_create(-1);
+        if (ctx == NULL)
+            bra_log_critical("no GPU context for the chunk loop (libbra_hip.so)");
+    }
+    return ctx;
+}
+
+/* ---- chunk headers: 3-byte little-endian pi, then the packed bra_huffman_t (:59-95) ---- */
+bool bra_io_file_chunks_read_header(bra_io_file_t* src, bra_io_chunk_header_t* chunk_header)
+{
+    assert(src != NULL && chunk_header != NULL);
+    uint8_t pi[BRA_BWT_INDEX_BYTES];
+    if (!bra_io_file_read(src, pi, sizeof pi))
+    {
+        bra_log_error("unable to read chunk primary index from %s", src->fn);
+        return false;
+    }
+    chunk_header->primary_index = (bra_bwt_index_t) pi[0] | (bra_bwt_index_t) pi[1] << 8 | (bra_bwt_index_t) pi[2] << 16;
+    if (!bra_io_file_read(src, &chunk_header->huffman, sizeof(bra_huffman_t)))
+    {
+        bra_log_error("unable to read chunk huffman header from %s", src->fn);
+        return false;
+    }
+    return true;
+}
+
+bool bra_io_file_chunks_write_header(bra_io_file_t* dst, const bra_io_chunk_header_t* chunk_header)
+{
+    assert(dst != NULL && chunk_header != NULL);
+    const uint8_t pi[BRA_BWT_INDEX_BYTES] = {(uint8_t) chunk_header->primary_index, (uint8_t) (chunk_header->primary_index >> 8),
+                                             (uint8_t) (chunk_header->primary_index >> 16)};
+    if (!bra_io_file_write(dst, pi, sizeof pi))
+    {
+        bra_log_error("unable to write chunk primary index to %s", dst->fn);
+        return false;
+    }
+    if (!bra_io_file_write(dst, &chunk_header->huffman, sizeof(bra_huffman_t)))
+    {
+        bra_log_error("unable to write chunk huffman header to %s", dst->fn);
+        return false;
+    }
+    return true;
+}
+
+bool bra_io_file_chunks_read_file(bra_io_file_t* src, const uint64_t data_size, bra_meta_entry_t* me, const bool decode)
+{
+    assert(src != NULL && me != NULL);
+    const unsigned comp = BRA_ATTR_COMP(me->attributes);
+    if (comp == BRA_ATTR_COMP_STORED)
+        return bra_io_file_chunks_copy_file(NULL, src, data_size, me, decode);
+    if (comp == BRA_ATTR_COMP_COMPRESSED)
+        return bra_io_file_chunks_decompress_file(NULL, src, data_size, me, decode);
+    bra_log_critical("invalid compression type for file: %u", comp);
+    return false;
+}
+
+/* Stored data: copied through in CHUNK_SIZE pieces, the CRC updated per piece (:119-167). */
+bool bra_io_file_chunks_copy_file(bra_io_file_t* dst, bra_io_file_t* src, const uint64_t data_size, bra_meta_entry_t* me, const bool compute_crc32)
+{
+    assert(src != NULL);
+    bool     ok  = !(dst != NULL && (dst->f == NULL || dst->fn == NULL));
+    uint8_t* buf = ok ? (uint8_t*) malloc(CHUNK_SIZE) : NULL;
+    if (ok && compute_crc32 && me == NULL)
+    {
+        bra_log_critical("can't compute crc32: me is null");
+        ok = false;
+    }
+    for (uint64_t done = 0; ok && buf != NULL && done < data_size;)
+    {
+        const size_t n = (size_t) _bra_min(CHUNK_SIZE, data_size - done);
+        ok             = bra_io_file_read(src, buf, n);
+        if (ok && compute_crc32)
+            me->crc32 = bra_crc32c(buf, n, me->crc32);
+        if (ok && dst != NULL)
+            ok = bra_io_file_write(dst, buf, n);
+        done += n;
+    }
+    ok = ok && buf != NULL;
+    free(buf);
+    if (!ok)
+    {
+        if (dst != NULL)
+            bra_io_file_close(dst);
+        bra_io_file_close(src);
+    }
+    return ok;
+}
+
+static uint64_t num_chunks(uint64_t n) { return (n + CHUNK_SIZE - 1) / CHUNK_SIZE; }
+
+bool bra_io_file_chunks_compress_file(bra_io_file_t* dst, bra_io_file_t* src, const uint64_t data_size, bra_meta_entry_t* me)
+{
+    assert(dst != NULL && src != NULL && me != NULL);
+    bra_gpu_ctx_t* ctx = front_ctx();
+    if (ctx == NULL)
+        return false;
+    // the records of the compressed chunks go to a temporary file first: kept only when smaller
+    // than the input (the reference's rule, :185-189 and :268-278)
+    bra_io_file_t tmpfile;
+    if (!bra_io_file_tmp_open(&tmpfile))
+    {
+        bra_log_error("unable to compress file: %s", src->fn);
+        return false;
+    }
+    const uint64_t batch = _bra_min((uint64_t) BATCH_CHUNKS * CHUNK_SIZE, data_size);
+    const uint64_t cap   = bra_gpu_chunks_bound(batch, (uint32_t) CHUNK_SIZE);
+    uint8_t*       in    = (uint8_t*) malloc(batch ? batch : 1);
+    uint8_t*       out   = (uint8_t*) malloc(cap ? cap : 1);
+    uint32_t       crc32 = BRA_CRC32C_INIT; /* the running CRC of header + source chunk pairs (:214,248-249) */
+    bool           ok    = in != NULL && out != NULL;
+    for (uint64_t done = 0; ok && done < data_size;)
+    {
+        const uint64_t n = _bra_min(batch, data_size - done);
+        bra_log_printf("%3u%%", (unsigned int) (done * 100 / data_size));
+        bra_log_printf("\b\b\b\b");
+        if (!bra_io_file_read(src, in, n))
+        {
+            bra_io_file_close(&tmpfile);
+            bra_io_file_close(dst);
+            free(in);
+            free(out);
+            return false;
+        }
+        uint64_t osz = 0;
+        uint32_t bcrc = 0;
+        const int rc = bra_gpu_compress_chunks_host(ctx, in, n, (uint32_t) CHUNK_SIZE, out, cap, &osz, &bcrc);
+        if (rc < 0)
+        {
+            bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, done);
+            ok = false;
+            break;
+        }
+        // this batch's share of the running CRC: its headers and chunks follow the previous ones
+        crc32 = bra_gpu_crc32c_combine(crc32, bcrc, n + num_chunks(n) * sizeof(bra_io_chunk_header_t));
+        ok    = bra_io_file_write(&tmpfile, out, (size_t) osz);
+        done += n;
+    }
+    free(in);
+    free(out);
+    if (!ok)
+    {
+        bra_io_file_close(&tmpfile);
+        bra_io_file_close(dst);
+        bra_io_file_close(src);
+        return false;
+    }
+
+    const int64_t tmpfile_size = bra_io_file_tell(&tmpfile);
+    bool          res          = tmpfile_size >= 0;
+    if (res && (uint64_t) tmpfile_size >= data_size)
+    {
+        res            = false; /* not smaller: the caller stores the file instead */
+        me->attributes = BRA_ATTR_SET_COMP(me->attributes, BRA_ATTR_COMP_STORED);
+    }
+    else if (res)
+    {
+        bra_meta_entry_file_t* mef = (bra_meta_entry_file_t*) me->entry_data;
+        mef->data_size             = (uint64_t) tmpfile_size;
+        me->crc32                  = bra_crc32c(&tmpfile_size, sizeof(tmpfile_size), me->crc32);
+        me->crc32                  = bra_crc32c_combine(me->crc32, crc32, data_size + (num_chunks(data_size) * sizeof(bra_io_chunk_header_t)));
+        res = bra_io_file_seek(&tmpfile, 0, SEEK_SET) && bra_io_file_meta_entry_write_file_entry(dst, me) &&
+              bra_io_file_chunks_copy_file(dst, &tmpfile, (uint64_t) tmpfile_size, me, false);
+    }
+    bra_io_file_close(&tmpfile);
+    return res;
+}
+
+/* Header checks of the reference decoder (:31-49). */
+static bool header_valid(const bra_io_chunk_header_t* h)
+{
+    return h->primary_index < BRA_MAX_CHUNK_SIZE && h->huffman.encoded_size <= BRA_MAX_CHUNK_SIZE &&
+           h->huffman.orig_size <= BRA_MAX_CHUNK_SIZE && h->huffman.encoded_size != 0 && h->huffman.orig_size != 0;
+}
+
+/* Listing (decode == false): only the decoded sizes, through the per-chunk entry points. */
+static bool chunk_decoded_size(const bra_io_chunk_header_t* h, const uint8_t* payload, uint64_t* size)
+{
+    uint32_t       huf_s = 0;
+    uint8_t* const huf   = bra_huffman_decode(&h->huffman, payload, &huf_s);
+    if (huf == NULL)
+        return false;
+    *size += bra_rle_decode_compute_size(huf, huf_s);
+    free(huf);
+    return true;
+}
+
+bool bra_io_file_chunks_decompress_file(bra_io_file_t* dst, bra_io_file_t* src, const uint64_t data_size, bra_meta_entry_t* me, const bool decode)
+{
+    assert(src != NULL && me != NULL);
+    bra_gpu_ctx_t* ctx = decode ? front_ctx() : NULL;
+    bool           ok  = !(dst != NULL && (dst->f == NULL || dst->fn == NULL)) && (!decode || ctx != NULL);
+    // a batch holds whole records: up to BATCH_CHUNKS of them, at most that many chunk sizes of
+    // decoded output (the headers bound every chunk by BRA_MAX_CHUNK_SIZE)
+    const uint64_t rec_max  = sizeof(bra_huffman_t) + BRA_BWT_INDEX_BYTES + CHUNK_SIZE;
+    const uint64_t scap     = (uint64_t) BATCH_CHUNKS * rec_max;
+    const uint64_t ocap     = (uint64_t) BATCH_CHUNKS * CHUNK_SIZE;
+    uint8_t*       stream   = ok ? (uint8_t*) malloc(scap) : NULL;
+    uint8_t*       decoded  = (ok && decode) ? (uint8_t*) malloc(ocap) : NULL;
+    uint64_t       orig     = 0;
+    ok                      = ok && stream != NULL && (!decode || decoded != NULL);
+    for (uint64_t done = 0; ok && done < data_size;)
+    {
+        // read up to BATCH_CHUNKS records (header, check, payload) into the stream buffer
+        uint64_t fill = 0;
+        uint32_t recs = 0;
+        while (ok && recs < BATCH_CHUNKS && done + fill < data_size)
+        {
+            bra_io_chunk_header_t h = {.primary_index = 0};
+            ok = bra_io_file_chunks_read_header(src, &h);
+            if (ok && !header_valid(&h))
+            {
+                bra_log_error("chunk header not valid in %s", src->fn);
+                ok = false;
+            }
+            if (!ok)
+                break;
+            uint8_t* rec = stream + fill;
+            rec[0] = (uint8_t) h.primary_index, rec[1] = (uint8_t) (h.primary_index >> 8), rec[2] = (uint8_t) (h.primary_index >> 16);
+            memcpy(rec + BRA_BWT_INDEX_BYTES, &h.huffman, sizeof(bra_huffman_t));
+            const uint64_t hsz = BRA_BWT_INDEX_BYTES + sizeof(bra_huffman_t);
+            ok                 = bra_io_file_read(src, rec + hsz, h.huffman.encoded_size);
+            if (ok && !decode)
+            {
+                ok = chunk_decoded_size(&h, rec + hsz, &orig);
+                if (!ok)
+                    bra_log_error("unable to decode huffman file: %s ", src->fn);
+            }
+            fill += hsz + h.huffman.encoded_size;
+            ++recs;
+        }
+        if (ok && decode)
+        {
+            uint64_t  osz = 0;
+            const int rc  = bra_gpu_decompress_chunks_host(ctx, stream, fill, (uint32_t) CHUNK_SIZE, decoded, ocap, &osz, me->crc32, &me->crc32, 0);
+            if (rc != 0)
+            {
+                bra_log_error("unable to decode chunks in %s", src->fn);
+                ok = false;
+            }
+            orig += osz;
+            if (ok && dst != NULL)
+                ok = bra_io_file_write(dst, decoded, (size_t) osz);
+        }
+        done += fill;
+    }
+    if (ok && orig <= data_size)
+    {
+        bra_log_error("corrupted file entry: %s", me->name);
+        ok = false;
+    }
+    if (ok)
+        me->_compression_ratio = (float) ((double) data_size / (double) orig);
+    free(stream);
+    free(decoded);
+    if (!ok)
+    {
+        if (dst != NULL)
+            bra_io_file_close(dst);
+        bra_io_file_close(src);
+    }
+    return ok;
+}

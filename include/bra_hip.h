@@ -82,7 +82,8 @@ void bra_huffman_chunk_free(bra_huffman_chunk_t* chunk);
 /* ---- Part 2: batched, device-resident block codec -------------------------------------------- */
 typedef struct bra_gpu_ctx_s bra_gpu_ctx_t;
 
-/* A context owns device scratch (grown on demand) and a HIP stream on `device`.  NULL on error. */
+/* A context owns device scratch (grown on demand) and a HIP stream on `device` (-1: the calling
+ * thread's current device).  NULL on error. */
 bra_gpu_ctx_t* bra_gpu_ctx_create(int device);
 void           bra_gpu_ctx_destroy(bra_gpu_ctx_t* ctx);
 
@@ -188,6 +189,20 @@ int bra_gpu_compress_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_in, uint64_t da
  */
 int bra_gpu_decompress_chunks(bra_gpu_ctx_t* ctx, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
                               uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, void* stream);
+
+/*
+ * Host-buffer forms of the two chunk loops, for a C front end that replaces lib_bra's
+ * src/io/lib_bra_io_file_chunks.c (frontend/bra_io_file_chunks_gpu.c): the input
+ * is staged into the context's device buffers, the device loop runs, the result is copied back to
+ * h_out; the call has completed when it returns.  Return codes as the device forms.  For the
+ * decode, whole_entry != 0 applies the reference's end-of-entry check (decoded size above the
+ * stream size, lib_bra_io_file_chunks.c:423-427); a caller decoding one entry in several batches
+ * passes 0 and checks the total itself.
+ */
+int bra_gpu_compress_chunks_host(bra_gpu_ctx_t* ctx, const uint8_t* h_in, uint64_t data_size, uint32_t block_size, uint8_t* h_out,
+                                 uint64_t out_cap, uint64_t* out_size, uint32_t* chunks_crc);
+int bra_gpu_decompress_chunks_host(bra_gpu_ctx_t* ctx, const uint8_t* h_stream, uint64_t stream_size, uint32_t block_size, uint8_t* h_out,
+                                   uint64_t out_cap, uint64_t* out_size, uint32_t prev_crc, uint32_t* crc_out, int whole_entry);
 
 /* ---- Part 4: blocks sharded over several GPUs (SURVEY 8.1 row e) ----------------------------- */
 

@@ -342,6 +342,8 @@ class ReferenceLib:
         L.bra_crc32c_combine.restype = C.c_uint32
         L.ref_compress_file.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ref_compress_file.restype = C.c_int
+        L.ref_decompress_file.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint32)]
+        L.ref_decompress_file.restype = C.c_int
 
     def crc32c(self, data: bytes, prev: int = 0) -> int:
         return self.lib.bra_crc32c(_buf(data), len(data), prev)
@@ -362,3 +364,15 @@ class ReferenceLib:
         with open(dst, "rb") as f:
             out = f.read()
         return bool(ok), out, cb.value, ca.value, at.value
+
+    def decompress_file(self, stream: bytes, workdir: str):
+        """Run bra_io_file_chunks_decompress_file on chunk records.  Returns (ok, decoded bytes,
+        me->crc32 after)."""
+        src = os.path.join(workdir, "stream.bin")
+        dst = os.path.join(workdir, "decoded.bin")
+        with open(src, "wb") as f:
+            f.write(stream)
+        crc = C.c_uint32()
+        ok = self.lib.ref_decompress_file(src.encode(), dst.encode(), len(stream), C.byref(crc))
+        out = open(dst, "rb").read() if os.path.exists(dst) else b""
+        return bool(ok), out, crc.value

@@ -41,3 +41,32 @@ int ref_compress_file(const char* src_fn, const char* dst_fn, uint64_t size, uin
     bra_quit();
     return ok;
 }
+
+/* Decode `size` bytes of chunk records (what ref_compress_file writes after the 8-byte data size)
+ * with the reference's bra_io_file_chunks_decompress_file (lib_bra_io_file_chunks.c:314-441) into
+ * dst_fn.  Returns 1 on success, 0 when the reference rejects the stream (e.g. a chunk header whose
+ * encoded_size exceeds BRA_MAX_CHUNK_SIZE, :36-40); *crc_after = the entry CRC it accumulated. */
+int ref_decompress_file(const char* src_fn, const char* dst_fn, uint64_t size, uint32_t* crc_after)
+{
+    if (!bra_init())
+        return 0;
+    bra_io_file_t src, dst;
+    memset(&src, 0, sizeof src);
+    memset(&dst, 0, sizeof dst);
+    int ok = 0;
+    if (bra_io_file_open(&src, src_fn, "rb") && bra_io_file_open(&dst, dst_fn, "wb"))
+    {
+        bra_meta_entry_t me;
+        memset(&me, 0, sizeof me);
+        if (bra_meta_entry_init(&me, BRA_ATTR_SET_COMP(BRA_ATTR_TYPE_FILE, BRA_ATTR_COMP_COMPRESSED), "f", 1) && bra_meta_entry_file_set(&me, size))
+        {
+            ok         = bra_io_file_chunks_decompress_file(&dst, &src, size, &me, true) ? 1 : 0;
+            *crc_after = me.crc32;
+        }
+        bra_meta_entry_free(&me);
+    }
+    bra_io_file_close(&src);
+    bra_io_file_close(&dst);
+    bra_quit();
+    return ok;
+}

@@ -35,6 +35,18 @@ CASES = [  # (name, synth kind, total bytes)
     ("sym16_524288", 2, 524288),
     ("random_100000", 1, 100000),
 ]
+# Inputs made of parts [synth kind, bytes, first synthetic block] or the reference's own fixture file:
+#   mixed_text_random -- SURVEY 0.5 / row f4: compressible text chunks around ONE uniform-random
+#                        256 KiB chunk.  The reference still archives the file compressed (the
+#                        tmpfile is smaller than the input), but the random chunk's Huffman payload
+#                        exceeds BRA_MAX_CHUNK_SIZE, so its own decoder rejects the stream
+#                        (lib_bra_io_file_chunks.c:36-40): `ref_decodes` is false.
+#   lorem_txt         -- test/fixtures/lorem.txt (3039 B, the input of test_bra_unbra_comp_2,
+#                        test/test_bra.cpp:353-398), committed as tests/golden/lorem.txt.
+PART_CASES = [
+    ("mixed_text_random", {"parts": [[0, 2 * 262144, 0], [1, 262144, 0], [0, 100000, 3]]}),
+    ("lorem_txt", {"file": "lorem.txt"}),
+]
 
 
 def synth(kind: int, total: int) -> bytes:
@@ -46,16 +58,33 @@ def synth(kind: int, total: int) -> bytes:
     return a.tobytes()
 
 
+def case_input(rec: dict) -> bytes:
+    """The input bytes of a chunks.json case (same rule as tests/test_gpu_chunks.py)."""
+    import numpy as np
+
+    if "file" in rec:
+        return open(os.path.join(ROOT, "tests", "golden", rec["file"]), "rb").read()
+    if "parts" in rec:
+        bra = __import__("importlib").import_module("br-archive_amd")
+        return np.concatenate([bra.synth_fill(k, n, 262144, first_block=fb) for k, n, fb in rec["parts"]]).tobytes()
+    return synth(rec["kind"], rec["total"])
+
+
 def main():
     if not have_reflib():
         sys.exit("oracle/_ref/libbralib.so missing: run `make -C oracle ref` where /root/reference exists")
+    lorem = os.path.join(ROOT, "tests", "golden", "lorem.txt")
+    if not os.path.exists(lorem):  # the reference's own fixture file, kept as test data
+        with open("/root/reference/test/fixtures/lorem.txt", "rb") as f, open(lorem, "wb") as g:
+            g.write(f.read())
     R = ReferenceLib()
     out = {}
-    for name, kind, total in CASES:
-        data = synth(kind, total)
+    cases = [(name, {"kind": kind, "total": total}) for name, kind, total in CASES] + PART_CASES
+    for name, spec in cases:
+        data = case_input(spec)
         with tempfile.TemporaryDirectory() as d:
             ok, dst, cb, ca, attr = R.compress_file(data, d)
-        rec = dict(kind=kind, total=total, compressed=ok, attr=attr, entry_crc_before=cb, entry_crc=ca)
+        rec = dict(spec, total=len(data), compressed=ok, attr=attr, entry_crc_before=cb, entry_crc=ca)
         if ok:
             tsz = int.from_bytes(dst[:8], "little")
             stream = dst[8:]
@@ -68,7 +97,15 @@ def main():
                 crcs.append(R.crc32c(chunk, R.crc32c(hdr)))
                 pos += 267 + esz
                 b += 1
-            rec.update(stream_size=tsz, stream_sha256=hashlib.sha256(stream).hexdigest(), chunk_crcs=crcs)
+            with tempfile.TemporaryDirectory() as d:
+                dok, dec, dcrc = R.decompress_file(stream, d)
+            esizes = []
+            pos = 0
+            while pos < len(stream):
+                esizes.append(int.from_bytes(stream[pos + 263: pos + 267], "little"))
+                pos += 267 + esizes[-1]
+            rec.update(stream_size=tsz, stream_sha256=hashlib.sha256(stream).hexdigest(), chunk_crcs=crcs, encoded_sizes=esizes,
+                       ref_decodes=dok and dec == data, ref_decode_crc=dcrc if dok else None)
         out[name] = rec
         print(name, {k: v for k, v in rec.items() if k != "chunk_crcs"}, flush=True)
     with open(os.path.join(ROOT, "tests", "golden", "chunks.json"), "w") as f:

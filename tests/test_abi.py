@@ -7,6 +7,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "bra_hip.h")
 
@@ -22,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     out = subprocess.check_output(["nm", "-D", "--defined-only", bra.LIB_PATH], text=True)
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     declared = _header_functions()
-    assert len(declared) == 37
+    assert len(declared) == 39
     missing = [f for f in declared if f not in exported]
     assert not missing, missing
     assert sorted(bra.ABI_SYMBOLS) == declared
@@ -56,3 +58,36 @@ def test_synthetic_generators_deterministic():
     assert a != bra.synth_block(bra.SYNTH_TEXT, 6, 4096)
     assert set(bra.synth_block(bra.SYNTH_SYM16, 0, 4096)) <= set(range(ord("a"), ord("a") + 16))
     assert bra.synth_block(bra.SYNTH_TILED, 0, 38) == b"Test File Fixture.\n" * 2
+
+
+def _undefined_bra(path):
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.split()[-1].startswith("bra_")}
+
+
+def _defined(path):
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines()}
+
+
+@pytest.mark.parametrize("lib", ["libbralib_hipenc.so", "libbralib_gpu.so"])
+def test_lib_bra_links_against_gpu_library(lib):
+    """lib_bra built from the reference sources minus src/encoders (oracle/Makefile target gpulib,
+    linked with -Wl,--no-undefined): every bra_* symbol it needs from outside is exported by
+    libbra_hip.so, and it carries no encoder of its own."""
+    path = os.path.join(ROOT, "oracle", "_ref", lib)
+    if not os.path.exists(path):
+        pytest.skip(f"{lib} not built (needs the reference tree)")
+    hip = os.path.join(ROOT, "br-archive_amd", "libbra_hip.so")
+    need = _undefined_bra(path)
+    assert need and need <= _defined(hip), need - _defined(hip)
+    encoders = {"bra_bwt_encode2", "bra_mtf_encode2", "bra_rle_encode", "bra_huffman_encode", "bra_huffman_decode"}
+    assert not (encoders & _defined(path))
+    if lib == "libbralib_hipenc.so":  # the reference's own chunk loop calls the drop-in encoders
+        assert {"bra_bwt_encode2", "bra_mtf_encode2", "bra_rle_encode", "bra_huffman_encode", "bra_huffman_chunk_free"} <= need
+    else:  # the batched front end calls the batch ABI
+        assert {"bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host"} <= need

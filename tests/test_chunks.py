@@ -30,6 +30,17 @@ def _synth(kind, total):
     return bra.synth_fill(kind, total, CS).tobytes()
 
 
+def _case_input(g) -> bytes:
+    """Input bytes of a chunks.json case (the rule of tests/golden/make_chunks_golden.py)."""
+    if "file" in g:
+        with open(os.path.join(os.path.dirname(CHUNKS), g["file"]), "rb") as f:
+            return f.read()
+    if "parts" in g:
+        bra = importlib.import_module("br-archive_amd")
+        return b"".join(bra.synth_fill(k, n, CS, first_block=fb).tobytes() for k, n, fb in g["parts"])
+    return _synth(g["kind"], g["total"])
+
+
 # ---- 1. CRC32C known answers (test/test_bra_crc32c.cpp:19-132) ------------------------------------
 def test_crc32c_kat(orc):
     d1, d2 = b"123456789", b"Hello World!"
@@ -66,7 +77,8 @@ def _golden():
 @pytest.mark.parametrize("name", sorted(_golden()))
 def test_oracle_chunk_loop_vs_golden(orc, name):
     g = _golden()[name]
-    data = _synth(g["kind"], g["total"])
+    data = _case_input(g)
+    assert len(data) == g["total"]
     stream, crc, chunks = orc.compress_chunks(data, CS)
     compressed = len(stream) < len(data)
     assert compressed == g["compressed"]
@@ -83,6 +95,13 @@ def test_oracle_chunk_loop_vs_golden(orc, name):
         assert orc.crc32c(part, orc.crc32c(hdr)) == g["chunk_crcs"][b], b
         running = orc.crc32c_combine(running, g["chunk_crcs"][b], 268 + len(part))
     assert running == crc
+    assert [ch.encoded_size for ch in chunks] == g["encoded_sizes"]
+    if not g["ref_decodes"]:
+        # the reference writes this stream but its decoder rejects it, because
+        # one chunk's Huffman payload exceeds BRA_MAX_CHUNK_SIZE (lib_bra_io_file_chunks.c:36-40)
+        assert max(g["encoded_sizes"]) > CS
+    else:
+        assert g["ref_decode_crc"] == crc
 
 
 @pytest.mark.skipif(not have_reflib(), reason="reference lib_bra build (oracle/_ref/libbralib.so) not present")

@@ -82,13 +82,24 @@ def _golden():
         return json.load(f)
 
 
+def case_input(bra, g) -> np.ndarray:
+    """Input bytes of a chunks.json case (the rule of tests/golden/make_chunks_golden.py)."""
+    if "file" in g:
+        return np.fromfile(os.path.join(ROOT, "tests", "golden", g["file"]), dtype=np.uint8)
+    if "parts" in g:
+        return np.concatenate([bra.synth_fill(k, n, CS, first_block=fb) for k, n, fb in g["parts"]])
+    return bra.synth_fill(g["kind"], g["total"], CS)
+
+
 @pytest.mark.parametrize("name", sorted(_golden()))
 def test_compress_chunks_vs_reference_golden(bra, codec, name):
-    """The device chunk loop reproduces the reference's tmpfile bytes and CRCs."""
+    """The device chunk loop reproduces the reference's tmpfile bytes and CRCs; the device decode
+    loop accepts exactly the streams the reference's decode loop accepts."""
     import torch
 
     g = _golden()[name]
-    data = bra.synth_fill(g["kind"], g["total"], CS)
+    data = case_input(bra, g)
+    assert data.size == g["total"]
     stream, crc, compressed = codec.compress_chunks(torch.from_numpy(data).cuda(), CS)
     assert compressed == g["compressed"]
     if not compressed:
@@ -98,10 +109,18 @@ def test_compress_chunks_vs_reference_golden(bra, codec, name):
     assert len(s) == g["stream_size"]
     assert hashlib.sha256(s).hexdigest() == g["stream_sha256"]
     assert bra.entry_crc32c(g["entry_crc_before"], len(s), crc, g["total"]) == g["entry_crc"]
-    # decode side: the same stream CRC folded over the decoded chunks
+    if not g["ref_decodes"]:
+        # a chunk whose Huffman payload exceeds BRA_MAX_CHUNK_SIZE is written
+        # (bit-exact above) but the reference's own decoder rejects it (lib_bra_io_file_chunks.c:
+        # 36-40); so does the device decode loop
+        assert max(g["encoded_sizes"]) > CS
+        with pytest.raises(ValueError):
+            codec.decompress_chunks(stream, CS, prev_crc=0)
+        return
+    # decode side: the same stream CRC folded over the decoded chunks, as the reference's decoder
     out, dcrc = codec.decompress_chunks(stream, CS, prev_crc=0)
     assert torch.equal(out.cpu(), torch.from_numpy(data))
-    assert dcrc == crc
+    assert dcrc == crc == g["ref_decode_crc"]
 
 
 @pytest.mark.parametrize("kind,total,bs", [(0, 8 << 20, 1 << 20), (2, 3 * CS + 1, CS), (1, 2 * CS, CS), (0, 1, CS)])

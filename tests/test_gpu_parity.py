@@ -236,3 +236,24 @@ def test_batch_decode_rejects_corruption(bra, codec):
     assert esz3 > 0
     with pytest.raises(RuntimeError):
         codec.decode(torch.from_numpy(h).cuda(), off, pay, data.size, bs)
+
+
+def test_huffman_code_lengths_over_32(bra):
+    """bra_huffman_encode on a Fibonacci histogram: 33-bit codes, wrapped u32 canonical codes and
+    leading zero bits, bit-exact with the reference (tests/golden/edge.json); the decoder rejects
+    the stream as the reference's does (its tree rebuild collides)."""
+    import hashlib
+    import json
+    import os
+
+    f = [1, 1]
+    while len(f) < 34:
+        f.append(f[-1] + f[-2])
+    fib = b"".join(bytes([s]) * f[s] for s in range(34))  # the rule of tests/golden/make_edge_golden.py
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "edge.json")))["huffman_fib34"]
+    ch = bra.huffman_encode(fib)
+    assert len(fib) == g["size"]
+    assert ch.lengths.hex() == g["lengths"] and max(ch.lengths) == 33
+    assert (ch.orig_size, ch.encoded_size) == (g["orig_size"], g["encoded_size"])
+    assert hashlib.sha256(ch.data).hexdigest() == g["payload_sha256"]
+    assert bra.huffman_decode(ch.lengths, ch.orig_size, ch.encoded_size, ch.data) is None

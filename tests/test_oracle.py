@@ -5,6 +5,7 @@
    /root/reference, see tests/golden/make_golden.py), stage by stage.
 3. When oracle/_ref/libbraref.so is present: seeded random cross-checks against the reference.
 """
+import os
 import random
 
 import pytest
@@ -151,3 +152,34 @@ def test_huffman_decode_malformed_vs_reference(orc):
     ref = Reference()
     for lens, osz, esz, pay in _huffman_mutations(orc):
         assert orc.huffman_decode(lens, osz, esz, pay) == ref.huffman_decode(lens, osz, esz, pay)
+
+
+# ---- code lengths > 32 bits (bra_huffman.c:227-261, emit :409-425): tests/golden/edge.json ----------
+def _edge():
+    import json
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "edge.json")) as f:
+        return json.load(f)
+
+
+def fib_input(nsym: int = 34) -> bytes:
+    """The rule of tests/golden/make_edge_golden.py: symbol s repeated F(s + 1) times, ascending."""
+    f = [1, 1]
+    while len(f) < nsym:
+        f.append(f[-1] + f[-2])
+    return b"".join(bytes([s]) * f[s] for s in range(nsym))
+
+
+def test_oracle_huffman_lengths_over_32(orc):
+    import hashlib
+
+    g = _edge()["huffman_fib34"]
+    data = fib_input()
+    assert len(data) == g["size"]
+    lens, osz, esz, pay = orc.huffman_encode(data)
+    assert max(lens) == g["max_length"] == 33
+    assert lens.hex() == g["lengths"] and (osz, esz) == (g["orig_size"], g["encoded_size"])
+    assert hashlib.sha256(pay).hexdigest() == g["payload_sha256"]
+    # the wrapped canonical codes collide: the reference's decoder cannot rebuild the tree
+    assert not g["ref_decodes"]
+    assert orc.huffman_decode(lens, osz, esz, pay) is None
