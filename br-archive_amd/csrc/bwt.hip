@@ -136,10 +136,11 @@ struct TileDesc
     uint32_t bstart;  // bucket slots [bstart, bstart + blen)
     uint32_t blen;
     uint32_t buf;     // KV buffer holding the bucket
-    uint32_t boff;    // block offset in the batch / block length
-    uint32_t nlen;
+    uint32_t poff;    // the block's packed key string (PackDesc): offset, bits, bits per character
+    uint32_t nbits;
     uint32_t kd;      // the payloads carry digits [kd, kd + CARRY)
     uint32_t pdig;    // 1: the bucket stayed in place, its digits are read from the payloads (not dig[])
+    uint32_t pb;
 };
 
 // Ordered tile list of a level: XCD x's part is [xseg[x], xseg[x + 1]) (workgroup w works on
@@ -164,32 +165,77 @@ __device__ __forceinline__ uint32_t tile_pos(const TileOrder& o, uint32_t i, uin
     return p < o.xseg[x + 1] ? p : ~0u;
 }
 
-// STRING-mode payload (64 bits): the rotation index in bits 0-23 and CARRY digits, bytes
+// -------------------------------------------------------------------------------------------------
+// Packed key strings.  Rotations are sorted on their characters mapped to their ranks in the block's
+// alphabet (a monotone map: the order of rotations is unchanged) and packed b bits per character,
+// b = ceil(log2(alphabet size)) in 1..8.  A key byte -- a "virtual byte", the unit of every digit,
+// depth and key below -- then covers 8 / b characters: synthetic text (26 letters, b = 5) needs
+// 1.6x fewer MSD levels and job rounds than raw bytes, 16-symbol data (b = 4) 2x fewer, uniform
+// random bytes (b = 8) are unchanged.  Block k's packed string is its n*b-bit cyclic bitstream
+// (MSB first) followed by its first PACK_EXT_BITS bits again, so any window of up to 136 bits
+// starting inside the stream is contiguous; it lives at packed + PackDesc.poff.  Two rotations are
+// identical once they agree on nvb = ceil(n*b / 8) virtual bytes.
+// -------------------------------------------------------------------------------------------------
+struct PackDesc
+{
+    uint32_t poff;   // byte offset of the block's packed string (block offset + PACK_PAD * block)
+    uint32_t nbits;  // n * b
+    uint32_t b;      // bits per character
+    uint32_t nvb;    // ceil(nbits / 8): depth at which tied rotations are identical
+};
+constexpr uint32_t PACK_PAD      = 96;   // bytes reserved per block beyond n (16-byte alignment, the extension, overreads)
+constexpr uint32_t PACK_EXT_BITS = 384;  // cyclic continuation written after the stream (>= 136 bits + 16-byte overread)
+
+typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
+typedef uint4 __attribute__((aligned(1))) uint4_u;
+
+// bit position of rotation idx's virtual byte vd in its block's cyclic bitstream
+__device__ __forceinline__ uint32_t pk_bitpos(uint32_t b, uint32_t nbits, uint32_t idx, uint32_t vd)
+{
+    uint32_t bp = idx * b + 8u * vd;
+    if (bp >= nbits)
+        bp %= nbits;
+    return bp;
+}
+
+// 64 bits of a packed string from bit bp (bit bp in the MSB)
+__device__ __forceinline__ uint64_t pk_load64(const uint8_t* __restrict__ pk, uint32_t bp)
+{
+    const uint8_t* p  = pk + (bp >> 3);
+    const uint64_t hi = __builtin_bswap64(*reinterpret_cast<const u64_unaligned*>(p));
+    const uint32_t sh = bp & 7;
+    return sh ? (hi << sh) | ((uint64_t) p[8] >> (8 - sh)) : hi;
+}
+
+// 128 bits of a packed string from bit bp: w0 = bits [bp, bp + 64), w1 = the next 64
+__device__ __forceinline__ void pk_load128(const uint8_t* __restrict__ pk, uint32_t bp, uint64_t& w0, uint64_t& w1)
+{
+    const uint8_t* p  = pk + (bp >> 3);
+    const uint4    q  = *reinterpret_cast<const uint4_u*>(p);
+    uint64_t       a  = __builtin_bswap64(((uint64_t) q.y << 32) | q.x);
+    uint64_t       c  = __builtin_bswap64(((uint64_t) q.w << 32) | q.z);
+    const uint32_t sh = bp & 7;
+    if (sh)
+    {
+        const uint64_t e = p[16];
+        a                = (a << sh) | (c >> (64 - sh));
+        c                = (c << sh) | (e >> (8 - sh));
+    }
+    w0 = a;
+    w1 = c;
+}
+
+// STRING-mode payload (64 bits): the rotation index in bits 0-23 and CARRY digits, virtual bytes
 // [kd, kd + CARRY) of the rotation, big-endian in bits 24-63.  A bucket at depth d reads digit
 // d - kd; the scatter that moves an element into a bucket at depth kd + CARRY gathers the next
-// CARRY bytes (one unaligned 8-byte load), so an element costs one gather per CARRY MSD levels.
+// CARRY digits (one 64-bit packed load), so an element costs one gather per CARRY MSD levels.
 constexpr uint32_t CARRY = 5;
 __device__ __forceinline__ uint32_t p_idx(uint64_t P) { return (uint32_t) P & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t p_digit(uint64_t P, uint32_t j) { return (uint32_t) (P >> (56 - 8 * j)) & 0xFFu; }
-typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
-typedef uint4 __attribute__((aligned(1))) uint4_u;
-// payload carrying bytes [st, st + CARRY) (cyclic) of a block of n bytes
-__device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ blk, uint32_t n, uint32_t st, uint32_t idx)
+// payload carrying virtual bytes [vd, vd + CARRY) of rotation idx
+__device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ pk, uint32_t b, uint32_t nbits, uint32_t vd, uint32_t idx)
 {
-    uint64_t k;
-    if (st + 8u <= n)
-        k = __builtin_bswap64(*reinterpret_cast<const u64_unaligned*>(blk + st));
-    else
-    {
-        k          = 0;
-        uint32_t q = st;
-        for (uint32_t i = 0; i < CARRY; ++i)
-        {
-            k = (k << 8) | blk[q];
-            q = (q + 1 == n) ? 0 : q + 1;
-        }
-        k <<= 64 - 8 * CARRY;
-    }
+    const uint64_t k = pk_load64(pk, pk_bitpos(b, nbits, idx, vd));
     return (k & 0xFFFFFFFFFF000000ull) | idx;
 }
 
@@ -245,32 +291,164 @@ struct L0Tile
     uint32_t block, start;
 };
 
-__global__ void __launch_bounds__(TPB) k_l0_hist(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
-                                                 const L0Tile* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ tile_hist)
+// ---- packing (see "Packed key strings") ----
+// Presence mask of the byte values of every block: amask[8 * block + w] bit v = value 32 w + v
+// occurs (zeroed by the host).  Each thread ORs its bytes into 8 registers, the wave reduces them,
+// one atomic per word and wave.
+__global__ void __launch_bounds__(TPB) k_alpha(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
+                                               const L0Tile* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ amask)
+{
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        const L0Tile    T   = tiles[t];
+        const BlockDesc B   = blocks[T.block];
+        const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
+        const uint8_t*  p   = in + B.off + T.start;
+        uint32_t        m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const auto      add  = [&](uint32_t v) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                m[k] |= ((v >> 5) == (uint32_t) k) ? (1u << (v & 31)) : 0u;
+        };
+        if (cnt == TILE && (((uintptr_t) p) & 15) == 0)
+        {
+            const uint4    q    = reinterpret_cast<const uint4*>(p)[threadIdx.x];
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                add((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+        }
+        else
+            for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
+                add(p[i]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+        {
+            uint32_t x = m[k];
+            for (int d = 32; d >= 1; d >>= 1)
+                x |= (uint32_t) __shfl_xor((int) x, d, WAVE);
+            if (lane_id() == 0 && x)
+                atomicOr(&amask[8 * T.block + k], x);
+        }
+    }
+}
+
+// One thread per block: bits per character from the alphabet size, the packed string's place.
+__global__ void k_pack_desc(const BlockDesc* __restrict__ blocks, uint32_t nblocks, const uint32_t* __restrict__ amask, PackDesc* __restrict__ pk)
+{
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nblocks; k += gridDim.x * blockDim.x)
+    {
+        uint32_t a = 0;
+        for (int w = 0; w < 8; ++w)
+            a += __popc(amask[8 * k + w]);
+        const uint32_t  b  = (a <= 2) ? 1u : 32u - __clz(a - 1);
+        const BlockDesc B  = blocks[k];
+        const uint32_t  nb = B.len * b;
+        pk[k]              = PackDesc{(uint32_t) ((B.off + (uint64_t) PACK_PAD * k + 15) & ~15ull), nb, b, (nb + 7) / 8};
+    }
+}
+
+// The packed strings: for every level-0 tile the 32-bit words covering its characters' bits (the
+// last tile of a block also the words of the cyclic extension), character c -> rank of its byte
+// value in the block's alphabet, b bits, MSB first.  Words are stored big-endian (byte 0 = bits 0-7).
+__global__ void __launch_bounds__(TPB) k_pack(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
+                                              const L0Tile* __restrict__ tiles, uint32_t ntiles, const uint32_t* __restrict__ amask,
+                                              const PackDesc* __restrict__ pkd, uint8_t* __restrict__ packed)
+{
+    __shared__ uint8_t  rank[256];
+    __shared__ uint32_t cur_block;
+    if (threadIdx.x == 0)
+        cur_block = ~0u;
+    __syncthreads();
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        const L0Tile T = tiles[t];
+        if (T.block != cur_block)
+        {
+            // rank of byte value v = number of present values below it
+            const uint32_t* m = amask + 8 * T.block;
+            const uint32_t  v = threadIdx.x, w = v >> 5;
+            uint32_t        r = __popc(m[w] & ((1u << (v & 31)) - 1u));
+            for (uint32_t k = 0; k < w; ++k)
+                r += __popc(m[k]);
+            __syncthreads();
+            rank[v] = (uint8_t) r;
+            if (threadIdx.x == 0)
+                cur_block = T.block;
+            __syncthreads();
+        }
+        const BlockDesc B    = blocks[T.block];
+        const PackDesc  P    = pkd[T.block];
+        const uint8_t*  blk  = in + B.off;
+        const uint32_t  b    = P.b;
+        const bool      last = T.start + TILE >= B.len;
+        const uint32_t  w0   = T.start * b / 32;
+        const uint32_t  w1   = last ? (P.nbits + PACK_EXT_BITS + 31) / 32 : (T.start + TILE) * b / 32;
+        uint32_t*       out  = reinterpret_cast<uint32_t*>(packed + P.poff);
+        for (uint32_t w = w0 + threadIdx.x; w < w1; w += TPB)
+        {
+            const uint32_t j0 = 32 * w, c0 = j0 / b, c1 = (j0 + 31) / b;
+            uint64_t       acc = 0;
+            for (uint32_t c = c0; c <= c1; ++c)
+            {
+                uint32_t cc = c;
+                if (cc >= B.len)
+                    cc %= B.len;
+                acc = (acc << b) | rank[blk[cc]];
+            }
+            const uint32_t L = (c1 - c0 + 1) * b, off = j0 - c0 * b;  // acc holds bits [c0 b, c0 b + L)
+            out[w]           = __builtin_bswap32((uint32_t) (acc >> (L - off - 32)));
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// level 0: histograms of the rotations' first virtual byte per tile
+// -------------------------------------------------------------------------------------------------
+// A level-0 tile's packed window in LDS: the bytes of its rotations' first characters plus 16 more
+// (tile starts are multiples of 4096 characters, so the window starts on a 16-byte boundary of the
+// packed string).  win_bits64 reads 64 bits from any bit of it.
+__device__ __forceinline__ void load_window(const uint8_t* __restrict__ pk, uint32_t start, uint32_t cnt, uint32_t b, uint8_t* win)
+{
+    const uint4*   src = reinterpret_cast<const uint4*>(pk + (start * b) / 8);
+    const uint32_t nq  = ((cnt * b + 7) / 8 + 16 + 15) / 16;
+    for (uint32_t i = threadIdx.x; i < nq; i += TPB)
+        reinterpret_cast<uint4*>(win)[i] = src[i];
+}
+
+__device__ __forceinline__ uint64_t win_bits64(const uint8_t* win, uint32_t bit)
+{
+    const uint32_t* w  = reinterpret_cast<const uint32_t*>(win) + (bit >> 5);
+    const uint64_t  hi = ((uint64_t) __builtin_bswap32(w[0]) << 32) | __builtin_bswap32(w[1]);
+    const uint32_t  s  = bit & 31;
+    return s ? (hi << s) | (__builtin_bswap32(w[2]) >> (32 - s)) : hi;
+}
+
+__global__ void __launch_bounds__(TPB) k_l0_hist(const uint8_t* __restrict__ packed, const BlockDesc* __restrict__ blocks,
+                                                 const PackDesc* __restrict__ pkd, const L0Tile* __restrict__ tiles, uint32_t ntiles,
+                                                 uint32_t* __restrict__ tile_hist)
 {
     __shared__ uint32_t h[SCATTER_NC * CSTRIDE];  // counter copies, see TileStagePN
+    __shared__ __attribute__((aligned(16))) uint8_t win[TILE + 64];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
 #pragma unroll
         for (int c = 0; c < SCATTER_NC; ++c)
             h[c * CSTRIDE + threadIdx.x] = 0;
-        __syncthreads();
-        const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
         const L0Tile    T   = tiles[t];
         const BlockDesc B   = blocks[T.block];
+        const PackDesc  P   = pkd[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
-        const uint8_t*  p   = in + B.off + T.start;
-        if (PER_THREAD == 16 && cnt == TILE && (((uintptr_t) p) & 15) == 0)
-        {
-            const uint4    q    = reinterpret_cast<const uint4*>(p)[threadIdx.x];  // 16 bytes per thread
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+        load_window(packed + P.poff, T.start, cnt, P.b, win);
+        __syncthreads();
+        const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                atomicAdd(&h[cp + ((w[i >> 2] >> (8 * (i & 3))) & 0xFF)], 1u);
+        for (int i = 0; i < PER_THREAD; ++i)
+        {
+            const uint32_t e = threadIdx.x + i * TPB;
+            if (e < cnt)
+                atomicAdd(&h[cp + (uint32_t) (win_bits64(win, e * P.b) >> 56)], 1u);
         }
-        else
-            for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
-                atomicAdd(&h[cp + p[i]], 1u);
         __syncthreads();
         uint32_t tot = 0;
 #pragma unroll
@@ -440,6 +618,7 @@ struct ScanArgs
     uint32_t        mjob_max;  // largest workgroup job (256 * waves; JOB_MAX = no workgroup jobs)
     const Counters* lin;       // this level's bucket count (n_big); null: nbuckets (level 0)
     Counters*       lout;      // the next level's buckets / tiles / byte accounting
+    const PackDesc* pk;        // STRING: packed key strings per block
 };
 
 constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into one wave job
@@ -742,11 +921,11 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
                             a.tile_bucket_next[t0 + t] = slot;
                         if (MODE == MODE_STRING)
                         {
-                            const BlockDesc BD = a.blocks[B.block];
+                            const PackDesc P = a.pk[B.block];
                             for (uint32_t t = 0; t < ntl[r]; ++t)
                                 a.tdesc_next[t0 + t] = TileDesc{t0 + t, slot, s0 + t * TILE, min((uint32_t) TILE, tot[r] - t * TILE), nd,
-                                                                s0, tot[r], obuf, (uint32_t) BD.off, BD.len, kd,
-                                                                (nomove && !regather) ? 1u : 0u};
+                                                                s0, tot[r], obuf, P.poff, P.nbits, kd,
+                                                                (nomove && !regather) ? 1u : 0u, P.b};
                         }
                     }
                     else
@@ -900,39 +1079,22 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
     }
 }
 
-// Level 0: every element gets its payload carrying rotation bytes 1..CARRY (the next digits).
-__global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
-                                                    const L0Tile* __restrict__ tiles, uint32_t ntiles,
+// Level 0: every element gets its payload carrying virtual bytes 1..CARRY (the next digits).
+__global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ packed, const BlockDesc* __restrict__ blocks,
+                                                    const PackDesc* __restrict__ pkd, const L0Tile* __restrict__ tiles, uint32_t ntiles,
                                                     const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay,
                                                     uint8_t* __restrict__ odig)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
-    uint8_t*     win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageL0));  // TILE + 32 bytes, 16-aligned
+    uint8_t*     win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageL0));  // TILE + 48 bytes, 16-aligned
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile    T   = tiles[t];
         const BlockDesc B   = blocks[T.block];
+        const PackDesc  P   = pkd[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
-        const uint8_t*  blk = in + B.off;
-        // window: win[i + 15] = byte (start - 1 + i) of the block, cyclic; i in [0, cnt + 9)
-        const uint8_t* src = blk + T.start;
-        if (T.start >= 16 && T.start + cnt + 16 <= B.len && (((uintptr_t) src) & 15) == 0)
-        {
-            // interior tile: 16-byte copies of [start - 16, start + cnt + 16)
-            for (uint32_t i = threadIdx.x; i < (cnt + 32) / 16; i += TPB)
-                reinterpret_cast<uint4*>(win)[i] = reinterpret_cast<const uint4*>(src - 16)[i];
-        }
-        else
-        {
-            for (uint32_t i = threadIdx.x; i < cnt + 9; i += TPB)
-            {
-                uint32_t q = T.start + i + B.len - 1;  // >= 0, < 3 * len for any block length
-                while (q >= B.len)
-                    q -= B.len;
-                win[i + 15] = blk[q];
-            }
-        }
+        load_window(packed + P.poff, T.start, cnt, P.b, win);
         stage_zero(S);
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x] & ~NEXT_FLAG;
         __syncthreads();
@@ -941,7 +1103,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
         for (int i = 0; i < PER_THREAD; ++i)
         {
             const uint32_t e = threadIdx.x + i * TPB;
-            dg[i]            = win[e + 16];  // rotation byte 0 (e < cnt; unused otherwise)
+            dg[i]            = (e < cnt) ? (uint32_t) (win_bits64(win, e * P.b) >> 56) : 0u;  // virtual byte 0
             v[i]             = (dg[i] << 24) | e;
         }
         stage_p(S, v, dg, cnt);
@@ -954,16 +1116,11 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                 const uint32_t vv   = (uint32_t) S.pay[q];
                 const uint32_t dd   = vv >> 24, e = vv & 0xFFFFFFu;
                 const uint32_t slot = S.goff[dd] + (q - S.base[dd]);
-                // window bytes [e + 16, e + 24) = rotation bytes 0..7: keep bytes 1..CARRY
-                const uint32_t  o  = e + 16;
-                const uint32_t* w4 = reinterpret_cast<const uint32_t*>(win) + (o >> 2);
-                const uint32_t  a0 = w4[0], a1 = w4[1], a2 = w4[2], sh = o & 3;
-                const uint32_t  lo = __builtin_amdgcn_alignbyte(a1, a0, sh), hi = __builtin_amdgcn_alignbyte(a2, a1, sh);
-                const uint64_t  kk = __builtin_bswap64(((uint64_t) hi << 32) | lo);
+                const uint64_t kk   = win_bits64(win, e * P.b);  // virtual bytes 0..7: keep bytes 1..CARRY
                 if (BRA_DCHECK(slot >= B.off && slot < B.off + B.len, "l0 scatter slot %u outside block %u", slot, T.block))
                 {
                     opay[slot] = ((kk << 8) & 0xFFFFFFFFFF000000ull) | (T.start + e);
-                    odig[slot] = (uint8_t) (kk >> 48);  // rotation byte 1: the level-1 digit
+                    odig[slot] = (uint8_t) (kk >> 48);  // virtual byte 1: the level-1 digit
                 }
             }
         }
@@ -976,7 +1133,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
 // the input (the block is in the XCD's L2); all others keep their payload (jobs only use the
 // index).  nomove 1: the bucket stays as it is; 2: it stays in place but continues and its
 // payloads are re-gathered in place.
-__global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict__ in, const uint8_t* __restrict__ nomove,
+__global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict__ packed, const uint8_t* __restrict__ nomove,
                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ pay0,
                                                    uint64_t* __restrict__ pay1, const Counters* __restrict__ lv, TileOrder to,
                                                    uint8_t* __restrict__ dig0, uint8_t* __restrict__ dig1)
@@ -994,19 +1151,15 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
         if (nm == 1)
             continue;  // uniform per workgroup: the bucket stays as it is (the next level reads its digits from the payloads)
         const uint32_t t   = D.t;
-        const uint8_t* blk = in + D.boff;
+        const uint8_t* pk  = packed + D.poff;
         const uint32_t cnt = D.cnt;
-        struct
-        {
-            uint32_t off, len;
-        } BD{D.boff, D.nlen};
         struct
         {
             uint32_t start, len, d, buf;
         } B{D.bstart, D.blen, D.d, D.buf};
         const uint32_t  j  = B.d - D.kd;              // this level's digit in the payload
         const bool      rg = j + 1 >= CARRY;          // next-level buckets start a new carry
-        const uint32_t  dn = (B.d + 1) % BD.len;      // their first digit's depth
+        const uint32_t  dn = B.d + 1;                 // their first digit's depth
         const size_t    s0 = D.s0;
         uint64_t*       ip = (B.buf ? pay1 : pay0) + s0;
         uint8_t*        id = (B.buf ? dig1 : dig0) + s0;
@@ -1027,10 +1180,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                 if (e < cnt)
                 {
                     const uint32_t idx = p_idx(v[i]);
-                    uint32_t       st  = idx + dn;
-                    if (st >= BD.len)
-                        st -= BD.len;
-                    const uint64_t np = p_make(blk, BD.len, st, idx);
+                    const uint64_t np  = p_make(pk, D.pb, D.nbits, dn, idx);
                     ip[e]             = np;
                     id[e]             = (uint8_t) p_digit(np, 0);
                 }
@@ -1066,11 +1216,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                 uint64_t       nv   = vv;
                 if (rg && (g & NEXT_FLAG))
                 {
-                    const uint32_t idx = p_idx(vv);
-                    uint32_t       st  = idx + dn;
-                    if (st >= BD.len)
-                        st -= BD.len;
-                    nv = p_make(blk, BD.len, st, idx);
+                    nv = p_make(pk, D.pb, D.nbits, dn, p_idx(vv));
                 }
                 if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
                 {
@@ -1167,6 +1313,8 @@ struct JobArgs
     const uint32_t*  dxseg;    // non-null: the per-XCD list ranges live in device memory (k_job_prefix), not in xseg
     uint32_t*        jq;       // dynamic order (xcd_major only): per-XCD claim counters, 32 dwords apart; null = static ranges
     uint32_t         jq_chunk; // jobs a wave claims at once
+    const uint8_t*   packed;   // STRING: packed key strings (keys are gathered from them)
+    const PackDesc*  pk;
 };
 
 // Hardware id (0-7) of the XCD the calling wave runs on.  Speed only: the job queues below stay
@@ -1348,30 +1496,6 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
         ex[r] += pre;
     total = wtot;
 }
-
-// 16 cyclic bytes at `start` (< n): (bytes 0-7, bytes 8-15), big-endian.  A non-wrapping read is
-// one 16-byte load at the byte address (gfx950 global loads need no alignment; one L2 request
-// unless it straddles a line, where two aligned loads always made two).
-
-__device__ __forceinline__ void load_key16(const uint8_t* __restrict__ blk, uint32_t n, uint32_t start, uint64_t& w0, uint64_t& w1)
-{
-    if (start + 16u <= n)
-    {
-        const uint4 q = *reinterpret_cast<const uint4_u*>(blk + start);
-        w0            = __builtin_bswap64(((uint64_t) q.y << 32) | q.x);
-        w1            = __builtin_bswap64(((uint64_t) q.w << 32) | q.z);
-        return;
-    }
-    w0          = load_key8(blk, n, start);
-    uint32_t s2 = start + 8;
-    while (s2 >= n)
-        s2 -= n;
-    w1 = load_key8(blk, n, s2);
-}
-
-
-// 128-bit key (kh, kl) "greater than"; keys are unique (the slot is in the low bits of kl).
-__device__ __forceinline__ bool k2_gt(uint64_t ha, uint64_t la, uint64_t hb, uint64_t lb) { return ha > hb || (ha == hb && la > lb); }
 
 // One bitonic stage whose partners sit LM lanes away (same element r): exchanged with DPP /
 // permlane swaps.  k[i][r] = dword i of element r's key.
@@ -1664,7 +1788,11 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     using G                 = JobGeom<W>;
     const int       lane    = lane_id();
     const BlockDesc BD      = a.blocks[J.block];
-    const uint8_t*  blk     = a.in + BD.off;
+    const uint8_t*  blk     = a.in + BD.off;  // raw bytes: the BWT output byte of a rotation
+    PackDesc        PK{0, 8, 8, 1};
+    if (MODE == MODE_STRING)
+        PK = a.pk[J.block];
+    const uint8_t*  pkb     = a.packed + PK.poff;
     const uint64_t* K       = J.buf ? a.key1 : a.key0;
     const uint32_t* V       = J.buf ? a.pay1 : a.pay0;
     const uint32_t  boff    = (uint32_t) BD.off;
@@ -1705,16 +1833,13 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 // STRING payloads carry an MSD digit in the top byte: replace it by the rotation's
                 // previous byte (its BWT output byte), gathered together with the key
                 const uint32_t idx = v[r] & 0xFFFFFFu;
-                uint32_t       st  = idx + ((depth - 1) % BD.len);
-                if (st >= BD.len)
-                    st -= BD.len;
 #ifdef BRA_EXP_NOGATHER
                 const uint8_t lb = 0;  // measurement variant: no gathers (results are wrong)
-                uint64_t      w0 = 0, w1 = ((uint64_t) idx << 20) ^ st;
+                uint64_t      w0 = 0, w1 = ((uint64_t) idx << 20) ^ depth;
 #else
                 const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
                 uint64_t      w0, w1;
-                load_key16(blk, BD.len, st, w0, w1);
+                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, depth - 1), w0, w1);
 #endif
                 make_key1<W>(c, w0, w1, kh[r], kl[r]);
                 v[r] = ((uint32_t) lb << 24) | idx;
@@ -1760,7 +1885,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         const bool any    = job_groups<W>(kh, km, T, S, wj, g, gend, tied);
         bool       finish = (MODE == MODE_RANK) || !any;
         bool final_ties = false, to_fallback = false;
-        if (!finish && depth >= BD.len)
+        if (!finish && depth >= PK.nvb)  // tied on every bit of the cyclic string: identical rotations
             finish = final_ties = true;
         else if (!finish && depth >= a.dcap)
             finish = to_fallback = true;
@@ -1831,11 +1956,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             {
                 const uint64_t gp = S.kh[c];
                 pos[r]            = (uint32_t) (gp & 0xFFFF);
-                uint32_t st       = (S.v[c] & 0xFFFFFFu) + (depth % BD.len);
-                if (st >= BD.len)
-                    st -= BD.len;
                 uint64_t w0, w1;
-                load_key16(blk, BD.len, st, w0, w1);
+                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth), w0, w1);
                 make_key<W>((uint32_t) (gp >> 16), c, w0, w1, kh[r], kl[r]);
             }
             else
@@ -2111,7 +2233,7 @@ __global__ void __launch_bounds__(256) k_job_prefix(const uint32_t* __restrict__
 
 __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__ buckets, const uint32_t* __restrict__ tile_bucket,
                                                       const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q, uint32_t nkeys,
-                                                      uint32_t* __restrict__ cursor, const BlockDesc* __restrict__ blocks,
+                                                      uint32_t* __restrict__ cursor, const PackDesc* __restrict__ pkd,
                                                       const TileDesc* __restrict__ nat, TileDesc* __restrict__ order)
 {
     extern __shared__ uint32_t h[];
@@ -2146,11 +2268,11 @@ __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__
             {
                 const uint32_t  bi = tile_bucket[j];
                 const Bucket    B  = buckets[bi];
-                const BlockDesc BD = blocks[B.block];
+                const PackDesc  P  = pkd[B.block];
                 const uint32_t  f  = (j - B.tile0) * TILE;
                 order[h[key[i]] + rank[i]] =
-                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, (uint32_t) BD.off, BD.len, B.kd,
-                             nat[j].pdig};
+                    TileDesc{j, bi, B.start + f, min((uint32_t) TILE, B.len - f), B.d, B.start, B.len, B.buf, P.poff, P.nbits, B.kd,
+                             nat[j].pdig, P.b};
             }
         }
         __syncthreads();
@@ -2211,6 +2333,15 @@ __global__ void k_group_mark(const Group* __restrict__ groups, uint32_t ng, cons
         if (threadIdx.x == 0)
             flag[b] = 1;
     }
+}
+
+// Fallback groups from the MSD levels and the jobs carry virtual-byte depths: their members share
+// 8 * depth bits of the packed string, i.e. at least floor(8 * depth / b) whole characters, the depth
+// unit of the prefix doubling below (a smaller depth is still a valid one, see k_rank_keys).
+__global__ void k_group_depth_chars(Group* __restrict__ groups, uint32_t ng, const PackDesc* __restrict__ pkd)
+{
+    for (uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x; gi < ng; gi += gridDim.x * blockDim.x)
+        groups[gi].depth = (uint32_t) ((8ull * groups[gi].depth) / pkd[groups[gi].block & 0x3FFFFFFFu].b);
 }
 
 // Gather rank keys for all members of the round's groups; they become level-0 RANK buckets (buf 0).
@@ -2357,6 +2488,9 @@ struct BwtWorkspace
     Mail*     h_mail         = nullptr;  // pinned, device-written mailbox records (one per level slot)
     uint32_t  mail_seq       = 0;
     L0Tile*   l0tiles        = nullptr;
+    uint8_t*  packed         = nullptr;  // packed key strings (PackDesc.poff), N + PACK_PAD per block
+    PackDesc* pkd            = nullptr;  // per block
+    uint32_t* amask          = nullptr;  // per block: 256-bit presence mask of the byte values
     std::vector<BlockDesc> geo;          // block geometry the level-0 tiles / buckets on the device were built for
     uint32_t  nt0 = 0;
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
@@ -2512,7 +2646,7 @@ static void ws_free(BwtWorkspace& w)
         (void) hipFree(w.dig[i]);
     }
     void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
-                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b};
+                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask};
     for (void* p : dev)
         (void) hipFree(p);
     if (w.h_ctr)
@@ -2589,7 +2723,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
          dev_alloc(w.jobs, w.cap_jobs) && dev_alloc(w.mjobs, w.cap_mjobs) && dev_alloc(w.jobs_sorted, cap_sorted) &&
          dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 8 * nkeys) && dev_alloc(w.jseg, 3 * 16) &&
          dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
-         dev_alloc(w.jobq, 3 * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B);
+         dev_alloc(w.jobq, 3 * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
+         dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B);
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -2656,7 +2791,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                 BRA_DSYNC(s);
                 hipLaunchKernelGGL(k_tile_prefix, dim3(1), dim3(256), 0, s, cnt, nk, kb, cur_, xs); BRA_DSYNC(s);
                 hipLaunchKernelGGL(k_tile_scatter, g, dim3(256), nk * 4, s, w.big[cur], w.tile_bucket[cur], &lin->n_tiles_next, kb, q, nk, cur_,
-                                   d_blocks, w.tdesc[cur], w.tile_order);
+                                   w.pkd, w.tdesc[cur], w.tile_order);
                 BRA_DSYNC(s);
                 to = TileOrder{w.tile_order, xs, 0};
             }
@@ -2668,7 +2803,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             ScanArgs a{d_blocks, w.big[cur],  0,           w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
                        w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
                        w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
-                       (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout};
+                       (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout, w.pkd};
             {
                 BRA_PROF(P_BWT_SCAN, s);
                 hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
@@ -2676,8 +2811,8 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             {
                 BRA_PROF(P_BWT_SCATTER, s);
                 if (MODE == MODE_STRING)
-                    hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, d_in, w.nomove, w.tile_off, w.key[0], w.key[1],
-                                       lin, to, w.dig[0], w.dig[1]);
+                    hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, w.packed, w.nomove, w.tile_off, w.key[0],
+                                       w.key[1], lin, to, w.dig[0], w.dig[1]);
                 else
                     hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], lin, w.tile_off,
                                        w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
@@ -2777,7 +2912,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageL0) + TILE + 48)));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageL0) + TILE + 64)));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
@@ -2809,22 +2944,33 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     hipLaunchKernelGGL(k_ctr_init, dim3(1), dim3(1024), 0, s, w.ctr, MAX_LEVELS);
     BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, nblocks, s));
     {
+        // packed key strings: alphabet per block, bits per character, the packed cyclic strings
+        BRA_PROF(P_BWT_PACK, s);
+        BRA_HIP_CHECK(hipMemsetAsync(w.amask, 0, 32ull * nblocks, s));
+        hipLaunchKernelGGL(k_alpha, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.amask); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_pack_desc, dim3(div_up(nblocks, 256)), dim3(256), 0, s, d_blocks, nblocks, w.amask, w.pkd); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_pack, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.amask, w.pkd, w.packed);
+        BRA_DSYNC(s);
+    }
+    {
         BRA_PROF(P_BWT_L0HIST, s);
-        hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tile_hist); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_l0_hist, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, w.packed, d_blocks, w.pkd, w.l0tiles, nt0, w.tile_hist);
+        BRA_DSYNC(s);
     }
     ScanArgs a0{d_blocks, w.l0b,     nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
-                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1};
+                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1, w.pkd};
     {
         BRA_PROF(P_BWT_SCAN, s);
         hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(div_up(nblocks, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a0); BRA_DSYNC(s);
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
-        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageL0) + TILE + 48, s, d_in, d_blocks,
-                           w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, w.packed, d_blocks,
+                           w.pkd, w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
+    prof_bytes(P_BWT_PACK, 3.0 * (double) N);  // input read twice, packed string written (<= N)
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
     prof_bytes(P_BWT_L0SCATTER, 9.0 * N + 1024.0 * nt0);  // window in, payload out
@@ -2834,7 +2980,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
 
     // ---- jobs (counts and list ranges stay on the device) ----
     JobArgs ja{w.jobs,  0,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
-               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0};
+               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0, w.packed, w.pkd};
     JobArgs jm = ja;
     jm.jobs    = w.mjobs;
     JobArgs ord[3];
@@ -2897,6 +3043,8 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return true;
     BRA_PROF(P_BWT_FALLBACK, s);
     int gcur = 0;
+    hipLaunchKernelGGL(k_group_depth_chars, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pkd);
+    BRA_DSYNC(s);
     hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.key[0], w.key[1], w.fsa); BRA_DSYNC(s);
     // mark blocks, build ranks: singletons rank = own slot, group members = group start
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
@@ -2925,7 +3073,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         const uint32_t ng_big = mr.n_groups;
         const uint32_t nj     = mr.n_jobs;
         JobArgs jr{w.jobs, nj, d_in, d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi, w.isa, gnext, w.cap_groups,
-                   w.ctr,  0,  hmin, 0, {}, nullptr, nullptr, 0};
+                   w.ctr,  0,  hmin, 0, {}, nullptr, nullptr, 0, w.packed, w.pkd};
         if (ng_big)
             hipLaunchKernelGGL(k_rank_flush, dim3(std::min<uint32_t>(ng_big, 4096u)), dim3(256), 0, s, gnext, ng_big, d_blocks, w.pay[0],
                                w.pay[1], w.fsa, d_L, w.isa, d_pi); BRA_DSYNC(s);
