@@ -179,6 +179,10 @@ struct OpAdd
 {
     __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
 };
+struct OpOr
+{
+    __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; }
+};
 
 // Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order.
 // Inclusive scan over the lanes of a wave in increasing (FWD) or decreasing lane order; with `ex`,

@@ -292,12 +292,14 @@ struct L0Tile
 };
 
 // ---- packing (see "Packed key strings") ----
-// Presence mask of the byte values of every block: amask[8 * block + w] bit v = value 32 w + v
-// occurs (zeroed by the host).  Each thread ORs its bytes into 8 registers, the wave reduces them,
-// one atomic per word and wave.
+// Presence mask of the byte values of every level-0 tile: tmask[8 * tile + w] bit v = value 32 w + v
+// occurs.  Each thread ORs its 16 bytes into 8 registers, DPP scans OR them over the wave, LDS over
+// the workgroup; plain stores, no atomics (same-address device atomics from every tile of a block
+// serialised this pass to half a millisecond).
 __global__ void __launch_bounds__(TPB) k_alpha(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
-                                               const L0Tile* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ amask)
+                                               const L0Tile* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ tmask)
 {
+    __shared__ uint32_t part[TPB / WAVE][8];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile    T   = tiles[t];
@@ -321,49 +323,86 @@ __global__ void __launch_bounds__(TPB) k_alpha(const uint8_t* __restrict__ in, c
         else
             for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
                 add(p[i]);
+        const uint32_t wv = threadIdx.x / WAVE;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
         {
-            uint32_t x = m[k];
-            for (int d = 32; d >= 1; d >>= 1)
-                x |= (uint32_t) __shfl_xor((int) x, d, WAVE);
-            if (lane_id() == 0 && x)
-                atomicOr(&amask[8 * T.block + k], x);
+            const uint32_t x = wave_scan<true>(m[k], 0u, OpOr());
+            if (lane_id() == WAVE - 1)
+                part[wv][k] = x;
         }
+        __syncthreads();
+        if (threadIdx.x < 8)
+        {
+            uint32_t x = 0;
+            for (uint32_t v = 0; v < TPB / WAVE; ++v)
+                x |= part[v][threadIdx.x];
+            tmask[8 * (size_t) t + threadIdx.x] = x;
+        }
+        __syncthreads();
     }
 }
 
-// One thread per block: bits per character from the alphabet size, the packed string's place.
-__global__ void k_pack_desc(const BlockDesc* __restrict__ blocks, uint32_t nblocks, const uint32_t* __restrict__ amask, PackDesc* __restrict__ pk)
+// One workgroup per block: the block's presence mask (OR of its tiles' masks), bits per character
+// from the alphabet size, the packed string's place.
+__global__ void __launch_bounds__(TPB) k_pack_desc(const BlockDesc* __restrict__ blocks, const Bucket* __restrict__ l0b, uint32_t nblocks,
+                                                   const uint32_t* __restrict__ tmask, uint32_t* __restrict__ amask, PackDesc* __restrict__ pk)
 {
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nblocks; k += gridDim.x * blockDim.x)
+    __shared__ uint32_t part[TPB / WAVE][8];
+    for (uint32_t k = blockIdx.x; k < nblocks; k += gridDim.x)
     {
-        uint32_t a = 0;
-        for (int w = 0; w < 8; ++w)
-            a += __popc(amask[8 * k + w]);
-        const uint32_t  b  = (a <= 2) ? 1u : 32u - __clz(a - 1);
         const BlockDesc B  = blocks[k];
-        const uint32_t  nb = B.len * b;
-        pk[k]              = PackDesc{(uint32_t) ((B.off + (uint64_t) PACK_PAD * k + 15) & ~15ull), nb, b, (nb + 7) / 8};
+        const uint32_t  t0 = l0b[k].tile0, nt = div_up(B.len, TILE);
+        uint32_t        m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t t = threadIdx.x; t < nt; t += TPB)
+        {
+            const uint4 a = reinterpret_cast<const uint4*>(tmask + 8 * (size_t) (t0 + t))[0];
+            const uint4 b = reinterpret_cast<const uint4*>(tmask + 8 * (size_t) (t0 + t))[1];
+            m[0] |= a.x, m[1] |= a.y, m[2] |= a.z, m[3] |= a.w, m[4] |= b.x, m[5] |= b.y, m[6] |= b.z, m[7] |= b.w;
+        }
+        const uint32_t wv = threadIdx.x / WAVE;
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+        {
+            const uint32_t x = wave_scan<true>(m[w], 0u, OpOr());
+            if (lane_id() == WAVE - 1)
+                part[wv][w] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            uint32_t a = 0;
+            for (int w = 0; w < 8; ++w)
+            {
+                uint32_t x = 0;
+                for (uint32_t v = 0; v < TPB / WAVE; ++v)
+                    x |= part[v][w];
+                amask[8 * k + w] = x;
+                a += __popc(x);
+            }
+            const uint32_t b  = (a <= 2) ? 1u : 32u - __clz(a - 1);
+            const uint32_t nb = B.len * b;
+            pk[k]             = PackDesc{(uint32_t) ((B.off + (uint64_t) PACK_PAD * k + 15) & ~15ull), nb, b, (nb + 7) / 8};
+        }
+        __syncthreads();
     }
 }
 
-// The packed strings: for every level-0 tile the 32-bit words covering its characters' bits (the
-// last tile of a block also the words of the cyclic extension), character c -> rank of its byte
-// value in the block's alphabet, b bits, MSB first.  Words are stored big-endian (byte 0 = bits 0-7).
+// The packed strings.  Per level-0 tile: the character codes (rank of the byte value in the block's
+// alphabet) are staged in LDS, every 8 consecutive characters give exactly b output bytes (8 b
+// bits, MSB first), assembled in LDS and stored with 16-byte stores.  The last tile of a block also
+// writes the cyclic extension (codes of the block's first characters again).
+constexpr uint32_t PACK_XCH = PACK_EXT_BITS + 64;  // characters staged beyond a block's last tile (b >= 1)
 __global__ void __launch_bounds__(TPB) k_pack(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
                                               const L0Tile* __restrict__ tiles, uint32_t ntiles, const uint32_t* __restrict__ amask,
                                               const PackDesc* __restrict__ pkd, uint8_t* __restrict__ packed)
 {
     __shared__ uint8_t  rank[256];
-    __shared__ uint32_t cur_block;
-    if (threadIdx.x == 0)
-        cur_block = ~0u;
-    __syncthreads();
+    __shared__ __attribute__((aligned(16))) uint8_t code[TILE + PACK_XCH];
+    __shared__ __attribute__((aligned(16))) uint8_t obuf[TILE + PACK_XCH];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile T = tiles[t];
-        if (T.block != cur_block)
         {
             // rank of byte value v = number of present values below it
             const uint32_t* m = amask + 8 * T.block;
@@ -371,34 +410,58 @@ __global__ void __launch_bounds__(TPB) k_pack(const uint8_t* __restrict__ in, co
             uint32_t        r = __popc(m[w] & ((1u << (v & 31)) - 1u));
             for (uint32_t k = 0; k < w; ++k)
                 r += __popc(m[k]);
-            __syncthreads();
             rank[v] = (uint8_t) r;
-            if (threadIdx.x == 0)
-                cur_block = T.block;
-            __syncthreads();
         }
+        __syncthreads();
         const BlockDesc B    = blocks[T.block];
         const PackDesc  P    = pkd[T.block];
-        const uint8_t*  blk  = in + B.off;
+        const uint8_t*  src  = in + B.off + T.start;
         const uint32_t  b    = P.b;
+        const uint32_t  cnt  = min((uint32_t) TILE, B.len - T.start);
         const bool      last = T.start + TILE >= B.len;
-        const uint32_t  w0   = T.start * b / 32;
-        const uint32_t  w1   = last ? (P.nbits + PACK_EXT_BITS + 31) / 32 : (T.start + TILE) * b / 32;
-        uint32_t*       out  = reinterpret_cast<uint32_t*>(packed + P.poff);
-        for (uint32_t w = w0 + threadIdx.x; w < w1; w += TPB)
+        // characters to emit: the tile's, plus (last tile) enough of the cyclic continuation to
+        // cover PACK_EXT_BITS bits, in whole groups of 8
+        const uint32_t  ngrp = last ? (cnt * b + PACK_EXT_BITS + 8 * b - 1) / (8 * b) : cnt / 8;
+        const uint32_t  nch  = 8 * ngrp;
+        if (cnt == TILE && (((uintptr_t) src) & 15) == 0)
         {
-            const uint32_t j0 = 32 * w, c0 = j0 / b, c1 = (j0 + 31) / b;
-            uint64_t       acc = 0;
-            for (uint32_t c = c0; c <= c1; ++c)
-            {
-                uint32_t cc = c;
-                if (cc >= B.len)
-                    cc %= B.len;
-                acc = (acc << b) | rank[blk[cc]];
-            }
-            const uint32_t L = (c1 - c0 + 1) * b, off = j0 - c0 * b;  // acc holds bits [c0 b, c0 b + L)
-            out[w]           = __builtin_bswap32((uint32_t) (acc >> (L - off - 32)));
+            const uint4    q    = reinterpret_cast<const uint4*>(src)[threadIdx.x];
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            uint32_t       o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                o[k] = (uint32_t) rank[w[k] & 0xFF] | (uint32_t) rank[(w[k] >> 8) & 0xFF] << 8 | (uint32_t) rank[(w[k] >> 16) & 0xFF] << 16 |
+                       (uint32_t) rank[w[k] >> 24] << 24;
+            reinterpret_cast<uint4*>(code)[threadIdx.x] = make_uint4(o[0], o[1], o[2], o[3]);
+            for (uint32_t i = TILE + threadIdx.x; i < nch; i += TPB)
+                code[i] = rank[in[B.off + (T.start + i) % B.len]];
         }
+        else
+            for (uint32_t i = threadIdx.x; i < nch; i += TPB)
+            {
+                uint32_t c = T.start + i;
+                if (c >= B.len)
+                    c %= B.len;
+                code[i] = rank[in[B.off + c]];
+            }
+        __syncthreads();
+        for (uint32_t g = threadIdx.x; g < ngrp; g += TPB)
+        {
+            const uint2    q   = reinterpret_cast<const uint2*>(code)[g];
+            uint64_t       acc = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                acc = (acc << b) | ((i < 4 ? q.x >> (8 * i) : q.y >> (8 * (i - 4))) & 0xFFu);
+            acc <<= 64 - 8 * b;  // the group's 8 b bits, MSB first
+            for (uint32_t k = 0; k < b; ++k)
+                obuf[g * b + k] = (uint8_t) (acc >> (56 - 8 * k));
+        }
+        __syncthreads();
+        uint8_t*       out  = packed + P.poff + (size_t) T.start * b / 8;  // 16-byte aligned (tile starts are multiples of 4096)
+        const uint32_t nout = ngrp * b;
+        for (uint32_t i = threadIdx.x; i < (nout + 15) / 16; i += TPB)
+            reinterpret_cast<uint4*>(out)[i] = reinterpret_cast<const uint4*>(obuf)[i];
+        __syncthreads();
     }
 }
 
@@ -1837,7 +1900,11 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 const uint8_t lb = 0;  // measurement variant: no gathers (results are wrong)
                 uint64_t      w0 = 0, w1 = ((uint64_t) idx << 20) ^ depth;
 #else
+#ifdef BRA_EXP_NOLB
+                const uint8_t lb = 0;  // measurement variant: no BWT-byte gather (results are wrong)
+#else
                 const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
+#endif
                 uint64_t      w0, w1;
                 pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, depth - 1), w0, w1);
 #endif
@@ -2491,6 +2558,7 @@ struct BwtWorkspace
     uint8_t*  packed         = nullptr;  // packed key strings (PackDesc.poff), N + PACK_PAD per block
     PackDesc* pkd            = nullptr;  // per block
     uint32_t* amask          = nullptr;  // per block: 256-bit presence mask of the byte values
+    uint32_t* tmask          = nullptr;  // per level-0 tile: the same mask
     std::vector<BlockDesc> geo;          // block geometry the level-0 tiles / buckets on the device were built for
     uint32_t  nt0 = 0;
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
@@ -2646,7 +2714,7 @@ static void ws_free(BwtWorkspace& w)
         (void) hipFree(w.dig[i]);
     }
     void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
-                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask};
+                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask};
     for (void* p : dev)
         (void) hipFree(p);
     if (w.h_ctr)
@@ -2724,7 +2792,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
          dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 8 * nkeys) && dev_alloc(w.jseg, 3 * 16) &&
          dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
          dev_alloc(w.jobq, 3 * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
-         dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B);
+         dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B) &&
+         dev_alloc(w.tmask, 8ull * w.cap_l0);
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -2946,9 +3015,9 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     {
         // packed key strings: alphabet per block, bits per character, the packed cyclic strings
         BRA_PROF(P_BWT_PACK, s);
-        BRA_HIP_CHECK(hipMemsetAsync(w.amask, 0, 32ull * nblocks, s));
-        hipLaunchKernelGGL(k_alpha, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.amask); BRA_DSYNC(s);
-        hipLaunchKernelGGL(k_pack_desc, dim3(div_up(nblocks, 256)), dim3(256), 0, s, d_blocks, nblocks, w.amask, w.pkd); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_alpha, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.tmask); BRA_DSYNC(s);
+        hipLaunchKernelGGL(k_pack_desc, dim3(std::min<uint32_t>(nblocks, 4096u)), dim3(TPB), 0, s, d_blocks, w.l0b, nblocks, w.tmask, w.amask, w.pkd);
+        BRA_DSYNC(s);
         hipLaunchKernelGGL(k_pack, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), 0, s, d_in, d_blocks, w.l0tiles, nt0, w.amask, w.pkd, w.packed);
         BRA_DSYNC(s);
     }
