@@ -83,13 +83,17 @@ struct Tiling
     }
 };
 
-constexpr uint32_t MTF_SEG = 2048;  // symbols per thread-segment
+constexpr uint32_t MTF_SEG     = 2048;  // symbols per thread-segment (decode)
+constexpr uint32_t MTF_SEG_ENC = 1024;  // encode segments: twice the threads, for the register-table kernel
+constexpr uint32_t MTF_REG     = 32;    // table entries the register kernel keeps (blocks of <= 32 distinct symbols)
 
 struct MtfWorkspace
 {
-    Tiling tiling;
-    void*  state     = nullptr;
-    size_t cap_state = 0;
+    Tiling    tiling;
+    void*     state     = nullptr;
+    size_t    cap_state = 0;
+    uint32_t* nsym      = nullptr;  // distinct symbols per block (k_mtf_scan)
+    uint32_t  cap_nsym  = 0;
 
     bool reserve(size_t bytes)
     {
@@ -102,12 +106,25 @@ struct MtfWorkspace
         cap_state = c;
         return true;
     }
+    bool reserve_blocks(uint32_t nblocks)
+    {
+        if (nblocks <= cap_nsym)
+            return true;
+        cap_nsym = 0;
+        if (!dev_alloc(nsym, (uint64_t) nblocks + 64))
+            return false;
+        cap_nsym = nblocks + 64;
+        return true;
+    }
     void release()
     {
         tiling.release();
         (void) hipFree(state);
+        (void) hipFree(nsym);
         state     = nullptr;
+        nsym      = nullptr;
         cap_state = 0;
+        cap_nsym  = 0;
     }
 };
 

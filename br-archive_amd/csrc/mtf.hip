@@ -37,7 +37,19 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
         __syncthreads();
         const Piece    P = segs[s];
         const uint8_t* p = in + P.off;
-        if (P.len == MTF_SEG && (P.off & 7) == 0)
+        if (P.len == 4 * TPB && (P.off & 3) == 0)
+        {
+            const uint32_t w    = reinterpret_cast<const uint32_t*>(p)[threadIdx.x];
+            const int32_t  base = (int32_t) threadIdx.x * 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+            {
+                const uint32_t c = (w >> (8 * i)) & 0xFF;
+                if (i == 3 || c != ((w >> (8 * i + 8)) & 0xFF))
+                    atomicMax(&lo[c], base + i);
+            }
+        }
+        else if (P.len == 8 * TPB && (P.off & 7) == 0)
         {
             // 8 consecutive bytes per thread: only the last byte of each equal run inside them
             // updates LDS (post-BWT input is run-heavy, and same-address LDS atomics serialise)
@@ -63,7 +75,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
 
 // One workgroup per block; thread c scans symbol c over the block's segments (exclusive max).
 __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
-                                                  uint32_t nblocks, int32_t* __restrict__ state)
+                                                  uint32_t nblocks, int32_t* __restrict__ state, uint32_t* __restrict__ nsym)
 {
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
@@ -91,6 +103,9 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
             state[(size_t) (s0 + k) * 256 + c] = run;
             run                                   = max(run, v);
         }
+        const int n = __syncthreads_count(run >= 0);  // distinct symbols of the block
+        if (threadIdx.x == 0)
+            nsym[b] = (uint32_t) n;
     }
 }
 
@@ -98,7 +113,15 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
 // 4w..4w+3, little-endian); the 4-dword pad makes 16-byte reads of 16 consecutive lanes hit
 // disjoint banks.  (Decode keeps its own interleaved layout, tbl[w * TPB + t].)
 constexpr uint32_t TSTRIDE = 68;
+__device__ __forceinline__ uint32_t start_table_dword(const int32_t* __restrict__ st);
+
 __device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st, uint32_t* tbl, uint32_t owner)
+{
+    tbl[owner * TSTRIDE + lane_id()] = start_table_dword(st);
+}
+
+// Lane l's dword of a segment's start table (entries 4l .. 4l+3, little-endian).
+__device__ __forceinline__ uint32_t start_table_dword(const int32_t* __restrict__ st)
 {
     // K(c) = last-occurrence time + 256 for seen symbols, 255 - c for unseen: the table is the
     // symbols by decreasing K.  Sort ascending by (2^40 - K) << 8 | c.
@@ -116,7 +139,7 @@ __device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st,
         v[r]             = c;
     }
     wave_bitonic_sort4(k, v, 256);
-    tbl[owner * TSTRIDE + lane] = (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
+    return (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
 }
 
 // Shift one table dword up by one entry: entry 0 becomes the top entry of the previous dword.
@@ -257,8 +280,9 @@ __device__ __forceinline__ void mtf_encode_segment(const uint8_t* __restrict__ i
         dst[i] = (uint8_t) mtf_step(R, tbl, src[i]);
 }
 
+// Segments of blocks with more than MTF_REG distinct symbols (the others go to k_mtf_encode_reg).
 __global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
-                                                    uint32_t nseg, const int32_t* __restrict__ state)
+                                                    uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];  // TSTRIDE * TPB dwords
     const uint32_t t    = threadIdx.x;
@@ -273,15 +297,235 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ 
             const uint32_t s     = g0 + owner;
             if (s >= nseg)
                 break;
-            if (segs[s].start == 0)
+            const Piece P = segs[s];
+            if (nsym[P.block] <= MTF_REG)
+                continue;
+            if (P.start == 0)
                 tbl[owner * TSTRIDE + lane] = (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u;
             else
                 build_table_wave(state + (size_t) s * 256, tbl, owner);
         }
         __syncthreads();
         const uint32_t s = g0 + t;
-        if (s < nseg)
+        if (s < nseg && nsym[segs[s].block] > MTF_REG)
             mtf_encode_segment(in, out, segs[s], tbl + t * TSTRIDE);
+        __syncthreads();
+    }
+}
+
+// ---- register tables: blocks of at most MTF_REG distinct symbols ----
+// Once a symbol has occurred it stays among the first (distinct symbols) positions of the table, so
+// with <= 32 distinct symbols per block the first 32 entries (8 dwords in registers) hold every
+// symbol that can be found by a search; entries beyond are byte values not yet seen in the block,
+// in increasing value order (true of the identity start table and kept by every move-to-front,
+// since the entry pushed out of the register part is then always an unseen value smaller than every
+// unseen value behind it).  A symbol not in registers therefore has rank
+// MTF_REG + #(unseen values below it) = MTF_REG + c - #(register entries below c).  No LDS table:
+// occupancy is bounded by registers, not by a 272-byte LDS row per thread.
+constexpr int NRD = MTF_REG / 4;  // register dwords
+
+__device__ __noinline__ uint32_t count_below(const uint32_t (&R)[NRD], uint32_t c)
+{
+    uint32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < NRD; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            n += ((R[k] >> (8 * j)) & 0xFFu) < c ? 1u : 0u;
+    return n;
+}
+
+__device__ __forceinline__ uint32_t mtf_step_reg(uint32_t (&R)[NRD], uint32_t c)
+{
+    const uint32_t cc = c * 0x01010101u;
+    uint32_t       z[NRD];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        z[k] = haszero8(R[k] ^ cc);
+    const bool near = (z[0] | z[1] | z[2] | z[3]) != 0;
+    if (__builtin_amdgcn_ballot_w64(!near) == 0)
+    {
+        // every lane finds its symbol among the first 16 entries: shift only those
+        const uint32_t k = z[0] ? 0 : z[1] ? 1 : z[2] ? 2 : 3;
+        const uint32_t zz = z[0] ? z[0] : z[1] ? z[1] : z[2] ? z[2] : z[3];
+        const uint32_t b = (uint32_t) __builtin_ctz(zz) >> 3;
+        uint32_t       top = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            const uint32_t cur = R[q], ntop = cur >> 24;
+            if ((uint32_t) q < k)
+                R[q] = shift1(cur, top);
+            else if ((uint32_t) q == k)
+                R[q] = shift_upto(cur, top, b);
+            top = ntop;
+        }
+        return k * 4 + b;
+    }
+#pragma unroll
+    for (int k = 4; k < NRD; ++k)
+        z[k] = haszero8(R[k] ^ cc);
+    uint32_t k = NRD, zz = 0;
+#pragma unroll
+    for (int q = NRD - 1; q >= 0; --q)
+        if (z[q])
+        {
+            k  = (uint32_t) q;
+            zz = z[q];
+        }
+    uint32_t rank;
+    uint32_t b = 3;
+    if (k < (uint32_t) NRD)
+    {
+        b    = (uint32_t) __builtin_ctz(zz) >> 3;
+        rank = k * 4 + b;
+    }
+    else
+        rank = MTF_REG + c - count_below(R, c);  // first occurrence: an unseen value from behind the registers
+    uint32_t top = c;
+#pragma unroll
+    for (int q = 0; q < NRD; ++q)
+    {
+        const uint32_t cur = R[q], ntop = cur >> 24;
+        if ((uint32_t) q < k)
+            R[q] = shift1(cur, top);
+        else if ((uint32_t) q == k)
+            R[q] = shift_upto(cur, top, b);
+        top = ntop;
+    }
+    return rank;
+}
+
+// The first MTF_REG entries of a segment's start table for a block of <= MTF_REG distinct symbols,
+// built by one wave: the seen symbols (last occurrence >= 0, at most MTF_REG of them) ordered by
+// decreasing last occurrence -- each one's position is the number of seen symbols seen later --
+// then the smallest unseen byte values in increasing order.  Lane l < NRD returns dword l (entries
+// 4l .. 4l+3).  Replaces a 256-key bitonic sort per segment.
+__device__ __forceinline__ uint32_t start_front_small(const int32_t* __restrict__ st, uint32_t* sc_t, uint32_t* sc_c, uint8_t* sc_out)
+{
+    const int      lane = lane_id();
+    const int4     tv   = reinterpret_cast<const int4*>(st)[lane];
+    const int32_t  tt[4] = {tv.x, tv.y, tv.z, tv.w};
+    uint32_t       nseen = 0, seen_before = 0, unseen_before = 0;
+    uint64_t       bal[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        bal[r] = __builtin_amdgcn_ballot_w64(tt[r] >= 0);
+        nseen += (uint32_t) __popcll(bal[r]);
+    }
+    // value c = 4 lane + r: seen values below it (lanes below, then r' < r in this lane)
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        seen_before += (uint32_t) __popcll(bal[r] & below);
+    uint32_t own_seen = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = (uint32_t) lane * 4 + r;
+        if (tt[r] >= 0)
+        {
+            const uint32_t i = seen_before + own_seen;  // index among seen values (value order)
+            sc_t[i]          = (uint32_t) tt[r];
+            sc_c[i]          = c;
+            ++own_seen;
+        }
+        else
+        {
+            unseen_before = c - (seen_before + own_seen);  // unseen values below c
+            const uint32_t pos = nseen + unseen_before;
+            if (pos < MTF_REG)
+                sc_out[pos] = (uint8_t) c;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if ((uint32_t) lane < nseen)
+    {
+        const uint32_t my = sc_t[lane];
+        uint32_t       p  = 0;
+        for (uint32_t j = 0; j < nseen; ++j)
+            p += sc_t[j] > my ? 1u : 0u;
+        sc_out[p] = (uint8_t) sc_c[lane];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t d = (lane < NRD) ? reinterpret_cast<const uint32_t*>(sc_out)[lane] : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return d;
+}
+
+__global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
+                                                        uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym)
+{
+    __shared__ uint32_t front[NRD][TPB];  // start-table fronts of the workgroup's segments (thread-major: conflict-free)
+    __shared__ uint32_t sc_t[TPB / 64][MTF_REG], sc_c[TPB / 64][MTF_REG];
+    __shared__ __attribute__((aligned(4))) uint8_t sc_out[TPB / 64][MTF_REG];
+    const uint32_t t    = threadIdx.x;
+    const int      lane = lane_id();
+    const uint32_t wave = t >> 6;
+    for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
+    {
+        for (int q = 0; q < 64; ++q)
+        {
+            const uint32_t owner = wave * 64 + q;
+            const uint32_t s     = g0 + owner;
+            if (s >= nseg)
+                break;
+            const Piece P = segs[s];
+            if (nsym[P.block] > MTF_REG)
+                continue;
+            const uint32_t d = (P.start == 0) ? (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u
+                                              : start_front_small(state + (size_t) s * 256, sc_t[wave], sc_c[wave], sc_out[wave]);
+            if (lane < NRD)
+                front[lane][owner] = d;
+        }
+        __syncthreads();
+        const uint32_t s = g0 + t;
+        if (s < nseg && nsym[segs[s].block] <= MTF_REG)
+        {
+            const Piece    P   = segs[s];
+            const uint8_t* src = in + P.off;
+            uint8_t*       dst = out + P.off;
+            uint32_t       R[NRD];
+#pragma unroll
+            for (int k = 0; k < NRD; ++k)
+                R[k] = front[k][t];
+            uint32_t i = 0;
+            if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0 && P.len >= 16)
+            {
+                const uint32_t nv  = P.len / 16;
+                uint4          nxt = reinterpret_cast<const uint4*>(src)[0];
+                for (uint32_t v = 0; v < nv; ++v)
+                {
+                    const uint4 cur = nxt;
+                    if (v + 1 < nv)
+                        nxt = reinterpret_cast<const uint4*>(src)[v + 1];
+                    // 16 symbols shifted out of a 128-bit register pair, ranks shifted in (a rolled
+                    // loop: 16 inlined steps cost 2x the registers for nothing, the steps are serial)
+                    uint64_t ilo = ((uint64_t) cur.y << 32) | cur.x, ihi = ((uint64_t) cur.w << 32) | cur.z;
+                    uint64_t olo = 0, ohi = 0;
+#pragma unroll 1
+                    for (int j = 0; j < 16; ++j)
+                    {
+                        const uint32_t r = mtf_step_reg(R, (uint32_t) ilo & 0xFFu);
+                        ilo              = (ilo >> 8) | (ihi << 56);
+                        ihi >>= 8;
+                        olo = (olo >> 8) | (ohi << 56);
+                        ohi = (ohi >> 8) | ((uint64_t) r << 56);
+                    }
+                    reinterpret_cast<uint4*>(dst)[v] = make_uint4((uint32_t) olo, (uint32_t) (olo >> 32), (uint32_t) ohi, (uint32_t) (ohi >> 32));
+                }
+                i = nv * 16;
+            }
+            for (; i < P.len; ++i)
+                dst[i] = (uint8_t) mtf_step_reg(R, src[i]);
+        }
         __syncthreads();
     }
 }
@@ -381,10 +625,10 @@ __global__ void __launch_bounds__(TPB) k_mtf_dec_relabel(const uint8_t* __restri
 
 bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s)
 {
-    if (!w.tiling.build(h_blocks, nblocks, MTF_SEG, s))
+    if (!w.tiling.build(h_blocks, nblocks, MTF_SEG_ENC, s))
         return false;
     const uint32_t nseg = w.tiling.n;
-    if (!w.reserve((size_t) nseg * 256 * 4))
+    if (!w.reserve((size_t) nseg * 256 * 4) || !w.reserve_blocks(nblocks))
         return false;
     int32_t* st = reinterpret_cast<int32_t*>(w.state);
     {
@@ -394,7 +638,7 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     {
         BRA_PROF(P_MTF_SCAN, s);
         hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
-                           nblocks, st);
+                           nblocks, st, w.nsym);
     }
     const size_t lds = (size_t) TSTRIDE * TPB * 4;
     static bool  attr = false;
@@ -405,8 +649,11 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     }
     {
         BRA_PROF(P_MTF_ENCODE, s);
+        // every segment goes to exactly one of the two kernels (by its block's distinct symbols)
+        hipLaunchKernelGGL(k_mtf_encode_reg, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), 0, s, d_in, d_out,
+                           w.tiling.d_pieces, nseg, st, w.nsym);
         hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
-                           w.tiling.d_pieces, nseg, st);
+                           w.tiling.d_pieces, nseg, st, w.nsym);
     }
     uint64_t N = 0;
     for (uint32_t b = 0; b < nblocks; ++b)
