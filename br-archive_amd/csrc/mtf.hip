@@ -530,6 +530,193 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restric
     }
 }
 
+// ---- wave-cooperative MTF: blocks of more than MTF_REG distinct symbols ----
+// One wave codes one segment (staged in LDS, ranks written back in place), 64 symbols at a time,
+// one per lane, from the table at the start of the 64-symbol chunk: list[p] = symbol at position p
+// and pos[c] = position of symbol c (256-byte LDS rows per wave).  The table lists symbols by
+// decreasing last-occurrence time, so the rank of lane i's symbol s is the number of symbols whose
+// last occurrence before i is later than s's:
+//   * s occurred earlier in the chunk, last at lane j ("repeat"): the distinct symbols of lanes
+//     (j, i) = #{k in (j, i): nxt_k >= i} (nxt_k = next lane holding s_k, 64 if none);
+//   * otherwise ("first"): pos[s] plus the chunk's distinct symbols before i that stood behind s,
+//     pos[s] + #{k in F, k < i} - #{k in F, k < i: pos_k < pos[s]} over the first lanes F.
+// The first count is bit-sliced: one ballot per key bit and a few 64-bit mask operations per lane
+// (v_bitop3 on gfx950).  Repeats are few in high-entropy data (about 7 of 64 in uniform random
+// bytes), so they are counted one at a time with a ballot each unless there are many.  Then the
+// table moves: the chunk's distinct symbols take the front by decreasing last occurrence and the
+// other entries keep their order behind them (a wave compaction of the list).  The cost does not
+// depend on the ranks (uniform random data: ranks average 127.5).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// bit b of x as an all-zeros / all-ones word (v_bfe_i32)
+__device__ __forceinline__ uint32_t bitmask(uint32_t x, int b) { return (uint32_t) (((int32_t) (x << (31 - b))) >> 31); }
+
+// #{k in dom : key_k < q} for this lane's query q (keys and queries of NB bits): walk the bits from
+// the top keeping E = the lanes of dom whose key agrees with q on the bits above; the lanes that
+// first differ at bit b with key bit 0 < query bit 1 are below q.  (32-bit halves, so that each
+// update is one v_bitop3 with the ballot as its scalar operand.)
+template <int NB>
+__device__ __forceinline__ uint32_t count_less(uint32_t key, uint32_t q, uint64_t dom)
+{
+    uint32_t el = (uint32_t) dom, eh = (uint32_t) (dom >> 32), ll = 0, lh = 0;
+#pragma unroll
+    for (int b = NB - 1; b >= 0; --b)
+    {
+        const uint64_t B  = ballot64(bitmask(key, b) != 0);
+        const uint32_t bl = (uint32_t) B, bh = (uint32_t) (B >> 32);
+        const uint32_t mq = bitmask(q, b);
+        ll |= el & ~bl & mq;
+        lh |= eh & ~bh & mq;
+        el &= ~(bl ^ mq);
+        eh &= ~(bh ^ mq);
+    }
+    return (uint32_t) __popc(ll) + (uint32_t) __popc(lh);
+}
+
+static_assert(MTF_SEG_ENC == 1024, "k_mtf_encode_wave stages a segment as 64 lanes x 16 bytes");
+
+__global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
+                                                         uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym)
+{
+    __shared__ uint32_t pos_s[TPB / 64][64];   // byte c of a wave's row: table position of symbol c
+    __shared__ uint32_t list_s[TPB / 64][64];  // byte p: symbol at table position p
+    __shared__ uint32_t mark_s[TPB / 64][64];  // byte p != 0: position p holds a symbol of the chunk
+    __shared__ uint4    buf_s[TPB / 64][64];   // the segment: symbols, overwritten by their ranks
+    const int      lane  = lane_id();
+    const uint32_t wave  = threadIdx.x >> 6;
+    uint8_t*       pos   = reinterpret_cast<uint8_t*>(pos_s[wave]);
+    uint8_t*       list  = reinterpret_cast<uint8_t*>(list_s[wave]);
+    uint8_t*       mark  = reinterpret_cast<uint8_t*>(mark_s[wave]);
+    uint8_t*       buf   = reinterpret_cast<uint8_t*>(buf_s[wave]);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t above = ~below << 1;
+    mark_s[wave][lane]   = 0;
+    for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
+    {
+        const Piece P = segs[s];
+        if (nsym[P.block] <= MTF_REG)
+            continue;
+        const bool full = P.len == MTF_SEG_ENC && ((P.off & 15) == 0);
+        if (full)
+            buf_s[wave][lane] = reinterpret_cast<const uint4*>(in + P.off)[lane];
+        else
+            for (uint32_t i = lane; i < P.len; i += 64)
+                buf[i] = in[P.off + i];
+        {
+            const uint32_t d = (P.start == 0) ? (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u
+                                              : start_table_dword(state + (size_t) s * 256);  // symbols at positions 4 lane + r
+            list_s[wave][lane] = d;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                pos[(d >> (8 * r)) & 0xFF] = (uint8_t) (lane * 4 + r);
+        }
+        wave_lds_sync();
+        for (uint32_t c0 = 0; c0 < P.len; c0 += 64)
+        {
+            const uint32_t nv    = min(64u, P.len - c0);
+            const bool     valid = (uint32_t) lane < nv;
+            const uint32_t sym   = valid ? buf[c0 + lane] : 0u;
+            const uint64_t V     = ballot64(valid);
+            uint32_t       el = (uint32_t) V, eh = (uint32_t) (V >> 32);  // lanes holding the same symbol
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+            {
+                const uint32_t m = bitmask(sym, b);
+                const uint64_t B = ballot64(m != 0);
+                el &= ~((uint32_t) B ^ m);
+                eh &= ~((uint32_t) (B >> 32) ^ m);
+            }
+            const uint64_t eq  = ((uint64_t) eh << 32) | el;
+            const uint64_t pm  = eq & below, nm = eq & above;
+            const int      j   = pm ? 63 - __builtin_clzll(pm) : -1;
+            const uint32_t nxt = nm ? (uint32_t) __builtin_ctzll(nm) : 64u;
+            const uint32_t p0  = pos[sym];
+            const bool     rep = j >= 0;
+            const uint64_t Fm  = V & ~ballot64(rep);  // first occurrences
+            const uint64_t Am  = V & ~Fm;             // repeats
+            uint32_t       rank = 0;
+            if (Fm)
+            {
+                const uint64_t fb = Fm & below;
+                rank              = p0 + (uint32_t) __popcll(fb) - count_less<8>(p0, p0, fb);
+            }
+            if (__popcll(Am) > 16)
+            {
+                // many repeats: #{k in (j, i): nxt_k < i}, nxt in [1, 64] -> 7 bits
+                const uint64_t in_ji = below & (rep ? ~((2ull << j) - 1ull) : 0ull);
+                const uint32_t ra    = (uint32_t) (lane - j - 1) - count_less<7>(nxt, (uint32_t) lane, in_ji);
+                if (rep)
+                    rank = ra;
+            }
+            else
+            {
+                uint64_t A = Am;
+                while (A)
+                {
+                    const int i = __builtin_ctzll(A);
+                    A &= A - 1;
+                    const int      ji = __builtin_amdgcn_readlane(j, i);
+                    const uint64_t G  = ballot64(nxt >= (uint32_t) i) & ((1ull << i) - 1ull) & ~((2ull << ji) - 1ull);
+                    rank              = lane == i ? (uint32_t) __popcll(G) : rank;
+                }
+            }
+            if (valid)
+                buf[c0 + lane] = (uint8_t) rank;
+            // move the chunk's symbols to the front: they take positions 0 .. Dc-1 by decreasing last
+            // occurrence, the other entries keep their order behind them
+            const bool     last = valid && nxt == 64u;
+            const uint64_t Lm   = ballot64(last);
+            const uint32_t Dc   = (uint32_t) __popcll(Lm);
+            if (last)
+                mark[p0] = 1;
+            wave_lds_sync();
+            const uint32_t mw = mark_s[wave][lane];  // positions 4 lane .. 4 lane + 3
+            const uint32_t lw = list_s[wave][lane];
+            uint32_t       kept[4], nk = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                kept[r] = ((mw >> (8 * r)) & 0xFF) ? 0u : 1u;
+                nk += kept[r];
+            }
+            uint32_t ex;
+            (void) wave_scan<true>(nk, 0u, OpAdd(), &ex);
+            wave_lds_sync();
+            mark_s[wave][lane] = 0;
+            uint32_t o = Dc + ex;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (kept[r])
+                {
+                    const uint32_t c = (lw >> (8 * r)) & 0xFF;
+                    list[o]          = (uint8_t) c;
+                    pos[c]           = (uint8_t) o;
+                    ++o;
+                }
+            if (last)
+            {
+                const uint32_t np = (uint32_t) __popcll(Lm & above);
+                list[np]          = (uint8_t) sym;
+                pos[sym]          = (uint8_t) np;
+            }
+            wave_lds_sync();
+        }
+        if (full)
+            reinterpret_cast<uint4*>(out + P.off)[lane] = buf_s[wave][lane];
+        else
+            for (uint32_t i = lane; i < P.len; i += 64)
+                out[P.off + i] = buf[i];
+        wave_lds_sync();
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
@@ -652,8 +839,16 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
         // every segment goes to exactly one of the two kernels (by its block's distinct symbols)
         hipLaunchKernelGGL(k_mtf_encode_reg, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), 0, s, d_in, d_out,
                            w.tiling.d_pieces, nseg, st, w.nsym);
-        hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
-                           w.tiling.d_pieces, nseg, st, w.nsym);
+        static const int wave_kernel = [] {
+            const char* e = getenv("BRA_MTF_WAVE");  // 0: per-thread table walks for blocks of > MTF_REG symbols
+            return e ? atoi(e) : 1;
+        }();
+        if (wave_kernel)
+            hipLaunchKernelGGL(k_mtf_encode_wave, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, d_out,
+                               w.tiling.d_pieces, nseg, st, w.nsym);
+        else
+            hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
+                               w.tiling.d_pieces, nseg, st, w.nsym);
     }
     uint64_t N = 0;
     for (uint32_t b = 0; b < nblocks; ++b)

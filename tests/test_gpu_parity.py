@@ -182,6 +182,29 @@ def test_batch_periodic_and_runs(bra, codec, orc):
     _encode_check(bra, codec, orc, data, 4096)
 
 
+def _dup_blocks(rng, bs: int, x: int, text: np.ndarray) -> np.ndarray:
+    """Blocks of size bs shaped X||X||R, X||Y||X||R, X||X (period bs/2) and text X||Y||X, with X
+    random (or text) of x bytes: long duplicated regions leave one tied group per byte once the
+    jobs reach their depth cap, so these stress the fallback group list."""
+    X = rng.integers(0, 256, x, dtype=np.uint8)
+    Y = rng.integers(0, 256, x // 2, dtype=np.uint8)
+    T = text[:x]
+    blocks = [
+        np.concatenate([X, X, rng.integers(0, 256, bs - 2 * x, dtype=np.uint8)]),
+        np.concatenate([X, Y, X, rng.integers(0, 256, bs - 2 * x - Y.size, dtype=np.uint8)]),
+        np.concatenate([rng.integers(0, 256, bs // 2, dtype=np.uint8)] * 2),
+        np.concatenate([T, Y, T, text[x: x + bs - 2 * x - Y.size]]),
+    ]
+    return np.concatenate(blocks)
+
+
+@pytest.mark.parametrize("bs,x", [(65536, 8192), (1 << 20, 128 << 10)])
+def test_batch_duplicated_regions(bra, codec, orc, bs, x):
+    rng = np.random.default_rng(bs + x)
+    text = bra.synth_fill(0, bs, bs, first_block=5)
+    _encode_check(bra, codec, orc, _dup_blocks(rng, bs, x, text), bs)
+
+
 def test_config1_tiled_block(bra, codec, golden):
     import torch
 
