@@ -196,8 +196,6 @@ struct bra_gpu_ctx_s
     uint64_t*      d_aux = nullptr;  // block offsets for decode, record bases
     HuffMetaRec*   d_meta = nullptr;
     uint64_t       cap_b = 0, cap_pi = 0, cap_rs = 0, cap_hist = 0, cap_st = 0, cap_rb = 0, cap_rc = 0, cap_aux = 0, cap_meta = 0;
-    uint64_t       cap_recs = 0;
-    uint64_t*      d_recs = nullptr;
     // single-call staging
     uint8_t*       d_io = nullptr;
     uint64_t       cap_io = 0;
@@ -242,7 +240,7 @@ static void ctx_free(bra_gpu_ctx_s* c)
     c->ib.release();
     c->hist_tiling.release();
     void* ptrs[] = {c->d_L,       c->d_mtf,   c->d_rle,  c->d_tmp,  c->d_blocks, c->d_pi,  c->d_rle_size, c->d_hist, c->d_status, c->d_rle_base,
-                    c->d_rle_cap, c->d_aux,   c->d_meta, c->d_recs, c->d_io,     c->d_off, c->d_pay,      c->d_hdr,
+                    c->d_rle_cap, c->d_aux,   c->d_meta, c->d_io,     c->d_off, c->d_pay,      c->d_hdr,
                     c->d_word,    c->d_enc_blocks, c->d_enc_rle_base, c->d_hin, c->d_hout};
     for (void* p : ptrs)
         (void) hipFree(p);
@@ -372,9 +370,9 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
         hipStreamSynchronize(s) != hipSuccess)
         return -1;
     // RLE streams back to back; record arrays; MTF input at the block offsets
-    std::vector<uint64_t> rbase(nb), rcap(nb), recb(nb), outb(nb), outcap(nb);
+    std::vector<uint64_t> rbase(nb), outb(nb), outcap(nb);
     std::vector<uint32_t> rsz(nb);
-    uint64_t R = 0, RC = 0;
+    uint64_t R = 0;
     for (uint32_t b = 0; b < nb; ++b)
     {
         const uint32_t os = hh[b].huffman.orig_size;
@@ -385,23 +383,19 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
         }
         rbase[b]  = R;
         rsz[b]    = os;
-        recb[b]   = RC;
         outb[b]   = hb[b].off;
         outcap[b] = hb[b].len;
         R += (uint64_t) os + 16;
-        RC += os / 2 + 2;
     }
-    if (!grow(c->d_rle, c->cap_rle, R + 16) || !grow(c->d_recs, c->cap_recs, RC + 16) || !grow(c->d_L, c->cap_L, N + 16) ||
+    if (!grow(c->d_rle, c->cap_rle, R + 16) || !grow(c->d_L, c->cap_L, N + 16) ||
         !grow(c->d_mtf, c->cap_mtf, N + 16) || !grow(c->d_tmp, c->cap_tmp, N + 16))
         return -1;
     uint64_t* d_rbase  = c->d_rle_base;
     uint64_t* d_outcap = c->d_rle_cap;
-    uint64_t* d_recb   = c->d_aux;
     uint64_t* d_outb   = c->d_aux + nb + 1;
     if (hipMemcpyAsync(c->d_blocks, hb.data(), nb * sizeof(BlockDesc), hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d_rbase, rbase.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d_outcap, outcap.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(d_recb, recb.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d_outb, outb.data(), nb * 8, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(c->d_rle_size, rsz.data(), nb * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return -1;
@@ -412,8 +406,7 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
     if (!huff_decode_device(c->huf, c->d_meta, esz.data(), nb, d_payload, d_payload_off, c->d_rle, d_rbase, c->d_status, s))
         return -1;
     uint32_t* d_dec_size = c->d_hist;           // nb words
-    uint32_t* d_nrec     = c->d_hist + nb;      // nb words
-    if (!rle_decode_device(c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, c->d_recs, d_recb, d_nrec, s))
+    if (!rle_decode_device(c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, s))
         return -1;
     std::vector<uint32_t> st(nb), dsz(nb);
     if (hipMemcpyAsync(st.data(), c->d_status, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1062,7 +1055,7 @@ void bra_bwt_decode2(const uint8_t* buf, const bra_bwt_index_t buf_size, const b
     if (hipMemcpyAsync(c->d_blocks, hb.data(), sizeof(BlockDesc), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemcpyAsync(c->d_pi, &primary_index, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return;
-    if (!ibwt_device(c->ib, c->d_io, c->d_pi, c->d_blocks, hb.data(), 1, c->d_L, c->stream))
+    if (!ibwt_device(c->ib, c->d_io, c->d_pi, c->d_blocks, hb.data(), 1, c->d_L, c->stream, transform != nullptr))
         return;
     if (transform)
         (void) download(c, transform, c->ib.T, (uint64_t) buf_size * 4);  // the LF transform, as the reference leaves it
@@ -1176,7 +1169,7 @@ static bool rle_decode_one(bra_gpu_ctx_s* c, const uint8_t* buf, size_t buf_size
     if (!upload(c, buf, buf_size) || !ensure_block_arrays(c, 1))
         return false;
     const uint64_t out_cap = expand ? (uint64_t) buf_size * 64 + 64 : 0;  // a 2-byte run block expands to <= 128 bytes
-    if (!grow(c->d_tmp, c->cap_tmp, std::max<uint64_t>(out_cap, 16)) || !grow(c->d_recs, c->cap_recs, buf_size / 2 + 16))
+    if (!grow(c->d_tmp, c->cap_tmp, std::max<uint64_t>(out_cap, 16)))
         return false;
     const uint64_t zero = 0, cap = out_cap;
     const uint32_t sz   = (uint32_t) buf_size;
@@ -1185,8 +1178,7 @@ static bool rle_decode_one(bra_gpu_ctx_s* c, const uint8_t* buf, size_t buf_size
         hipMemcpyAsync(c->d_aux, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemcpyAsync(c->d_rle_size, &sz, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return false;
-    if (!rle_decode_device(c->d_io, c->d_rle_base, c->d_rle_size, 1, c->d_tmp, c->d_aux, c->d_rle_cap, c->d_status, c->d_recs, c->d_aux,
-                           c->d_pi, c->stream))
+    if (!rle_decode_device(c->d_io, c->d_rle_base, c->d_rle_size, 1, c->d_tmp, c->d_aux, c->d_rle_cap, c->d_status, c->stream))
         return false;
     return download(c, dec_size, c->d_status, 4);
 }

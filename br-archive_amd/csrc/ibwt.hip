@@ -4,12 +4,25 @@
 // position of the k-th c in L (a stable partition of positions by byte, :141-159), then n steps
 // `index = transform[index]; out[i] = L[index]` starting at the primary index (:161-167).
 //
-// The pointer chase is split with splitters: every SPL-th transform index plus the primary index.
-// Each splitter's thread walks to the next splitter (pass 1, recording the hop and its length),
-// one lane per block chains the hops from the primary index in LDS to get output offsets, and the
-// walkers re-walk writing their output (pass 3).  A primary index on a cycle shorter than n (a
-// periodic block) makes the output periodic with that cycle length, exactly like the reference.
+// The pointer chase is split with splitters: every S-th transform index plus the primary index.
+// Main path (blocks < 2^24 bytes):
+//   k_ib_hist / k_ib_scan / k_ib_scatter2  TL[k] = transform[k] | L[transform[k]] << 24, so one
+//        4-byte load per step gives both the next index and the output byte;
+//   k_ib_walk3   persistent waves claim splitters from per-XCD queues (each XCD works through its
+//        own range of blocks, so the random loads of an XCD stay in few blocks' TL); a lane walks
+//        from its splitter to the next one, staging the bytes 16 at a time into the splitter's slot
+//        (4 S bytes; longer hops continue in 256-byte chunks from a pool) and records the hop;
+//        lanes that finish claim the next splitter at once, so no lane idles on a long hop;
+//   k_ib_chain3  one workgroup per block ranks the splitter list from the primary splitter by
+//        pointer jumping in LDS -> output offset of every hop (and the primary cycle's length);
+//   k_ib_copy3   one wave per hop copies its staged bytes to their output offset.
+// A primary index on a cycle shorter than n (a periodic block) makes the output periodic with that
+// cycle length, exactly like the reference (k_ib_repeat).  The round-1 two-walk kernels remain for
+// blocks of >= 2^24 bytes, for callers that want the transform itself, and as the fallback when
+// the overflow pool runs out.
 #include "ibwt.h"
+
+#include <cstring>
 
 namespace bra {
 
@@ -18,6 +31,19 @@ namespace {
 constexpr int      TPB        = 256;
 constexpr uint32_t MAX_SPLIT  = 4096;  // splitters per block (+1 for the primary index)
 constexpr uint32_t ITILE      = 4096;
+
+// main-path block record: splitter step S = 2^shift, ns regular splitters (0, S, 2S, ...) plus the
+// primary index; the block's splitter slots (4 S bytes each) start at tslot in the slot buffer
+struct IbBlk
+{
+    uint64_t off;
+    uint64_t tslot;
+    uint32_t len;
+    uint32_t shift;
+    uint32_t ns;
+    uint32_t pad;
+};
+static_assert(sizeof(IbBlk) == 32, "IbBlk is stored in a uint64_t[4] per block");
 
 __device__ __forceinline__ uint32_t split_step(uint32_t n)
 {
@@ -247,6 +273,349 @@ __global__ void k_ib_repeat(const BlockDesc* __restrict__ blocks, uint32_t nbloc
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// main path
+// ------------------------------------------------------------------------------------------------
+// stable scatter of (index | byte << 24): as k_ib_scatter, packed
+__global__ void __launch_bounds__(64) k_ib_scatter2(const uint8_t* __restrict__ L, const Piece* __restrict__ tiles, uint32_t ntiles,
+                                                    const uint32_t* __restrict__ th, const BlockDesc* __restrict__ blocks,
+                                                    uint32_t* __restrict__ TL)
+{
+    __shared__ uint32_t cnt[256];
+    const int           lane = lane_id();
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        const Piece P = tiles[t];
+        for (int i = lane; i < 256; i += 64)
+            cnt[i] = th[(size_t) t * 256 + i];
+        __syncthreads();
+        const uint64_t boff = blocks[P.block].off;
+        for (uint32_t base = 0; base < P.len; base += 64)
+        {
+            const uint32_t i     = base + lane;
+            const bool     valid = i < P.len;
+            const uint32_t c     = valid ? L[P.off + i] : 0xFFFFFFFFu;
+            uint64_t       m     = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit)
+            {
+                const uint64_t bb = __ballot(valid && ((c >> bit) & 1));
+                m &= ((c >> bit) & 1) ? bb : ~bb;
+            }
+            const uint64_t lt   = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+            const uint32_t rank = (uint32_t) __popcll(m & lt);
+            const uint32_t tot  = (uint32_t) __popcll(m);
+            uint32_t       dst  = 0;
+            if (valid)
+                dst = cnt[c] + rank;
+            __syncthreads();
+            if (valid)
+            {
+                TL[boff + dst] = (P.start + i) | (c << 24);
+                if (rank == tot - 1)
+                    cnt[c] += tot;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Hardware id (0-7) of the XCD the calling wave runs on (placement only: correctness never
+// depends on it, every wave drains all eight queues).
+__device__ __forceinline__ uint32_t xcd_id()
+{
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x & 7u;
+}
+
+struct WalkArgs
+{
+    const IbBlk*    blk;
+    const uint32_t* pi;
+    const uint32_t* cum;   // cum[b] = global id of block b's splitter 0 (cum[nblocks] = total)
+    const uint32_t* xr;    // XCD x serves blocks [xr[x], xr[x+1])
+    uint32_t*       qc;    // claim counters, one per XCD (32-word stride)
+    const uint32_t* TL;
+    uint8_t*        slot;  // splitter slots
+    uint8_t*        pool;  // overflow chunks of IB_CHUNK bytes
+    uint32_t*       pool_ctr;
+    uint32_t        pool_cap;
+    uint32_t*       ovl_next;  // chunk -> next chunk of the same hop
+    uint32_t*       hop_next;  // per splitter: block-local id of the next splitter
+    uint32_t*       hop_len;
+    uint32_t*       hop_ovf;   // first overflow chunk
+};
+
+constexpr uint32_t IB_CHUNK = 256;
+
+__device__ __forceinline__ uint8_t* walk_dst(const WalkArgs& a, uint8_t* slot, uint32_t cap, uint32_t o, uint32_t& chunk, uint32_t g)
+{
+    if (o < cap)
+        return slot + o;
+    const uint32_t r = o - cap;
+    if ((r & (IB_CHUNK - 1)) == 0)
+    {
+        const uint32_t c = atomicAdd(a.pool_ctr, 1u);
+        if (c >= a.pool_cap)
+        {
+            chunk = 0xFFFFFFFFu;
+            return nullptr;  // pool exhausted: the host falls back to the two-walk path
+        }
+        if (r == 0)
+            a.hop_ovf[g] = c;
+        else if (chunk != 0xFFFFFFFFu)
+            a.ovl_next[chunk] = c;
+        chunk = c;
+    }
+    return chunk == 0xFFFFFFFFu ? nullptr : a.pool + (size_t) chunk * IB_CHUNK + (r & (IB_CHUNK - 1));
+}
+
+__global__ void __launch_bounds__(256) k_ib_walk3(WalkArgs a)
+{
+    const int      lane = lane_id();
+    const uint32_t x0   = xcd_id();
+    uint32_t       t    = 0;  // queues tried: (x0 + t) & 7
+    bool           act  = false;
+    uint32_t       g = 0, k = 0, y = 0, j = 0, p = 0, mask = 0, shift = 0, ns = 0, cap = 0, chunk = 0xFFFFFFFFu;
+    uint64_t       boff = 0, lo = 0, hi = 0;
+    uint8_t*       slot = nullptr;
+    while (true)
+    {
+        const uint64_t idle = __builtin_amdgcn_ballot_w64(!act);
+        if (idle && t < 8)
+        {
+            const uint32_t n  = (uint32_t) __popcll(idle);
+            const uint32_t x  = (x0 + t) & 7u;
+            const uint32_t q0 = a.cum[a.xr[x]], q1 = a.cum[a.xr[x + 1]];
+            uint32_t       b0 = 0;
+            if (lane == 0)
+                b0 = atomicAdd(&a.qc[x * 32], n);
+            b0 = __builtin_amdgcn_readfirstlane(b0);
+            if (b0 + n >= q1 - q0)
+                ++t;
+            if (!act)
+            {
+                const uint32_t pos = q0 + b0 + (uint32_t) __popcll(idle & ((1ull << lane) - 1ull));
+                if (pos < q1)
+                {
+                    // block of splitter pos: last b in [xr[x], xr[x+1]) with cum[b] <= pos
+                    uint32_t l = a.xr[x], h = a.xr[x + 1] - 1;
+                    while (l < h)
+                    {
+                        const uint32_t mid = (l + h + 1) >> 1;
+                        if (a.cum[mid] <= pos)
+                            l = mid;
+                        else
+                            h = mid - 1;
+                    }
+                    const IbBlk B = a.blk[l];
+                    g             = pos;
+                    k             = pos - a.cum[l];
+                    p             = a.pi[l];
+                    shift         = B.shift;
+                    mask          = (1u << shift) - 1u;
+                    ns            = B.ns;
+                    cap           = 4u << shift;
+                    boff          = B.off;
+                    slot          = a.slot + B.tslot + (size_t) k * cap;
+                    chunk         = 0xFFFFFFFFu;
+                    j             = 0;
+                    lo = hi = 0;
+                    if (k < ns)
+                    {
+                        y   = k << shift;
+                        act = true;
+                    }
+                    else if (p & mask)
+                    {
+                        y   = p;
+                        act = true;
+                    }
+                    else
+                    {
+                        a.hop_len[g]  = 0;  // the primary index is a regular splitter: no extra hop
+                        a.hop_next[g] = 0xFFFFFFFFu;
+                    }
+                }
+            }
+        }
+        if (!__builtin_amdgcn_ballot_w64(act))
+        {
+            if (t >= 8)
+                break;
+            continue;
+        }
+        if (act)
+        {
+#pragma unroll 1
+            for (int st = 0; st < 32; ++st)
+            {
+                const uint32_t v = a.TL[boff + y];
+                y                = v & 0xFFFFFFu;
+                lo               = (lo >> 8) | (hi << 56);
+                hi               = (hi >> 8) | ((uint64_t) (v >> 24) << 56);
+                ++j;
+                const bool split = (y & mask) == 0 || y == p;
+                if ((j & 15) == 0 || split)
+                {
+                    const uint32_t nb = ((j - 1) & 15) + 1;  // staged bytes (the top nb of the register)
+                    if (nb < 16)
+                    {
+                        const uint32_t sh = (16 - nb) * 8;  // move them to the bottom
+                        if (sh >= 64)
+                        {
+                            lo = hi >> (sh - 64);
+                            hi = 0;
+                        }
+                        else
+                        {
+                            lo = (lo >> sh) | (hi << (64 - sh));
+                            hi >>= sh;
+                        }
+                    }
+                    uint8_t* d = walk_dst(a, slot, cap, (j - 1) & ~15u, chunk, g);
+                    if (d)
+                        *reinterpret_cast<uint4*>(d) = make_uint4((uint32_t) lo, (uint32_t) (lo >> 32), (uint32_t) hi, (uint32_t) (hi >> 32));
+                    lo = hi = 0;
+                }
+                if (split)
+                {
+                    a.hop_next[g] = (y == p && (p & mask)) ? ns : (y >> shift);
+                    a.hop_len[g]  = j;
+                    act           = false;
+                    break;
+                }
+            }
+        }
+    }
+}
+
+// One workgroup per block: rank the splitter list from the primary splitter (pointer jumping in
+// LDS over the hops), start offset of every hop on the primary cycle (0xFFFFFFFF elsewhere) and the
+// cycle's length.
+constexpr uint32_t IB_MAXS   = 16385;  // splitters per block (16384 regular + the primary index)
+constexpr uint32_t IB_CH_TPB = 1024;
+
+__global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ pi,
+                                                         const uint32_t* __restrict__ cum, uint32_t nblocks,
+                                                         const uint32_t* __restrict__ hop_next, const uint32_t* __restrict__ hop_len,
+                                                         uint32_t* __restrict__ start, uint32_t* __restrict__ cyc)
+{
+    __shared__ uint16_t nx[IB_MAXS];
+    __shared__ uint32_t R[IB_MAXS];
+    __shared__ uint32_t sh_tot;
+    constexpr uint16_t  END = 0xFFFF;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const IbBlk    B    = blk[b];
+        const uint32_t base = cum[b], nn = cum[b + 1] - base;
+        const uint32_t p = pi[b], mask = (1u << B.shift) - 1u;
+        const uint32_t s0 = (p & mask) ? B.ns : (p >> B.shift);
+        for (uint32_t q = threadIdx.x; q < nn; q += IB_CH_TPB)
+        {
+            const uint32_t h = hop_next[base + q];
+            nx[q]            = h == 0xFFFFFFFFu ? END : (uint16_t) h;
+            R[q]             = hop_len[base + q];
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < nn; q += IB_CH_TPB)
+            if (nx[q] == s0)
+                nx[q] = END;  // the cycle through s0 ends before s0
+        __syncthreads();
+        uint32_t rounds = 1;
+        while ((1u << rounds) < nn)
+            ++rounds;
+        for (uint32_t r = 0; r <= rounds; ++r)
+        {
+            uint32_t nn2[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB], rr[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB];
+#pragma unroll
+            for (uint32_t u = 0; u < (IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB; ++u)
+            {
+                const uint32_t q = threadIdx.x + u * IB_CH_TPB;
+                nn2[u]           = END;
+                rr[u]            = 0;
+                if (q < nn && nx[q] != END)
+                {
+                    nn2[u] = nx[nx[q]];
+                    rr[u]  = R[nx[q]];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t u = 0; u < (IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB; ++u)
+            {
+                const uint32_t q = threadIdx.x + u * IB_CH_TPB;
+                if (q < nn && nx[q] != END)
+                {
+                    nx[q] = (uint16_t) nn2[u];
+                    R[q] += rr[u];
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0)
+        {
+            sh_tot = R[s0];
+            cyc[b] = min(R[s0], B.len);
+        }
+        __syncthreads();
+        const uint32_t tot = sh_tot;
+        for (uint32_t q = threadIdx.x; q < nn; q += IB_CH_TPB)
+            start[base + q] = (nx[q] == END && hop_len[base + q] != 0) ? tot - R[q] : 0xFFFFFFFFu;
+        __syncthreads();
+    }
+}
+
+// One wave per hop: staged bytes -> out[start ...].
+__global__ void __launch_bounds__(256) k_ib_copy3(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ cum, uint32_t nblocks,
+                                                  const uint32_t* __restrict__ start, const uint32_t* __restrict__ hop_len,
+                                                  const uint32_t* __restrict__ hop_ovf, const uint32_t* __restrict__ ovl_next,
+                                                  const uint8_t* __restrict__ slots, const uint8_t* __restrict__ pool, uint32_t pool_cap,
+                                                  uint8_t* __restrict__ out)
+{
+    const int      lane  = lane_id();
+    const uint32_t wpg   = blockDim.x / 64;
+    for (uint32_t b = blockIdx.y; b < nblocks; b += gridDim.y)
+    {
+        const IbBlk    B    = blk[b];
+        const uint32_t base = cum[b], nn = cum[b + 1] - base, cap = 4u << B.shift;
+        uint8_t*       ob   = out + B.off;
+        for (uint32_t q = blockIdx.x * wpg + (threadIdx.x >> 6); q < nn; q += gridDim.x * wpg)
+        {
+            const uint32_t st = start[base + q];
+            if (st == 0xFFFFFFFFu)
+                continue;
+            const uint32_t len = hop_len[base + q];
+            const uint32_t n1  = min(len, cap);
+            const uint8_t* src = slots + B.tslot + (size_t) q * cap;
+            for (uint32_t o = lane * 4; o < n1; o += 256)
+            {
+                const uint32_t v = *reinterpret_cast<const uint32_t*>(src + o);
+#pragma unroll
+                for (uint32_t h = 0; h < 4; ++h)
+                    if (o + h < n1 && st + o + h < B.len)
+                        ob[st + o + h] = (uint8_t) (v >> (8 * h));
+            }
+            uint32_t c = len > cap ? hop_ovf[base + q] : 0xFFFFFFFFu;
+            for (uint32_t o0 = cap; o0 < len && c < pool_cap; o0 += IB_CHUNK)
+            {
+                const uint8_t* cs = pool + (size_t) c * IB_CHUNK;
+                const uint32_t o  = o0 + lane * 4;
+                if (o < len)
+                {
+                    const uint32_t v = *reinterpret_cast<const uint32_t*>(cs + lane * 4);
+#pragma unroll
+                    for (uint32_t h = 0; h < 4; ++h)
+                        if (o + h < len && st + o + h < B.len)
+                            ob[st + o + h] = (uint8_t) (v >> (8 * h));
+                }
+                c = ovl_next[c];
+            }
+        }
+    }
+}
+
 }  // namespace
 
 bool IbwtWorkspace::reserve(uint64_t n, uint32_t nblocks, uint32_t ntiles)
@@ -288,22 +657,17 @@ void IbwtWorkspace::release()
     (void) hipFree(hop_len);
     (void) hipFree(start);
     (void) hipFree(cyc);
+    for (void* p : {(void*) blk, (void*) cum, (void*) ctl, (void*) m_next, (void*) m_len, (void*) m_ovf, (void*) m_start, (void*) ovl_next,
+                    (void*) slot, (void*) pool})
+        (void) hipFree(p);
     *this = IbwtWorkspace{};
 }
 
-bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, const BlockDesc* d_blocks, const BlockDesc* h_blocks,
-                 uint32_t nblocks, uint8_t* d_out, hipStream_t s)
+// the round-1 path: two walks over the transform (T and L separate)
+static bool ibwt_two_walk(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, const BlockDesc* d_blocks, uint32_t nblocks,
+                          uint8_t* d_out, hipStream_t s)
 {
-    if (!w.tiling.build(h_blocks, nblocks, ITILE, s))
-        return false;
-    uint64_t N = 0;
-    for (uint32_t b = 0; b < nblocks; ++b)
-        N = std::max<uint64_t>(N, h_blocks[b].off + h_blocks[b].len);
     const uint32_t nt = w.tiling.n;
-    if (!w.reserve(N, nblocks, nt))
-        return false;
-    hipLaunchKernelGGL(k_ib_hist, dim3(std::min<uint32_t>(nt, 8192)), dim3(TPB), 0, s, d_L, w.tiling.d_pieces, nt, w.th);
-    hipLaunchKernelGGL(k_ib_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, w.th);
     hipLaunchKernelGGL(k_ib_scatter, dim3(std::min<uint32_t>(nt, 16384)), dim3(64), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks, w.T);
     const dim3 g(div_up(MAX_SPLIT + 1, 128), std::min<uint32_t>(nblocks, 65535));
     hipLaunchKernelGGL(k_ib_walk1, g, dim3(128), 0, s, d_blocks, nblocks, d_pi, w.T, w.hop_next, w.hop_len);
@@ -312,6 +676,117 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
     hipLaunchKernelGGL(k_ib_walk2, g, dim3(128), 0, s, d_blocks, nblocks, d_pi, w.T, d_L, w.start, w.hop_len, d_out);
     hipLaunchKernelGGL(k_ib_repeat, dim3(64, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_blocks, nblocks, w.cyc, d_out);
     BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+bool IbwtWorkspace::reserve_main(uint32_t nblocks, uint32_t nsplit, uint64_t slot_bytes)
+{
+    if (nblocks + 1 > cap_mb)
+    {
+        cap_mb           = 0;
+        const uint32_t c = nblocks + 64;
+        if (!dev_alloc(blk, (uint64_t) c * 4) || !dev_alloc(cum, c) || !dev_alloc(ctl, 512))
+            return false;
+        cap_mb = c;
+    }
+    if (nsplit > cap_ms)
+    {
+        cap_ms           = 0;
+        const uint32_t c = nsplit + nsplit / 8 + 64;
+        const uint32_t pc = c / 8 + 256;  // overflow chunks (hops longer than 4 S: ~2 % of them)
+        if (!dev_alloc(m_next, c) || !dev_alloc(m_len, c) || !dev_alloc(m_ovf, c) || !dev_alloc(m_start, c) || !dev_alloc(ovl_next, pc) ||
+            !dev_alloc(pool, (uint64_t) pc * IB_CHUNK))
+            return false;
+        cap_ms   = c;
+        pool_cap = pc;
+    }
+    if (slot_bytes > cap_slot)
+    {
+        cap_slot         = 0;
+        const uint64_t c = slot_bytes + slot_bytes / 8 + 4096;
+        if (!dev_alloc(slot, c))
+            return false;
+        cap_slot = c;
+    }
+    return true;
+}
+
+bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, const BlockDesc* d_blocks, const BlockDesc* h_blocks,
+                 uint32_t nblocks, uint8_t* d_out, hipStream_t s, bool keep_transform)
+{
+    if (!w.tiling.build(h_blocks, nblocks, ITILE, s))
+        return false;
+    uint64_t N = 0;
+    bool     main_path = !keep_transform;
+    for (uint32_t b = 0; b < nblocks; ++b)
+    {
+        N = std::max<uint64_t>(N, h_blocks[b].off + h_blocks[b].len);
+        main_path = main_path && h_blocks[b].len < (1u << 24);
+    }
+    const uint32_t nt = w.tiling.n;
+    if (!w.reserve(N, nblocks, nt))
+        return false;
+    hipLaunchKernelGGL(k_ib_hist, dim3(std::min<uint32_t>(nt, 8192)), dim3(TPB), 0, s, d_L, w.tiling.d_pieces, nt, w.th);
+    hipLaunchKernelGGL(k_ib_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, w.th);
+    if (!main_path)
+        return ibwt_two_walk(w, d_L, d_pi, d_blocks, nblocks, d_out, s);
+
+    // splitter geometry: step S >= 64, at most 16384 regular splitters per block; slots of 4 S bytes
+    if (w.h_key.size() != nblocks || !std::equal(w.h_key.begin(), w.h_key.end(), h_blocks,
+                                                 [](const BlockDesc& a, const BlockDesc& b) { return a.off == b.off && a.len == b.len; }))
+    {
+        w.h_blk.assign(nblocks * 4, 0);
+        std::vector<uint32_t> cum(nblocks + 1), ctl(512, 0);
+        uint64_t              slot = 0;
+        uint32_t              G    = 0;
+        for (uint32_t b = 0; b < nblocks; ++b)
+        {
+            const uint32_t n     = h_blocks[b].len;
+            uint32_t       shift = 6;
+            while (((uint64_t) n + (1u << shift) - 1) >> shift > IB_MAXS - 1)
+                ++shift;
+            const uint32_t ns = (uint32_t) (((uint64_t) n + (1u << shift) - 1) >> shift);
+            IbBlk          B{h_blocks[b].off, slot, n, shift, ns, 0};
+            std::memcpy(&w.h_blk[(size_t) b * 4], &B, sizeof B);
+            cum[b] = G;
+            G += ns + 1;
+            slot += (uint64_t) (ns + 1) * (4u << shift);
+        }
+        cum[nblocks] = G;
+        // XCD x serves blocks [xr[x], xr[x+1]): contiguous eighths of the batch
+        for (uint32_t x = 0; x <= 8; ++x)
+            ctl[256 + x] = (uint32_t) ((uint64_t) nblocks * x / 8);
+        if (!w.reserve_main(nblocks, G, slot))
+            return false;
+        w.G = G;
+        w.h_key.clear();
+        BRA_HIP_CHECK(hipMemcpyAsync(w.blk, w.h_blk.data(), (size_t) nblocks * sizeof(IbBlk), hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipMemcpyAsync(w.cum, cum.data(), (size_t) (nblocks + 1) * 4, hipMemcpyHostToDevice, s));
+        w.h_ctl = ctl;
+        BRA_HIP_CHECK(hipMemcpyAsync(w.ctl, w.h_ctl.data(), 512 * 4, hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));  // host vectors are the copies' sources
+        w.h_key.assign(h_blocks, h_blocks + nblocks);
+    }
+    const IbBlk* blk = reinterpret_cast<const IbBlk*>(w.blk);
+    // ctl[0..255]: 8 claim counters (32-word stride), ctl[256..264]: XCD block ranges, ctl[300]: pool counter
+    BRA_HIP_CHECK(hipMemsetAsync(w.ctl, 0, 256 * 4, s));
+    BRA_HIP_CHECK(hipMemsetAsync(w.ctl + 300, 0, 4, s));
+    hipLaunchKernelGGL(k_ib_scatter2, dim3(std::min<uint32_t>(nt, 16384)), dim3(64), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks, w.T);
+    WalkArgs a{blk, d_pi, w.cum, w.ctl + 256, w.ctl, w.T, w.slot, w.pool, w.ctl + 300, w.pool_cap, w.ovl_next, w.m_next, w.m_len, w.m_ovf};
+    hipLaunchKernelGGL(k_ib_walk3, dim3(2048), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
+                       w.m_len, w.m_start, w.cyc);
+    hipLaunchKernelGGL(k_ib_copy3, dim3(256, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, blk, w.cum, nblocks, w.m_start, w.m_len,
+                       w.m_ovf, w.ovl_next, w.slot, w.pool, w.pool_cap, d_out);
+    hipLaunchKernelGGL(k_ib_repeat, dim3(64, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_blocks, nblocks, w.cyc, d_out);
+    BRA_HIP_CHECK(hipGetLastError());
+    // overflow pool exhausted (hops far longer than 4 S, e.g. adversarial inputs): redo the batch
+    // with the two-walk path, which needs no staging
+    uint32_t used = 0;
+    BRA_HIP_CHECK(hipMemcpyAsync(&used, w.ctl + 300, 4, hipMemcpyDeviceToHost, s));
+    BRA_HIP_CHECK(hipStreamSynchronize(s));
+    if (used > w.pool_cap)
+        return ibwt_two_walk(w, d_L, d_pi, d_blocks, nblocks, d_out, s);
     return true;
 }
 

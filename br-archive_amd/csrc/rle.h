@@ -28,11 +28,9 @@ bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_
                        uint8_t* d_out, uint32_t* d_rle_size, uint32_t* d_hist, hipStream_t s);
 
 // Decode: block b's stream is at d_in + d_in_base[b] (d_in_size[b] bytes); output goes to
-// d_out + d_out_base[b] (capacity d_out_cap[b]).  d_out_size[b] = decoded size, 0 on a malformed
-// stream (bra_rle_decode_compute_size semantics).  d_recs: 8 bytes per record, block b's records
-// from index d_rec_base[b] (a block needs <= in_size/2 + 1 records); d_nrec: nblocks words.
+// d_out + d_out_base[b] (capacity d_out_cap[b]; writes past it are dropped).  d_out_size[b] =
+// decoded size, 0 on a malformed stream (bra_rle_decode_compute_size semantics).
 bool rle_decode_device(const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
-                       const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, void* d_recs, const uint64_t* d_rec_base,
-                       uint32_t* d_nrec, hipStream_t s);
+                       const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, hipStream_t s);
 
 }  // namespace bra

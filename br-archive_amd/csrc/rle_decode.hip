@@ -5,141 +5,292 @@
 // 1-c times; c == -128 -> no-op; a block truncated by the end of the stream makes the decoded size
 // 0 (error).
 //
-// The position of each control byte depends on every earlier one, so one lane per block parses the
-// control bytes out of an LDS window of the stream (the payload bytes are never touched) and
-// records (stream offset, output offset) per control; all threads then expand the records.
+// The position of each control byte depends on every earlier one: the controls form a chain
+// p -> nxt(p) = p + (c+2 | 2 | 1) through the stream.  One 1024-thread workgroup decodes one block,
+// a 16 KiB window of the stream at a time, one wave per 1 KiB sub-window:
+//   1. every wave computes, for every position p of its sub-window, where the chain from p leaves
+//      the sub-window and how many output bytes it produces on the way (pointer jumping in LDS:
+//      log2 of the chain length rounds, usually 3..8);
+//   2. one lane chains the 16 sub-windows from the window's entry control (16 LDS lookups);
+//   3. every wave walks the chain through its sub-window from its entry (lane-exchange steps on
+//      the original successors, 64 positions per register), compacts the controls on the chain
+//      with their output offsets, and writes its output range: each lane finds the control of its
+//      16 output bytes (binary search + forward steps) and takes them from the staged window.
+// Everything stays in LDS; the next window's bytes are loaded while the current one is decoded.
 #include "rle.h"
 
 namespace bra {
 
 namespace {
 
-constexpr uint32_t WIN = 8192;
+constexpr uint32_t RD_WAVES = 16;                   // waves per workgroup = sub-windows per window
+constexpr uint32_t RD_TPB   = RD_WAVES * 64;
+constexpr uint32_t RD_SUB   = 1024;                 // stream bytes per sub-window (16 per lane)
+constexpr uint32_t RD_PER   = RD_SUB / 64;          // positions per lane
+constexpr uint32_t RD_WIN   = RD_WAVES * RD_SUB;    // 16 KiB window
+constexpr uint32_t RD_HALO  = 256;                  // a literal's payload runs up to 128 bytes past its window
+constexpr uint32_t RD_LOAD  = (RD_WIN + RD_HALO) / 16;  // 16-byte loads per window (<= 2 per thread)
 
-struct Rec
+__device__ __forceinline__ void wave_lds_sync()
 {
-    uint32_t src, dst;
-};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
-// one 64-thread workgroup per block
-__global__ void __launch_bounds__(64) k_rled_parse(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_base,
-                                                   const uint32_t* __restrict__ in_size, uint32_t nblocks, Rec* __restrict__ recs,
-                                                   const uint64_t* __restrict__ rec_base, uint32_t* __restrict__ nrec,
-                                                   uint32_t* __restrict__ out_size)
+// control byte -> (stream step, output bytes)
+__device__ __forceinline__ uint32_t ctl_step(uint32_t c) { return c < 128u ? c + 2u : (c > 128u ? 2u : 1u); }
+__device__ __forceinline__ uint32_t ctl_prod(uint32_t c) { return c < 128u ? c + 1u : (c > 128u ? 257u - c : 0u); }
+
+// 16 bytes of the stream at window offset q (global), zero past the end
+__device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ src, uint32_t size, uint32_t at)
 {
-    __shared__ uint8_t  win[WIN];
-    __shared__ uint32_t sh_i, sh_dst, sh_n, sh_err;
+    if (at + 16u <= size && (((uintptr_t) (src + at)) & 15) == 0)
+        return *reinterpret_cast<const uint4*>(src + at);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < 16; ++k)
+        if (at + k < size)
+            w[k >> 2] |= (uint32_t) src[at + k] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_base,
+                                                 const uint32_t* __restrict__ in_size, uint32_t nblocks, uint8_t* __restrict__ out,
+                                                 const uint64_t* __restrict__ out_base, const uint64_t* __restrict__ out_cap,
+                                                 uint32_t* __restrict__ out_size)
+{
+    __shared__ uint4    win4[(RD_WIN + RD_HALO) / 16];
+    __shared__ uint16_t NX[RD_WAVES][RD_SUB];  // successor (sub-window position; >= len: exit) / later: chain positions
+    __shared__ uint32_t SM[RD_WAVES][RD_SUB];  // output bytes to the exit / later: output offsets of the chain
+    __shared__ uint32_t sub_entry[RD_WAVES], sub_out[RD_WAVES], sub_tot[RD_WAVES];
+    __shared__ uint32_t sh_E, sh_O;
+    const uint8_t* win  = reinterpret_cast<const uint8_t*>(win4);
+    const int      lane = lane_id();
+    const uint32_t k    = threadIdx.x >> 6;  // this wave's sub-window
+    const uint64_t below = (1ull << lane) - 1ull;
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint8_t* src  = in + in_base[b];
         const uint32_t size = in_size[b];
-        Rec*           R    = recs + rec_base[b];
+        uint8_t*       dst  = out + out_base[b];
+        const uint64_t cap  = out_cap[b];
         if (threadIdx.x == 0)
         {
-            sh_i = 0;
-            sh_dst = 0;
-            sh_n = 0;
-            sh_err = 0;
+            sh_E = 0;
+            sh_O = 0;
         }
-        __syncthreads();
-        while (true)
+        // prefetch window 0
+        uint4 pf[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
         {
-            const uint32_t w0 = sh_i;
-            if (w0 >= size || sh_err)
-                break;
-            const uint32_t wl = min(WIN, size - w0);
-            for (uint32_t k = threadIdx.x; k < wl; k += 64)
-                win[k] = src[w0 + k];
+            const uint32_t t = threadIdx.x + h * RD_TPB;
+            pf[h]            = t < RD_LOAD ? load16(src, size, t * 16) : make_uint4(0, 0, 0, 0);
+        }
+        for (uint32_t w0 = 0; w0 < size; w0 += RD_WIN)
+        {
+            __syncthreads();  // previous window fully consumed
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+            {
+                const uint32_t t = threadIdx.x + h * RD_TPB;
+                if (t < RD_LOAD)
+                    win4[t] = pf[h];
+            }
             __syncthreads();
+            // prefetch the next window while this one is decoded
+            if (w0 + RD_WIN < size)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                {
+                    const uint32_t t = threadIdx.x + h * RD_TPB;
+                    pf[h]            = t < RD_LOAD ? load16(src, size, w0 + RD_WIN + t * 16) : make_uint4(0, 0, 0, 0);
+                }
+
+            // ---- 1. chain exits of every position of this wave's sub-window ----
+            const uint32_t sb  = k * RD_SUB;
+            const uint32_t rem = size - w0;
+            const uint32_t len = rem > sb ? min(RD_SUB, rem - sb) : 0u;
+            uint32_t       nx0[RD_PER], nx[RD_PER], sm[RD_PER];
+#pragma unroll
+            for (int m = 0; m < (int) RD_PER; ++m)
+            {
+                const uint32_t p = m * 64 + lane;
+                const uint32_t c = win[sb + p];
+                nx0[m]           = p + ctl_step(c);
+                nx[m]            = nx0[m];
+                sm[m]            = ctl_prod(c);
+                if (p < len)
+                {
+                    NX[k][p] = (uint16_t) nx[m];
+                    SM[k][p] = sm[m];
+                }
+            }
+            wave_lds_sync();
+            while (true)
+            {
+                bool     act = false;
+                uint32_t nn[RD_PER], ss[RD_PER];
+#pragma unroll
+                for (int m = 0; m < (int) RD_PER; ++m)
+                {
+                    const uint32_t p = m * 64 + lane;
+                    nn[m]            = nx[m];
+                    ss[m]            = 0;
+                    if (p < len && nx[m] < len)
+                    {
+                        nn[m] = NX[k][nx[m]];
+                        ss[m] = SM[k][nx[m]];
+                        act   = true;
+                    }
+                }
+                if (!__builtin_amdgcn_ballot_w64(act))
+                    break;
+                wave_lds_sync();
+#pragma unroll
+                for (int m = 0; m < (int) RD_PER; ++m)
+                {
+                    const uint32_t p = m * 64 + lane;
+                    if (p < len && nx[m] < len)
+                    {
+                        nx[m] = nn[m];
+                        sm[m] += ss[m];
+                        NX[k][p] = (uint16_t) nx[m];
+                        SM[k][p] = sm[m];
+                    }
+                }
+                wave_lds_sync();
+            }
+            __syncthreads();
+
+            // ---- 2. entries and output offsets of the sub-windows ----
             if (threadIdx.x == 0)
             {
-                uint32_t i = w0, dst = sh_dst, n = sh_n;
-                while (i < size && i < w0 + wl)
+                uint32_t e = sh_E, o = sh_O;  // e: window offset of the next control
+                for (uint32_t q = 0; q < RD_WAVES; ++q)
                 {
-                    const int c = (int8_t) win[i - w0];
-                    if (c >= 0)
+                    const uint32_t qb = q * RD_SUB;
+                    const uint32_t ql = rem > qb ? min(RD_SUB, rem - qb) : 0u;
+                    sub_entry[q]      = e - qb;  // >= ql: the chain skips this sub-window (end of stream)
+                    sub_out[q]        = o;
+                    uint32_t t        = 0;
+                    if (e - qb < ql)
                     {
-                        if (i + 1 + (uint32_t) c + 1 > size)
-                        {
-                            sh_err = 1;
-                            break;
-                        }
-                        R[n++] = Rec{i, dst};
-                        dst += (uint32_t) c + 1;
-                        i += (uint32_t) c + 2;
+                        const uint32_t el = e - qb;
+                        t                 = SM[q][el];
+                        e                 = qb + NX[q][el];
                     }
-                    else if (c >= -127)
-                    {
-                        if (i + 1 >= size)
-                        {
-                            sh_err = 1;
-                            break;
-                        }
-                        R[n++] = Rec{i, dst};
-                        dst += (uint32_t) (1 - c);
-                        i += 2;
-                    }
-                    else
-                        i += 1;
+                    sub_tot[q] = t;
+                    o += t;
                 }
-                sh_i   = i;
-                sh_dst = dst;
-                sh_n   = n;
+                sh_E = e - RD_WIN;  // entry of the next window (exit offset past the stream end at the last one)
+                sh_O = o;
             }
             __syncthreads();
-        }
-        if (threadIdx.x == 0)
-        {
-            nrec[b]     = sh_n;
-            out_size[b] = sh_err ? 0 : sh_dst;
-        }
-        __syncthreads();
-    }
-}
 
-// expand records: grid.y = block
-__global__ void k_rled_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_base, uint32_t nblocks,
-                              const Rec* __restrict__ recs, const uint64_t* __restrict__ rec_base, const uint32_t* __restrict__ nrec,
-                              const uint32_t* __restrict__ out_size, uint8_t* __restrict__ out, const uint64_t* __restrict__ out_base,
-                              const uint64_t* __restrict__ out_cap)
-{
-    for (uint32_t b = blockIdx.y; b < nblocks; b += gridDim.y)
-    {
-        const uint32_t os = out_size[b];
-        if (os == 0 || os > out_cap[b])
-            continue;
-        const uint8_t* src = in + in_base[b];
-        const Rec*     R   = recs + rec_base[b];
-        uint8_t*       dst = out + out_base[b];
-        const uint32_t n   = nrec[b];
-        for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
-        {
-            const Rec E = R[r];
-            const int c = (int8_t) src[E.src];
-            if (c >= 0)
-                for (int k = 0; k <= c; ++k)
-                    dst[E.dst + k] = src[E.src + 1 + k];
-            else
+            // ---- 3. walk the chain through this sub-window, compact it, write the output ----
+            const uint32_t ent = sub_entry[k];
+            const uint32_t tot = sub_tot[k];
+            const uint32_t ob0 = sub_out[k];
+            uint32_t       ncon = 0;
+            if (ent < len)
             {
-                const uint8_t v = src[E.src + 1];
-                for (int k = 0; k < 1 - c; ++k)
-                    dst[E.dst + k] = v;
+                const uint32_t sm_entry = SM[k][ent];
+                wave_lds_sync();  // everyone read SM[k][ent] before the compaction overwrites it
+                uint32_t e = ent;
+#pragma unroll
+                for (int m = 0; m < (int) RD_PER; ++m)
+                {
+                    uint64_t       on  = 0;
+                    const uint32_t top = min((uint32_t) (m + 1) * 64u, len);
+                    while (e < top)
+                    {
+                        const uint32_t l = e - m * 64;
+                        on |= 1ull << l;
+                        e = (uint32_t) __builtin_amdgcn_readlane((int) nx0[m], (int) l);
+                    }
+                    if ((on >> lane) & 1)
+                    {
+                        const uint32_t idx = ncon + (uint32_t) __popcll(on & below);
+                        NX[k][idx]         = (uint16_t) (m * 64 + lane);
+                        SM[k][idx]         = sm_entry - sm[m];  // output offset inside the sub-window's range
+                    }
+                    ncon += (uint32_t) __popcll(on);
+                }
+                wave_lds_sync();
+            }
+            // output bytes [ob0, ob0 + tot) of the block: 16 per lane per round
+            for (uint32_t r0 = 0; r0 < tot; r0 += 64 * 16)
+            {
+                const uint32_t o0 = r0 + lane * 16;  // relative to ob0
+                if (o0 < tot)
+                {
+                    // last control with offset <= o0
+                    uint32_t lo = 0, hi = ncon - 1;
+                    while (lo < hi)
+                    {
+                        const uint32_t mid = (lo + hi + 1) >> 1;
+                        if (SM[k][mid] <= o0)
+                            lo = mid;
+                        else
+                            hi = mid - 1;
+                    }
+                    uint32_t idx = lo, d = SM[k][idx], p = NX[k][idx];
+                    uint32_t dn = idx + 1 < ncon ? SM[k][idx + 1] : 0xFFFFFFFFu;
+                    uint32_t wv[4] = {0, 0, 0, 0};
+                    const uint32_t nb = min(16u, tot - o0);
+                    for (uint32_t j = 0; j < nb; ++j)
+                    {
+                        const uint32_t o = o0 + j;
+                        while (o >= dn)
+                        {
+                            ++idx;
+                            d  = dn;
+                            p  = NX[k][idx];
+                            dn = idx + 1 < ncon ? SM[k][idx + 1] : 0xFFFFFFFFu;
+                        }
+                        const uint32_t at = sb + p;
+                        const uint32_t c  = win[at];
+                        const uint32_t v  = win[at + 1 + (c < 128u ? o - d : 0u)];
+                        wv[j >> 2] |= v << (8 * (j & 3));
+                    }
+                    const uint64_t a = (uint64_t) ob0 + o0;  // block output offset
+                    uint8_t*       q = dst + a;
+                    if (nb == 16 && a + 16 <= cap && (((uintptr_t) q) & 15) == 0)
+                        *reinterpret_cast<uint4*>(q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                    else if (nb == 16 && a + 16 <= cap && (((uintptr_t) q) & 3) == 0)
+                    {
+#pragma unroll
+                        for (int h = 0; h < 4; ++h)
+                            reinterpret_cast<uint32_t*>(q)[h] = wv[h];
+                    }
+                    else
+                        for (uint32_t j = 0; j < nb; ++j)
+                            if (a + j < cap)
+                                q[j] = (uint8_t) (wv[j >> 2] >> (8 * (j & 3)));
+                }
             }
         }
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            // the chain must end exactly at the end of the stream (sh_E = its overshoot past the
+            // window holding the stream end, measured from that window's end: recompute it)
+            const uint32_t last_w0 = size ? ((size - 1) / RD_WIN) * RD_WIN : 0u;
+            const uint32_t over    = (sh_E + RD_WIN) - (size - last_w0);  // exit position minus stream length
+            out_size[b]            = (size == 0 || over != 0) ? 0u : sh_O;
+        }
+        __syncthreads();
     }
 }
 
 }  // namespace
 
 bool rle_decode_device(const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
-                       const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, void* d_recs, const uint64_t* d_rec_base,
-                       uint32_t* d_nrec, hipStream_t s)
+                       const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, hipStream_t s)
 {
-    Rec* recs = static_cast<Rec*>(d_recs);
-    hipLaunchKernelGGL(k_rled_parse, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_in, d_in_base, d_in_size, nblocks, recs,
-                       d_rec_base, d_nrec, d_out_size);
-    hipLaunchKernelGGL(k_rled_expand, dim3(64, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_in, d_in_base, nblocks, recs,
-                       d_rec_base, d_nrec, d_out_size, d_out, d_out_base, d_out_cap);
+    hipLaunchKernelGGL(k_rled, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks, d_out,
+                       d_out_base, d_out_cap, d_out_size);
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }
