@@ -33,7 +33,15 @@ struct HuffWorkspace
     uint32_t* flag       = nullptr;
     uint32_t* h_flag     = nullptr;  // pinned: flag, then the segment bases
     uint32_t  cap_b = 0, cap_t = 0, cap_tree = 0, cap_seg = 0, cap_segb = 0;
+    // canonical fast path: per-block tables, per-segment transfer words, WG tasks
+    uint32_t*             tab   = nullptr;
+    uint32_t*             trans = nullptr;
+    uint32_t*             seg_info = nullptr;
+    void*                 tasks = nullptr;
+    uint32_t              cap_fb = 0, cap_fs = 0, cap_ft = 0;
+    std::vector<uint32_t> h_segb;
     bool      reserve(uint32_t nblocks, uint32_t ntiles);
+    bool      reserve_fast(uint32_t nblocks, uint32_t nseg, uint32_t ntasks);
     bool      reserve_tree(uint32_t nblocks);
     bool      reserve_segs(uint32_t nseg, uint32_t nblocks);
     void      release();

@@ -903,6 +903,481 @@ __global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Canonical fast path.  A block whose code lengths are "clean" (at least one symbol, every length
+// <= 30, Kraft sum <= 1) has a reference tree that is exactly its canonical code: codes are
+// prefix-free, so the tree rebuild never collides (bra_huffman.c:263-348) and decoding walks the
+// canonical intervals.  Such blocks decode through tables (11-bit primary LUT, left-justified
+// interval limits for longer codes) and exact per-segment transfer functions:
+//   k_hd_canon   per block: interval limits, symbols by (length, value), the 11-bit LUT;
+//   k_hd_trans   per 2048-bit segment (one lane each, the block's tables in LDS, the bits in a
+//                4-dword register window): for every possible entry bit offset e < lmax (the true
+//                path enters the segment within lmax bits of its start) the exit offset past the
+//                segment end, the symbol count and whether the path dies (dead edge / out of data).
+//                The path from e = 0 records its codeword boundaries over the first 256 bits; a
+//                path from e > 0 that lands on one of them has merged and takes its count from
+//                the boundary's rank -- Huffman paths resynchronise within a few codewords, while
+//                codes of near-equal lengths (uniform data) keep separate phases and are walked out.
+//                No iteration over segments: the round-1 self-synchronisation loop needed up to 31
+//                passes on uniform random data (the phases drift).
+//   k_hd_chain   per block: follow the true entry from segment to segment -> entry and output
+//                offset of every segment, and the reference's acceptance (no death before symbol
+//                orig_size, enough data);
+//   k_hd_write2  per segment: decode the true path into its output range;
+//   k_hd_tail2   per block: the reference's end-of-stream walk (:455-498) on the intervals.
+// Any block that is not clean sends the batch to the tree-walking path above.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t HD2_SEG   = 2048;  // bits per segment
+constexpr uint32_t HD2_LMAX  = 30;
+constexpr uint32_t HD2_TPB   = 256;
+constexpr uint32_t HD2_REFB  = 256;   // boundary bitmap of the reference path (bits from the segment start)
+constexpr uint32_t HD2_STRD  = 32;    // transfer words per segment
+constexpr uint32_t HD2_TAB   = 2304;  // u32 words per block table
+
+// table layout (u32 words)
+constexpr uint32_t T_LUT = 0, T_LIM = 2048, T_FIRST = 2112, T_IDX = 2144, T_PERM = 2176, T_INFO = 2240;  // info: lmax, clean
+
+struct Hd2Lds
+{
+    uint32_t lut[2048];
+    uint64_t lim[32];
+    uint32_t first[32];
+    uint32_t idx[32];
+    uint8_t  perm[256];
+    uint32_t lmax;
+};
+
+__global__ void __launch_bounds__(256) k_hd_canon(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, uint32_t* __restrict__ tab,
+                                                  uint32_t* __restrict__ unclean)
+{
+    __shared__ uint32_t ln[256], cnt[257];
+    __shared__ uint64_t lim[32];
+    __shared__ uint32_t first[32], idx[32], sh_lmax, sh_clean;
+    __shared__ __attribute__((aligned(4))) uint8_t perm[256];
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        uint32_t* T = tab + (size_t) b * HD2_TAB;
+        const uint32_t t = threadIdx.x;
+        ln[t]   = meta[b].lengths[t];
+        cnt[t]  = 0;
+        perm[t] = 0;
+        if (t == 0)
+            cnt[256] = 0;
+        __syncthreads();
+        if (ln[t])
+            atomicAdd(&cnt[ln[t]], 1u);
+        __syncthreads();
+        if (t == 0)
+        {
+            uint32_t lmax = 0, nsym = 0;
+            for (uint32_t l = 1; l <= 255; ++l)
+                if (cnt[l])
+                {
+                    lmax = l;
+                    nsym += cnt[l];
+                }
+            bool     clean = nsym > 0 && lmax <= HD2_LMAX;
+            uint64_t code = 0;
+            uint32_t id   = 0;
+            for (uint32_t l = 1; l < 32; ++l)
+            {
+                code <<= 1;
+                const uint32_t c = l <= HD2_LMAX ? cnt[l] : 0u;
+                first[l]         = (uint32_t) code;
+                idx[l]           = id;
+                code += c;
+                id += c;
+                lim[l] = code << (32 - l);  // left-justified end of the length-l interval
+            }
+            first[0] = idx[0] = 0;
+            lim[0]            = 0;
+            clean             = clean && lim[lmax < 32 ? lmax : 31] <= (1ull << 32);  // Kraft sum <= 1
+            sh_lmax           = lmax;
+            sh_clean          = clean ? 1u : 0u;
+            if (!clean)
+                atomicOr(unclean, 1u);
+        }
+        __syncthreads();
+        const uint32_t lmax = sh_lmax;
+        if (sh_clean)
+        {
+            // symbols by (length, value)
+            if (ln[t])
+            {
+                uint32_t r = 0;
+                for (uint32_t u = 0; u < t; ++u)
+                    r += ln[u] == ln[t] ? 1u : 0u;
+                perm[idx[ln[t]] + r] = (uint8_t) t;
+            }
+            __syncthreads();
+            // 11-bit LUT: sym | len << 8 | kind << 13 (0 leaf, 1 longer code, 2 dead)
+            for (uint32_t v = t; v < 2048; v += 256)
+            {
+                const uint64_t vj    = (uint64_t) v << 21;
+                uint32_t       e     = 2u << 13;
+                bool           found = false;
+                for (uint32_t l = 1; l <= min(lmax, 11u) && !found; ++l)
+                    if (vj < lim[l])
+                    {
+                        e     = perm[idx[l] + (uint32_t) (v >> (11 - l)) - first[l]] | (l << 8);
+                        found = true;
+                    }
+                if (!found && lmax > 11 && vj < lim[lmax])
+                    e = 1u << 13;
+                T[T_LUT + v] = e;
+            }
+            if (t < 32)
+            {
+                reinterpret_cast<uint64_t*>(T + T_LIM)[t] = lim[t];
+                T[T_FIRST + t]                            = first[t];
+                T[T_IDX + t]                              = idx[t];
+            }
+            if (t < 64)
+                T[T_PERM + t] = reinterpret_cast<const uint32_t*>(perm)[t];
+            if (t == 0)
+            {
+                T[T_INFO]     = lmax;
+                T[T_INFO + 1] = 1;
+            }
+        }
+        else if (t == 0)
+        {
+            T[T_INFO]     = lmax;
+            T[T_INFO + 1] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void hd2_load_tables(const uint32_t* __restrict__ T, Hd2Lds& L)
+{
+    for (uint32_t i = threadIdx.x; i < 2048; i += blockDim.x)
+        L.lut[i] = T[T_LUT + i];
+    if (threadIdx.x < 32)
+    {
+        L.lim[threadIdx.x]   = reinterpret_cast<const uint64_t*>(T + T_LIM)[threadIdx.x];
+        L.first[threadIdx.x] = T[T_FIRST + threadIdx.x];
+        L.idx[threadIdx.x]   = T[T_IDX + threadIdx.x];
+    }
+    if (threadIdx.x < 64)
+        reinterpret_cast<uint32_t*>(L.perm)[threadIdx.x] = T[T_PERM + threadIdx.x];
+    if (threadIdx.x == 0)
+        L.lmax = T[T_INFO];
+    __syncthreads();
+}
+
+// One codeword from the left-justified 32 bits v: length and symbol, false on a dead edge.
+__device__ __forceinline__ bool hd2_dec(const Hd2Lds& L, uint32_t v, uint32_t& len, uint32_t& sym)
+{
+    const uint32_t e = L.lut[v >> 21], kind = e >> 13;
+    if (kind == 0)
+    {
+        len = (e >> 8) & 31u;
+        sym = e & 0xFFu;
+        return true;
+    }
+    if (kind == 2)
+        return false;
+    for (uint32_t l = 12; l <= L.lmax; ++l)
+        if ((uint64_t) v < L.lim[l])
+        {
+            len = l;
+            sym = L.perm[L.idx[l] + (v >> (32 - l)) - L.first[l]];
+            return true;
+        }
+    return false;
+}
+
+// The bits of one block seen through a 4-dword window (MSB-first, byte-swapped dwords).  Block bit p
+// is bit q = p + lead of the dword-aligned stream starting at `base`; dwords past the block's data
+// are clamped to its last dword (their bits are never decisive: a codeword that needs them does
+// not fit in the data).
+struct BitWin
+{
+    const uint32_t* base;
+    uint32_t        lead, kmax;
+    uint32_t        wb;  // bit q of W[0]'s first bit
+    uint32_t        W[4];
+
+    __device__ __forceinline__ uint32_t ld(uint32_t k) const { return __builtin_bswap32(base[min(k, kmax)]); }
+    __device__ __forceinline__ void     init(uint32_t p)
+    {
+        const uint32_t q = p + lead;
+        wb               = q & ~31u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            W[i] = ld((wb >> 5) + i);
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t p)
+    {
+        uint32_t o = p + lead - wb;
+        if (o >= 64)
+        {
+            W[0] = W[1];
+            W[1] = W[2];
+            W[2] = W[3];
+            wb += 32;
+            W[3] = ld((wb >> 5) + 3);
+            o -= 32;
+        }
+        const uint32_t i = o >> 5, sh = o & 31;
+        const uint32_t a = i == 0 ? W[0] : i == 1 ? W[1] : W[2];
+        const uint32_t c = i == 0 ? W[1] : i == 1 ? W[2] : W[3];
+        return (uint32_t) ((((uint64_t) a << 32) | c) >> (32 - sh));
+    }
+};
+
+__device__ __forceinline__ BitWin hd2_win(const uint8_t* payload, uint64_t off, uint32_t nbytes)
+{
+    BitWin         W;
+    const uint64_t a = (uint64_t) (uintptr_t) (payload + off);
+    W.base           = reinterpret_cast<const uint32_t*>((uintptr_t) (a & ~3ull));
+    W.lead           = (uint32_t) (a & 3) * 8;
+    W.kmax           = nbytes ? (uint32_t) ((a & 3) + nbytes - 1) >> 2 : 0u;
+    W.wb             = 0;
+    return W;
+}
+
+struct Hd2Task
+{
+    uint32_t block, seg0;
+};
+
+__global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restrict__ meta, const uint8_t* __restrict__ payload,
+                                                      const uint64_t* __restrict__ payload_off, const uint32_t* __restrict__ tab,
+                                                      const Hd2Task* __restrict__ tasks, uint32_t ntasks, const uint32_t* __restrict__ seg_base,
+                                                      uint32_t* __restrict__ trans)
+{
+    __shared__ Hd2Lds L;
+    for (uint32_t tk = blockIdx.x; tk < ntasks; tk += gridDim.x)
+    {
+        const Hd2Task  K = tasks[tk];
+        const uint32_t b = K.block;
+        __syncthreads();
+        hd2_load_tables(tab + (size_t) b * HD2_TAB, L);
+        const uint32_t nbytes = meta[b].encoded_size, nbits = nbytes * 8;
+        const uint32_t j = K.seg0 + threadIdx.x, g0 = seg_base[b], ns = seg_base[b + 1] - g0;
+        if (j >= ns)
+            continue;
+        BitWin         W = hd2_win(payload, payload_off[b], nbytes);
+        const uint32_t s = j * HD2_SEG, stop = min(s + HD2_SEG, nbits), nent = j == 0 ? 1u : L.lmax;
+        uint32_t*      out = trans + (size_t) (g0 + j) * HD2_STRD;
+        // the reference path from entry 0, recording its boundaries over the first HD2_REFB bits
+        uint32_t bm[HD2_REFB / 32];
+#pragma unroll
+        for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+            bm[i] = 0;
+        W.init(s);
+        uint32_t p = s, c = 0, bad = 0, len, sym;
+        while (p < stop)
+        {
+            const uint32_t d = p - s;
+            if (d < HD2_REFB)
+            {
+#pragma unroll
+                for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                    if ((d >> 5) == (uint32_t) i)
+                        bm[i] |= 1u << (d & 31);
+            }
+            if (!hd2_dec(L, W.peek(p), len, sym) || len > nbits - p)
+            {
+                bad = 1;
+                break;
+            }
+            p += len;
+            ++c;
+        }
+        const uint32_t c0 = c, r0 = (bad << 31) | (((p - stop) & 31u) << 16);
+        out[0]               = r0 | c0;
+        for (uint32_t e = 1; e < nent; ++e)
+        {
+            W.init(s + e);
+            p = s + e;
+            c = 0;
+            bad = 0;
+            bool merged = false;
+            while (p < stop)
+            {
+                const uint32_t d = p - s;
+                if (d < HD2_REFB)
+                {
+                    uint32_t hit = 0, rank = 0;
+#pragma unroll
+                    for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                    {
+                        const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
+                        rank += (uint32_t) __popc(bm[i] & m);
+                        hit |= (d >> 5) == (uint32_t) i ? (bm[i] >> (d & 31)) & 1u : 0u;
+                    }
+                    if (hit)
+                    {
+                        out[e] = r0 | (c + c0 - rank);
+                        merged = true;
+                        break;
+                    }
+                }
+                if (!hd2_dec(L, W.peek(p), len, sym) || len > nbits - p)
+                {
+                    bad = 1;
+                    break;
+                }
+                p += len;
+                ++c;
+            }
+            if (!merged)
+                out[e] = (bad << 31) | (((p - stop) & 31u) << 16) | c;
+        }
+    }
+}
+
+// Per block: the true path from segment to segment.
+__global__ void __launch_bounds__(64) k_hd_chain(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint32_t* __restrict__ seg_base,
+                                                 const uint32_t* __restrict__ trans, uint32_t* __restrict__ seg_info, uint32_t* __restrict__ status)
+{
+    __shared__ uint32_t rows[64 * HD2_STRD];
+    const int           lane = lane_id();
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const uint32_t g0 = seg_base[b], ns = seg_base[b + 1] - g0, osz = meta[b].orig_size;
+        uint32_t       e = 0, acc = 0, fail = 0, done = 0;
+        for (uint32_t c0 = 0; c0 < ns; c0 += 64)
+        {
+            const uint32_t nr = min(64u, ns - c0);
+            __syncthreads();
+            for (uint32_t i = lane; i < nr * HD2_STRD; i += 64)
+                rows[i] = trans[(size_t) (g0 + c0) * HD2_STRD + i];
+            __syncthreads();
+            if (lane == 0)
+                for (uint32_t k = 0; k < nr; ++k)
+                {
+                    uint32_t info = 0xFFFFFFFFu;  // (entry << 27) | output offset; all ones: nothing to write
+                    if (!done && acc < osz)
+                    {
+                        const uint32_t r = rows[k * HD2_STRD + e], cnt = r & 0xFFFFu;
+                        info             = (e << 27) | acc;
+                        if (r >> 31)
+                        {
+                            if (acc + cnt < osz)
+                                fail = 1;  // the path dies before symbol orig_size
+                            done = 1;
+                        }
+                        acc += cnt;
+                        e = (r >> 16) & 31u;
+                    }
+                    seg_info[g0 + c0 + k] = info;
+                }
+        }
+        if (lane == 0)
+            status[b] = (fail || acc < osz) ? 1u : 0u;
+    }
+}
+
+// Per segment: decode the true path into out[off, off + n).
+__global__ void __launch_bounds__(HD2_TPB) k_hd_write2(const HuffMetaRec* __restrict__ meta, const uint8_t* __restrict__ payload,
+                                                       const uint64_t* __restrict__ payload_off, const uint32_t* __restrict__ tab,
+                                                       const Hd2Task* __restrict__ tasks, uint32_t ntasks, const uint32_t* __restrict__ seg_base,
+                                                       const uint32_t* __restrict__ trans, const uint32_t* __restrict__ seg_info,
+                                                       const uint32_t* __restrict__ status, uint8_t* __restrict__ out,
+                                                       const uint64_t* __restrict__ out_base, uint64_t* __restrict__ end_pos)
+{
+    __shared__ Hd2Lds L;
+    for (uint32_t tk = blockIdx.x; tk < ntasks; tk += gridDim.x)
+    {
+        const Hd2Task  K = tasks[tk];
+        const uint32_t b = K.block;
+        __syncthreads();
+        hd2_load_tables(tab + (size_t) b * HD2_TAB, L);
+        const uint32_t j = K.seg0 + threadIdx.x, g0 = seg_base[b], ns = seg_base[b + 1] - g0;
+        if (j >= ns || status[b])
+            continue;
+        const uint32_t info = seg_info[g0 + j];
+        const uint32_t osz  = meta[b].orig_size;
+        if (info == 0xFFFFFFFFu)
+            continue;
+        const uint32_t e = info >> 27, off = info & 0x7FFFFFFu;
+        if (off >= osz)
+            continue;
+        const uint32_t cnt = trans[(size_t) (g0 + j) * HD2_STRD + e] & 0xFFFFu;
+        const uint32_t n   = min(cnt, osz - off);
+        const uint32_t nbytes = meta[b].encoded_size;
+        BitWin         W      = hd2_win(payload, payload_off[b], nbytes);
+        uint32_t       p      = j * HD2_SEG + e, len = 0, sym = 0;
+        W.init(p);
+        uint8_t* dst = out + out_base[b] + off;
+        // bytes until dst is dword aligned, then whole dwords, then the rest
+        uint32_t i = 0;
+        for (; i < n && (((uintptr_t) (dst + i)) & 3); ++i)
+        {
+            (void) hd2_dec(L, W.peek(p), len, sym);
+            p += len;
+            dst[i] = (uint8_t) sym;
+        }
+        for (; i + 4 <= n; i += 4)
+        {
+            uint32_t wv = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+            {
+                (void) hd2_dec(L, W.peek(p), len, sym);
+                p += len;
+                wv |= sym << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(dst + i) = wv;
+        }
+        for (; i < n; ++i)
+        {
+            (void) hd2_dec(L, W.peek(p), len, sym);
+            p += len;
+            dst[i] = (uint8_t) sym;
+        }
+        if (off + n == osz)
+            end_pos[b] = p;
+    }
+}
+
+// Per block: the end-of-stream walk on the intervals.  From the byte boundary after the last symbol
+// (bit 0 for orig_size 0) the reference walks the remaining r bits as one codeword: completing a
+// symbol or meeting a dead edge within them is an error.  With v = those bits left-justified and
+// zero-filled: dead within r bits <=> v >= lim[lmax]; a codeword completes <=> v's interval length
+// is <= r (a shorter codeword that is a prefix of the bits would contain v).
+__global__ void k_hd_tail2(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint8_t* __restrict__ payload,
+                           const uint64_t* __restrict__ payload_off, const uint32_t* __restrict__ tab, const uint64_t* __restrict__ end_pos,
+                           uint32_t* __restrict__ status)
+{
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nblocks; b += gridDim.x * blockDim.x)
+    {
+        if (status[b])
+            continue;
+        const uint32_t  nbytes = meta[b].encoded_size, nbits = nbytes * 8;
+        const uint64_t  p2     = meta[b].orig_size ? ((end_pos[b] + 7) & ~7ull) : 0;
+        const uint32_t* T      = tab + (size_t) b * HD2_TAB;
+        const uint32_t  lmax   = T[T_INFO];
+        if (p2 >= nbits)
+            continue;
+        const uint32_t r = nbits - (uint32_t) p2;
+        if (r >= lmax)
+        {
+            status[b] = 1;  // within lmax bits a walk completes or dies
+            continue;
+        }
+        const uint8_t* src = payload + payload_off[b] + (p2 >> 3);
+        uint32_t       v   = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+            v = (v << 8) | ((p2 >> 3) + k < nbytes ? src[k] : 0u);
+        v &= r >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> r);
+        const uint64_t* lim = reinterpret_cast<const uint64_t*>(T + T_LIM);
+        uint32_t        err = (uint64_t) v >= lim[lmax] ? 1u : 0u;
+        if (!err)
+            for (uint32_t l = 1; l <= lmax; ++l)
+                if ((uint64_t) v < lim[l])
+                {
+                    err = l <= r ? 1u : 0u;
+                    break;
+                }
+        status[b] = err;
+    }
+}
+
 }  // namespace
 
 bool HuffWorkspace::reserve(uint32_t nblocks, uint32_t ntiles)
@@ -987,6 +1462,10 @@ void HuffWorkspace::release()
     (void) hipFree(tree_sym);
     (void) hipFree(table);
     (void) hipFree(status);
+    (void) hipFree(tab);
+    (void) hipFree(trans);
+    (void) hipFree(seg_info);
+    (void) hipFree(tasks);
     *this = HuffWorkspace{};
 }
 
@@ -1042,8 +1521,11 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
     return true;
 }
 
-bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint32_t* h_encoded_size, uint32_t nblocks, const uint8_t* d_payload,
-                        const uint64_t* d_payload_off, uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s)
+// The tree-walking decoder (any code-length set the reference accepts, e.g. codes longer than 30
+// bits or an over-full length set the tree rebuild rejects): self-synchronising segments.
+static bool huff_decode_tree(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint32_t* h_encoded_size, uint32_t nblocks,
+                             const uint8_t* d_payload, const uint64_t* d_payload_off, uint8_t* d_out, const uint64_t* d_out_base,
+                             uint32_t* d_status, hipStream_t s)
 {
     if (!w.reserve(nblocks, 1) || !w.reserve_tree(nblocks))
         return false;
@@ -1102,6 +1584,84 @@ bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint3
     hipLaunchKernelGGL(k_hd_tail, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tree_child, w.tree_sym,
                        w.table, w.end_pos, d_status);
     BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint32_t* h_encoded_size, uint32_t nblocks, const uint8_t* d_payload,
+                        const uint64_t* d_payload_off, uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s)
+{
+    if (nblocks == 0)
+        return true;
+    if (!w.reserve(nblocks, 1) || !w.reserve_segs(1, nblocks))
+        return false;
+    // segments and WG tasks from the host-side encoded sizes
+    std::vector<uint32_t>& hb = w.h_segb;
+    hb.resize(nblocks + 1);
+    std::vector<Hd2Task> tasks;
+    tasks.reserve(nblocks);
+    uint32_t ns = 0;
+    for (uint32_t b = 0; b < nblocks; ++b)
+    {
+        hb[b]            = ns;
+        const uint32_t n = (uint32_t) div_up((uint64_t) h_encoded_size[b] * 8, HD2_SEG);
+        for (uint32_t j = 0; j < n; j += HD2_TPB)
+            tasks.push_back(Hd2Task{b, j});
+        ns += n;
+    }
+    hb[nblocks] = ns;
+    const uint32_t nt = (uint32_t) tasks.size();
+    if (!w.reserve_fast(nblocks, ns, nt))
+        return false;
+    BRA_HIP_CHECK(hipMemsetAsync(w.flag, 0, 4, s));
+    BRA_HIP_CHECK(hipMemcpyAsync(w.seg_base, hb.data(), (size_t) (nblocks + 1) * 4, hipMemcpyHostToDevice, s));
+    if (nt)
+        BRA_HIP_CHECK(hipMemcpyAsync(w.tasks, tasks.data(), (size_t) nt * sizeof(Hd2Task), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_hd_canon, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_meta, nblocks, w.tab, w.flag);
+    BRA_HIP_CHECK(hipMemcpyAsync(w.h_flag, w.flag, 4, hipMemcpyDeviceToHost, s));
+    BRA_HIP_CHECK(hipStreamSynchronize(s));  // also: the host vectors above were the copies' sources
+    if (*w.h_flag)
+        return huff_decode_tree(w, d_meta, h_encoded_size, nblocks, d_payload, d_payload_off, d_out, d_out_base, d_status, s);
+    const Hd2Task* dt = reinterpret_cast<const Hd2Task*>(w.tasks);
+    if (nt)
+        hipLaunchKernelGGL(k_hd_trans, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
+                           w.seg_base, w.trans);
+    hipLaunchKernelGGL(k_hd_chain, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_meta, nblocks, w.seg_base, w.trans, w.seg_info,
+                       d_status);
+    if (nt)
+        hipLaunchKernelGGL(k_hd_write2, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
+                           w.seg_base, w.trans, w.seg_info, d_status, d_out, d_out_base, w.end_pos);
+    hipLaunchKernelGGL(k_hd_tail2, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tab, w.end_pos,
+                       d_status);
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+bool HuffWorkspace::reserve_fast(uint32_t nblocks, uint32_t nseg, uint32_t ntasks)
+{
+    if (nblocks > cap_fb)
+    {
+        cap_fb           = 0;
+        const uint32_t c = nblocks + 64;
+        if (!dev_alloc(tab, (uint64_t) c * HD2_TAB))
+            return false;
+        cap_fb = c;
+    }
+    if (nseg > cap_fs)
+    {
+        cap_fs           = 0;
+        const uint32_t c = nseg + nseg / 4 + 256;
+        if (!dev_alloc(trans, (uint64_t) c * HD2_STRD) || !dev_alloc(seg_info, c))
+            return false;
+        cap_fs = c;
+    }
+    if (ntasks > cap_ft)
+    {
+        cap_ft           = 0;
+        const uint32_t c = ntasks + ntasks / 4 + 64;
+        if (!dev_alloc_bytes(tasks, (uint64_t) c * sizeof(Hd2Task)))
+            return false;
+        cap_ft = c;
+    }
     return true;
 }
 
