@@ -720,43 +720,149 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restri
 // ------------------------------------------------------------------------------------------------
 // decode
 // ------------------------------------------------------------------------------------------------
-// Pass 1: decode each segment from the identity table; labels -> out, end table -> perm.
-__global__ void __launch_bounds__(TPB) k_mtf_dec_local(const uint8_t* __restrict__ in, uint8_t* __restrict__ lab,
-                                                       const Piece* __restrict__ segs, uint32_t nseg, uint32_t* __restrict__ perm)
+// Pass 1: decode each segment from the identity table (labels -> lab, end table -> perm), with the
+// table front (entries 0..15) in four registers and entries 16..255 in 15 LDS chunks of 16 bytes, chunk-major (tb[k * TPB + t]: the
+// 16-byte accesses of consecutive lanes are conflict-free).  A step at rank r reads its symbol
+// straight from the register or chunk holding position r, then shifts the positions below r up by
+// one, 16 at a time; post-BWT ranks are small, so most steps touch registers only.  Input and
+// labels move 16 bytes at a time, the next 16 input bytes loaded before the current ones decode.
+__device__ __forceinline__ uint4 shift_chunk(const uint4& v, uint32_t& top)
 {
-    extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    uint32_t       o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t ntop = d[q] >> 24;
+        o[q]                = shift1(d[q], top);
+        top                 = ntop;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ uint4 shift_chunk_upto(const uint4& v, uint32_t top, uint32_t rr)
+{
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t k = rr >> 2, b = rr & 3;
+    uint32_t       o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t ntop = d[q] >> 24;
+        o[q]                = ((uint32_t) q < k) ? shift1(d[q], top) : ((uint32_t) q == k) ? shift_upto(d[q], top, b) : d[q];
+        top                 = ntop;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t i)
+{
+    const uint32_t q = i >> 2;
+    const uint32_t d = q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
+    return (d >> (8 * (i & 3))) & 0xFF;
+}
+
+__device__ __forceinline__ uint32_t dec_step(uint32_t (&R)[4], uint4* tb, uint32_t t, uint32_t r)
+{
+    if (r < 16)
+    {
+        const uint32_t k = r >> 2, b = r & 3;
+        const uint32_t c = ((k == 0 ? R[0] : k == 1 ? R[1] : k == 2 ? R[2] : R[3]) >> (8 * b)) & 0xFF;
+        uint32_t       top = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            const uint32_t cur = R[q], ntop = cur >> 24;
+            if ((uint32_t) q < k)
+                R[q] = shift1(cur, top);
+            else if ((uint32_t) q == k)
+                R[q] = shift_upto(cur, top, b);
+            top = ntop;
+        }
+        return c;
+    }
+    const uint32_t ch = r >> 4, rr = r & 15;
+    const uint4    v  = tb[(ch - 1) * TPB + t];
+    const uint32_t c  = byte_of(v, rr);
+    uint32_t       top = c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+    {
+        const uint32_t cur = R[q], ntop = cur >> 24;
+        R[q]                = shift1(cur, top);
+        top                 = ntop;
+    }
+    for (uint32_t k = 1; k < ch; ++k)
+    {
+        const uint4 u            = tb[(k - 1) * TPB + t];
+        tb[(k - 1) * TPB + t]    = shift_chunk(u, top);
+    }
+    tb[(ch - 1) * TPB + t] = shift_chunk_upto(v, top, rr);
+    return c;
+}
+
+__global__ void __launch_bounds__(TPB) k_mtf_dec_local2(const uint8_t* __restrict__ in, uint8_t* __restrict__ lab,
+                                                        const Piece* __restrict__ segs, uint32_t nseg, uint32_t* __restrict__ perm)
+{
+    extern __shared__ __attribute__((aligned(16))) uint4 tb[];  // 15 * TPB chunks
     const uint32_t t = threadIdx.x;
     for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
     {
         const uint32_t s = g0 + t;
-        if (s < nseg)
+        if (s >= nseg)
+            continue;
+        uint32_t R[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            R[q] = (uint32_t) (q * 4) * 0x01010101u + 0x03020100u;
+        for (uint32_t k = 1; k < 16; ++k)
         {
-            for (int w = 0; w < 64; ++w)
-                tbl[w * TPB + t] = (uint32_t) (w * 4) * 0x01010101u + 0x03020100u;
-            const Piece    P   = segs[s];
-            const uint8_t* src = in + P.off;
-            uint8_t*       dst = lab + P.off;
-            for (uint32_t i = 0; i < P.len; ++i)
+            const uint32_t b0 = k * 16;
+            tb[(k - 1) * TPB + t] = make_uint4(b0 * 0x01010101u + 0x03020100u, (b0 + 4) * 0x01010101u + 0x03020100u,
+                                               (b0 + 8) * 0x01010101u + 0x03020100u, (b0 + 12) * 0x01010101u + 0x03020100u);
+        }
+        const Piece    P   = segs[s];
+        const uint8_t* src = in + P.off;
+        uint8_t*       dst = lab + P.off;
+        uint32_t       i   = 0;
+        if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0 && P.len >= 16)
+        {
+            const uint32_t nv  = P.len / 16;
+            uint4          nxt = reinterpret_cast<const uint4*>(src)[0];
+            for (uint32_t v = 0; v < nv; ++v)
             {
-                const uint32_t p   = src[i];
-                const uint32_t w   = p >> 2, b = p & 3;
-                const uint32_t cur = tbl[w * TPB + t];
-                const uint32_t c   = (cur >> (8 * b)) & 0xFF;
-                dst[i]             = (uint8_t) c;
-                const uint32_t below   = w ? tbl[(w - 1) * TPB + t] : c << 24;
-                const uint32_t shifted = (cur << 8) | (below >> 24);
-                const uint32_t keep    = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
-                tbl[w * TPB + t]       = (cur & keep) | (shifted & ~keep);
-                uint32_t hi            = below;
-                for (int x = (int) w - 1; x >= 0; --x)
+                const uint4 cur = nxt;
+                if (v + 1 < nv)
+                    nxt = reinterpret_cast<const uint4*>(src)[v + 1];
+                // 16 ranks shifted out of a 128-bit register pair, labels shifted in (rolled: the steps are serial)
+                uint64_t ilo = ((uint64_t) cur.y << 32) | cur.x, ihi = ((uint64_t) cur.w << 32) | cur.z;
+                uint64_t olo = 0, ohi = 0;
+#pragma unroll 1
+                for (int j = 0; j < 16; ++j)
                 {
-                    const uint32_t lo = x ? tbl[(x - 1) * TPB + t] : c << 24;
-                    tbl[x * TPB + t]  = (hi << 8) | (lo >> 24);
-                    hi                = lo;
+                    const uint32_t c = dec_step(R, tb, t, (uint32_t) ilo & 0xFFu);
+                    ilo              = (ilo >> 8) | (ihi << 56);
+                    ihi >>= 8;
+                    olo = (olo >> 8) | (ohi << 56);
+                    ohi = (ohi >> 8) | ((uint64_t) c << 56);
                 }
+                reinterpret_cast<uint4*>(dst)[v] = make_uint4((uint32_t) olo, (uint32_t) (olo >> 32), (uint32_t) ohi, (uint32_t) (ohi >> 32));
             }
-            for (int w = 0; w < 64; ++w)
-                perm[(size_t) s * 64 + w] = tbl[w * TPB + t];
+            i = nv * 16;
+        }
+        for (; i < P.len; ++i)
+            dst[i] = (uint8_t) dec_step(R, tb, t, src[i]);
+        uint32_t* pm = perm + (size_t) s * 64;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            pm[q] = R[q];
+        for (uint32_t k = 1; k < 16; ++k)
+        {
+            const uint4 u = tb[(k - 1) * TPB + t];
+            pm[k * 4 + 0] = u.x;
+            pm[k * 4 + 1] = u.y;
+            pm[k * 4 + 2] = u.z;
+            pm[k * 4 + 3] = u.w;
         }
     }
 }
@@ -869,14 +975,14 @@ bool mtf_decode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, uin
     if (!w.reserve((size_t) nseg * 256))
         return false;
     uint32_t*    perm = reinterpret_cast<uint32_t*>(w.state);
-    const size_t lds  = 64 * TPB * 4;
+    const size_t lds  = 15 * TPB * 16;
     static bool  attr = false;
     if (!attr)
     {
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local2, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         attr = true;
     }
-    hipLaunchKernelGGL(k_mtf_dec_local, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_tmp,
+    hipLaunchKernelGGL(k_mtf_dec_local2, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_tmp,
                        w.tiling.d_pieces, nseg, perm);
     hipLaunchKernelGGL(k_mtf_dec_compose, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count,
                        nblocks, perm);
