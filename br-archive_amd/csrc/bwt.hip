@@ -264,6 +264,16 @@ __device__ __forceinline__ uint32_t dev_count(const uint32_t* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The call-wide job counts as they stand (the boundary between the two job phases, see run_jobs).
+__global__ void k_job_snap(const Counters* __restrict__ ctr, uint32_t* __restrict__ snap)
+{
+    if (threadIdx.x == 0)
+    {
+        snap[0] = dev_count(&ctr->n_jobs);
+        snap[1] = dev_count(&ctr->n_mjobs);
+    }
+}
+
 // Host mailbox record: a level's counts, written by k_publish into pinned host memory so the host
 // can follow the level loop without a copy or a stream synchronisation.  `seq` is stored last.
 struct Mail
@@ -2136,12 +2146,12 @@ constexpr uint32_t JOB_CHUNK = 4096;  // jobs per workgroup of the ordering kern
 // Per-key job counts.  Each workgroup counts a chunk of the list in LDS and adds its nonzero counts
 // to the global ones (one atomic per key and workgroup instead of one per job: thousands of jobs of
 // one block share a key, and same-address device atomics serialise).  nkeys <= lds capacity.
-__global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q,
-                                                   uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cnt)
+__global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs, const uint32_t* __restrict__ pb, const uint32_t* __restrict__ pn,
+                                                   uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cnt)
 {
     extern __shared__ uint32_t h[];
-    const uint32_t n = dev_count(pn);
-    for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
+    const uint32_t b0 = pb ? dev_count(pb) : 0u, n = dev_count(pn);
+    for (uint32_t c0 = b0 + blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
         for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
             h[k] = 0;
@@ -2159,13 +2169,14 @@ __global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs,
 
 // Scatter into key order: per chunk, local ranks from LDS atomics, one global cursor reservation per
 // nonzero key and workgroup.  (Job order within a key only affects speed.)
-__global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in, const uint32_t* __restrict__ pn, uint32_t kb, uint32_t q,
-                                                     uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cursor, Job* __restrict__ out)
+__global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in, const uint32_t* __restrict__ pb, const uint32_t* __restrict__ pn,
+                                                     uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cursor,
+                                                     Job* __restrict__ out)
 {
     extern __shared__ uint32_t h[];
-    const uint32_t n = dev_count(pn);
+    const uint32_t b0 = pb ? dev_count(pb) : 0u, n = dev_count(pn);
     constexpr int PT = JOB_CHUNK / 256;
-    for (uint32_t c0 = blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
+    for (uint32_t c0 = b0 + blockIdx.x * JOB_CHUNK; c0 < n; c0 += gridDim.x * JOB_CHUNK)
     {
         for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
             h[k] = 0;
@@ -2573,6 +2584,11 @@ struct BwtWorkspace
     int       jobq_on   = 1;            // dynamic job order (env BRA_JOBQ=0: static strides)
     int       tile_order_mode = 1;      // MSD tile order: 0 scan order, 1 XCD-major on re-gather levels, 2 always (env BRA_TILE_ORDER)
     uint32_t  jobq_chunk = 2;           // wave jobs claimed at once (env BRA_JOBQ_CH)
+    hipStream_t s2      = nullptr;      // job stream: the jobs of the first levels run beside the later MSD levels
+    hipEvent_t  ev_a = nullptr, ev_j = nullptr;
+    uint32_t*   snap      = nullptr;    // job counts at the phase boundary (k_job_snap)
+    int         overlap   = 0;          // env BRA_OVERLAP=1: two job phases (measured slower: the levels starve)
+    uint32_t    grid_div_a = 2;         // phase-1 job launches use 1/grid_div_a of the resident capacity (env BRA_JOBS_DIV_A)
     uint32_t  nblocks   = 0;            // blocks of the current call
     uint32_t  levels    = 0;            // MSD levels enqueued by the last STRING level loop
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
@@ -2642,27 +2658,30 @@ static bool post_wait(BwtWorkspace& w, uint32_t slot, hipStream_t s, Mail& out)
 // The workgroup jobs are also split into two size classes (<= half the workgroup-job size, larger):
 // out[0] wave jobs, out[1] small workgroup jobs, out[2] large ones.  The job counts are read on the
 // device (counters slot 0), so the host never waits for them.
-static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[3], hipStream_t s)
+static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[3], hipStream_t s,
+                       const uint32_t* beg = nullptr, const uint32_t* end = nullptr)
 {
     const uint32_t  kb0 = div_up(nblocks, 8), q = div_up(kb0, 1024u);
     const uint32_t  kb = div_up(kb0, q), nk = 8 * kb;  // keys per size class (<= 8192)
     const uint32_t  split[2] = {0, w.mjob_max() / 2};
     const Job*      src[2]   = {w.jobs, w.mjobs};
     Job*            dst[2]   = {w.jobs_sorted, w.mjobs_sorted};
-    const uint32_t* pn[2]    = {&w.ctr[0].n_jobs, &w.ctr[0].n_mjobs};
+    const uint32_t* pn[2]    = {end ? end : &w.ctr[0].n_jobs, end ? end + 1 : &w.ctr[0].n_mjobs};
+    const uint32_t* pb[2]    = {beg, beg ? beg + 1 : nullptr};
     uint32_t*       dcnt     = w.job_cnt;                    // [list][class][nk] counts
     uint32_t*       dcur     = w.job_cnt + 4 * (size_t) nk;  // cursors, same layout
     const dim3      g(1024);
     BRA_HIP_CHECK(hipMemsetAsync(dcnt, 0, 4 * (size_t) nk * 4, s));
     for (int l = 0; l < 2; ++l)
     {
-        hipLaunchKernelGGL(k_job_count, g, dim3(256), 2 * nk * 4, s, src[l], pn[l], kb, q, split[l], 2 * nk, dcnt + (size_t) l * 2 * nk);
+        hipLaunchKernelGGL(k_job_count, g, dim3(256), 2 * nk * 4, s, src[l], pb[l], pn[l], kb, q, split[l], 2 * nk, dcnt + (size_t) l * 2 * nk);
         BRA_DSYNC(s);
     }
     hipLaunchKernelGGL(k_job_prefix, dim3(1), dim3(256), 0, s, dcnt, nk, kb, dcur, w.jseg); BRA_DSYNC(s);
     for (int l = 0; l < 2; ++l)
     {
-        hipLaunchKernelGGL(k_job_scatter, g, dim3(256), 2 * nk * 4, s, src[l], pn[l], kb, q, split[l], 2 * nk, dcur + (size_t) l * 2 * nk, dst[l]);
+        hipLaunchKernelGGL(k_job_scatter, g, dim3(256), 2 * nk * 4, s, src[l], pb[l], pn[l], kb, q, split[l], 2 * nk, dcur + (size_t) l * 2 * nk,
+                           dst[l]);
         BRA_DSYNC(s);
     }
     for (int k = 0; k < 3; ++k)
@@ -2682,10 +2701,10 @@ static uint32_t round8(uint32_t g) { return (g + 7u) & ~7u; }
 static uint32_t g_mjobs_grid = 0;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID; 0 = by size class)
 
 template <uint32_t MODE>
-static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
+static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s, uint32_t div = 1)
 {
     // about the resident capacity: 2-wave jobs fit twice as many groups per CU as 4-wave ones
-    const uint32_t cap = g_mjobs_grid ? g_mjobs_grid : (waves <= 2 ? 3072u : 1536u);
+    const uint32_t cap = (g_mjobs_grid ? g_mjobs_grid : (waves <= 2 ? 3072u : 1536u)) / div;
     const dim3     g(round8(std::min<uint32_t>(n, cap)));
     if (waves == 16)
         hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>) + 16, s, a);
@@ -2721,6 +2740,13 @@ static void ws_free(BwtWorkspace& w)
         (void) hipHostFree(w.h_ctr);
     if (w.h_mail)
         (void) hipHostFree(w.h_mail);
+    (void) hipFree(w.snap);
+    if (w.ev_a)
+        (void) hipEventDestroy(w.ev_a);
+    if (w.ev_j)
+        (void) hipEventDestroy(w.ev_j);
+    if (w.s2)
+        (void) hipStreamDestroy(w.s2);
     w = BwtWorkspace{};
 }
 
@@ -2758,6 +2784,10 @@ static void ws_env(BwtWorkspace& w)
         w.tile_order_mode = atoi(e);
     if (const char* e = getenv("BRA_JOBQ_CH"))
         w.jobq_chunk = (uint32_t) std::max(1, atoi(e));
+    if (const char* e = getenv("BRA_OVERLAP"))
+        w.overlap = atoi(e) != 0;
+    if (const char* e = getenv("BRA_JOBS_DIV_A"))
+        w.grid_div_a = (uint32_t) std::max(1, atoi(e));
 }
 
 static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
@@ -2794,6 +2824,8 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
          dev_alloc(w.jobq, 3 * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
          dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B) &&
          dev_alloc(w.tmask, 8ull * w.cap_l0);
+    ok = ok && dev_alloc(w.snap, 16) && hipStreamCreateWithFlags(&w.s2, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&w.ev_a, hipEventDisableTiming) == hipSuccess && hipEventCreateWithFlags(&w.ev_j, hipEventDisableTiming) == hipSuccess;
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -2814,6 +2846,55 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
 
 static size_t tile_stage_bytes() { return sizeof(TileStage); }
 
+// The STRING jobs of one phase, enqueued on w.s2 behind everything enqueued on s so far: order the
+// jobs appended between the counts at `beg` and `end` (device words; null beg = 0, null end = the
+// call-wide counts) block-major per XCD, then the wave-job and the two workgroup-job launches.
+// Phase 1 takes the jobs of level 0 and level 1 while s goes on with the deeper MSD levels: the
+// job kernels are VALU bound and the levels memory bound, so they share the CUs (phase 1 launches
+// about 1/grid_div_a of the resident capacity, the levels' tiles fill the rest).  Jobs are final
+// when emitted: no later level touches their slots.  Phase 2 takes the rest after the last level.
+struct JobPhase
+{
+    JobArgs  ja, jm;
+    uint32_t nblocks;
+};
+
+static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s, const uint32_t* beg, const uint32_t* end, uint32_t div)
+{
+    hipStream_t s2 = w.s2;
+    BRA_HIP_CHECK(hipEventRecord(w.ev_a, s));
+    BRA_HIP_CHECK(hipStreamWaitEvent(s2, w.ev_a, 0));
+    JobArgs ord[3];
+    if (!order_jobs(w, ph.nblocks, ph.ja, ph.jm, ord, s2, beg, end))
+        return false;
+    if (w.jobq_on)
+    {
+        BRA_HIP_CHECK(hipMemsetAsync(w.jobq, 0, 3 * 8 * 32 * 4, s2));
+        for (int k = 0; k < 3; ++k)
+        {
+            ord[k].jq       = w.jobq + k * 8 * 32;
+            ord[k].jq_chunk = w.jobq_chunk;
+        }
+    }
+    {
+        BRA_PROF(P_BWT_JOBS, s2);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::max<uint32_t>(w.jobs_grid / div, 8))), dim3(256), 0, s2, ord[0]);
+        BRA_DSYNC(s2);
+    }
+    {
+        // workgroup jobs of at most half the size run on half the waves
+        BRA_PROF(P_BWT_MJOBS, s2);
+        const int half = w.mj_waves / 2;
+        if (w.mj_waves)
+        {
+            launch_mjobs<MODE_STRING>(half >= 2 ? half : w.mj_waves, ~0u, ord[1], s2, div);
+            launch_mjobs<MODE_STRING>(w.mj_waves, ~0u, ord[2], s2, div);
+        }
+    }
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
 // MSD levels for the buckets listed in counters slot 1 (w.big[cur], tiles in w.tile_bucket[cur]);
 // the caller has posted slot 1's mailbox record.  Level k (k >= 1) consumes slot k and fills slot
 // k + 1.  Every level's kernels read their counts on the device, so the host only decides when to
@@ -2822,7 +2903,7 @@ static size_t tile_stage_bytes() { return sizeof(TileStage); }
 // Sub-buckets become jobs / fallback groups (appended to the call-wide lists, slot 0).
 template <uint32_t MODE>
 static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, int cur, Group* groups_out, hipStream_t s,
-                       uint32_t first_seq)
+                       uint32_t first_seq, const JobPhase* phase1 = nullptr)
 {
     const size_t   lds    = tile_stage_bytes();
     const int      grid   = w.grid;
@@ -2889,6 +2970,12 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             }
             BRA_HIP_CHECK(hipGetLastError());
             seqs[k + 1] = post(w, k + 1, s);
+            if (phase1 && k == 1)
+            {
+                hipLaunchKernelGGL(k_job_snap, dim3(1), dim3(64), 0, s, w.ctr, w.snap);
+                if (!run_jobs(w, *phase1, s, nullptr, w.snap, w.grid_div_a))
+                    return false;
+            }
             cur ^= 1;
             if (rg)
                 lvl_kd = lvl_d + 1;
@@ -3043,45 +3130,36 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
     prof_bytes(P_BWT_L0SCATTER, 9.0 * N + 1024.0 * nt0);  // window in, payload out
-    // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]
-    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s)))
+    // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]; the jobs of levels
+    // 0 and 1 run on w.s2 beside the deeper levels (run_jobs), the rest after the last level
+    JobPhase ph;
+    ph.ja = JobArgs{w.jobs,  0,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
+                    w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0, w.packed, w.pkd};
+    ph.jm      = ph.ja;
+    ph.jm.jobs = w.mjobs;
+    ph.nblocks = nblocks;
+    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s), w.overlap ? &ph : nullptr))
         return false;
-
-    // ---- jobs (counts and list ranges stay on the device) ----
-    JobArgs ja{w.jobs,  0,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
-               w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0, w.packed, w.pkd};
-    JobArgs jm = ja;
-    jm.jobs    = w.mjobs;
-    JobArgs ord[3];
-    if (!order_jobs(w, nblocks, ja, jm, ord, s))
+    if (!run_jobs(w, ph, s, w.overlap ? w.snap : nullptr, nullptr, 1))
         return false;
-    if (w.jobq_on)
-    {
-        BRA_HIP_CHECK(hipMemsetAsync(w.jobq, 0, 3 * 8 * 32 * 4, s));
-        for (int k = 0; k < 3; ++k)
-        {
-            ord[k].jq       = w.jobq + k * 8 * 32;
-            ord[k].jq_chunk = w.jobq_chunk;
-        }
-    }
-    {
-        BRA_PROF(P_BWT_JOBS, s);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, s, ord[0]);
-        BRA_DSYNC(s);
-    }
-    {
-        // workgroup jobs of at most half the size run on half the waves
-        BRA_PROF(P_BWT_MJOBS, s);
-        const int half = w.mj_waves / 2;
-        if (w.mj_waves)
-        {
-            launch_mjobs<MODE_STRING>(half >= 2 ? half : w.mj_waves, ~0u, ord[1], s);
-            launch_mjobs<MODE_STRING>(w.mj_waves, ~0u, ord[2], s);
-        }
-    }
+    BRA_HIP_CHECK(hipEventRecord(w.ev_j, w.s2));
+    BRA_HIP_CHECK(hipStreamWaitEvent(s, w.ev_j, 0));
     BRA_HIP_CHECK(hipGetLastError());
     if (!account_levels<MODE_STRING>(w, s))
         return false;
+    static const bool level_stats = getenv("BRA_LEVEL_STATS") != nullptr;  // diagnostic: per-level counts to stderr
+    if (level_stats)
+    {
+        const uint32_t ns = std::min<uint32_t>(w.levels + 2, MAX_LEVELS);
+        BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, ns * sizeof(Counters), hipMemcpyDeviceToHost, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));
+        const Counters& c0 = w.h_ctr[0];
+        fprintf(stderr, "[bwt levels] N %llu jobs %u mjobs %u melems %u groups %u\n", (unsigned long long) N, c0.n_jobs, c0.n_mjobs, c0.n_melems,
+                c0.n_groups);
+        for (uint32_t k = 1; k < ns; ++k)
+            fprintf(stderr, "[bwt levels] slot %u: buckets %u tiles %u elems %u moved(into) %u\n", k, w.h_ctr[k].n_big, w.h_ctr[k].n_tiles_next,
+                    w.h_ctr[k].n_elems_next, w.h_ctr[k].n_moved);
+    }
     Mail mc{};
     if (!post_wait(w, 0, s, mc))
         return false;

@@ -5,4 +5,4 @@ for k in ${KINDS:-text random}; do
   timeout -k 10 300 python scripts/decode_bench.py --kind $k >> $O/decode.log 2>&1
 done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tr -o run --output-format csv -- python3 scripts/decode_bench.py --kind text --reps 2 > $O/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/tr -o run --output-format csv -- python3 scripts/decode_bench.py --kind ${PKIND:-text} --reps 2 > $O/trace.log 2>&1
