@@ -314,6 +314,45 @@ __device__ __forceinline__ void cx128_pair(uint32_t& a0, uint32_t& a1, uint32_t&
     b0 = m0, b1 = m1, b2 = m2, b3 = m3;
 }
 
+// 96-bit keys as three dwords (k0 lowest): the same compare-exchange with three subtractions and
+// three selects (the job sort network; a 96-bit key holds 11 rotation bytes after the slot bits).
+__device__ __forceinline__ void cx96(uint32_t& k0, uint32_t& k1, uint32_t& k2, uint32_t o0, uint32_t o1, uint32_t o2, uint64_t keep_min)
+{
+    uint32_t t;
+    asm volatile(
+        "v_sub_co_u32 %[t], vcc, %[o0], %[k0]\n\t"
+        "v_subb_co_u32 %[t], vcc, %[o1], %[k1], vcc\n\t"
+        "v_subb_co_u32 %[t], vcc, %[o2], %[k2], vcc\n\t"
+        "s_xnor_b64 vcc, vcc, %[km]\n\t"
+        "v_cndmask_b32 %[k0], %[k0], %[o0], vcc\n\t"
+        "v_cndmask_b32 %[k1], %[k1], %[o1], vcc\n\t"
+        "v_cndmask_b32 %[k2], %[k2], %[o2], vcc"
+        : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1), [k2] "+v"(k2)
+        : [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2), [km] "s"(keep_min)
+        : "vcc");
+}
+
+__device__ __forceinline__ void cx96_pair(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& b0, uint32_t& b1, uint32_t& b2, uint64_t asc)
+{
+    uint32_t t, n0, n1, n2, m0, m1, m2;
+    asm volatile(
+        "v_sub_co_u32 %[t], vcc, %[b0], %[a0]\n\t"
+        "v_subb_co_u32 %[t], vcc, %[b1], %[a1], vcc\n\t"
+        "v_subb_co_u32 %[t], vcc, %[b2], %[a2], vcc\n\t"
+        "s_xnor_b64 vcc, vcc, %[asc]\n\t"
+        "v_cndmask_b32 %[n0], %[a0], %[b0], vcc\n\t"
+        "v_cndmask_b32 %[m0], %[b0], %[a0], vcc\n\t"
+        "v_cndmask_b32 %[n1], %[a1], %[b1], vcc\n\t"
+        "v_cndmask_b32 %[m1], %[b1], %[a1], vcc\n\t"
+        "v_cndmask_b32 %[n2], %[a2], %[b2], vcc\n\t"
+        "v_cndmask_b32 %[m2], %[b2], %[a2], vcc"
+        : [t] "=&v"(t), [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2)
+        : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [asc] "s"(asc)
+        : "vcc");
+    a0 = n0, a1 = n1, a2 = n2;
+    b0 = m0, b1 = m1, b2 = m2;
+}
+
 template <int LM>
 __device__ __forceinline__ uint64_t xlane64(uint64_t x)
 {

@@ -1471,6 +1471,21 @@ struct JobLds
 };
 
 template <int W>
+struct JobGeom
+{
+    static constexpr int      LOGS  = (W == 1) ? 8 : (W == 2) ? 9 : (W == 4) ? 10 : (W == 8) ? 11 : 12;  // log2(256 * W)
+    static constexpr int      GBITS = LOGS;                                // group id bits (top of kh)
+    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;                  // slot bits (bottom of kl)
+    // key dwords: 96-bit keys for wave jobs (11 rotation bytes in round 1; the cheaper network
+    // outweighs the extra rounds), 128 bits for workgroup jobs (with 96 bits 62 % of them needed a
+    // second round, which cost what the network saved)
+    static constexpr int      KD    = (W == 1) ? 3 : 4;
+    static constexpr uint32_t KBITS = 32 * KD;
+    static constexpr uint32_t ADV   = (KBITS - GBITS - LOGS) / 8;          // whole rotation bytes per key
+    static constexpr uint32_t ADV1  = (KBITS - LOGS) / 8;                  // round 1: no group bits
+};
+
+template <int W>
 __device__ __forceinline__ void job_sync()
 {
     if (W > 1)
@@ -1572,40 +1587,62 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
 
 // One bitonic stage whose partners sit LM lanes away (same element r): exchanged with DPP /
 // permlane swaps.  k[i][r] = dword i of element r's key.
-template <int LM>
-__device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[4][4], uint64_t keep_min)
+// Keys of KD dwords (3: 96 bits, wave jobs; 4: 128 bits, workgroup jobs).
+template <int KD>
+__device__ __forceinline__ void cxk(uint32_t (&k)[KD][4], int r, const uint32_t (&o)[KD], uint64_t keep_min)
+{
+    if constexpr (KD == 3)
+        cx96(k[0][r], k[1][r], k[2][r], o[0], o[1], o[2], keep_min);
+    else
+        cx128(k[0][r], k[1][r], k[2][r], k[3][r], o[0], o[1], o[2], o[3], keep_min);
+}
+
+template <int KD>
+__device__ __forceinline__ void cxk_pair(uint32_t (&a)[KD], uint32_t (&b)[KD], uint64_t asc)
+{
+    if constexpr (KD == 3)
+        cx96_pair(a[0], a[1], a[2], b[0], b[1], b[2], asc);
+    else
+        cx128_pair(a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], asc);
+}
+
+template <int LM, int KD>
+__device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[KD][4], uint64_t keep_min)
 {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        const uint32_t o0 = xlane<LM>(k[0][r]), o1 = xlane<LM>(k[1][r]), o2 = xlane<LM>(k[2][r]), o3 = xlane<LM>(k[3][r]);
-        cx128(k[0][r], k[1][r], k[2][r], k[3][r], o0, o1, o2, o3, keep_min);
+        uint32_t o[KD];
+#pragma unroll
+        for (int i = 0; i < KD; ++i)
+            o[i] = xlane<LM>(k[i][r]);
+        cxk<KD>(k, r, o, keep_min);
     }
 }
 
 // Stage whose partners sit 16 or 32 lanes away (J = 64 or 128 slots): a permlane swap of the
 // registers of elements (0, 1) and of (2, 3) gathers each partner pair into ONE lane (element r0's
 // pair in the lower rows, r1's in the upper rows, the lower slot in the first register), an
-// in-lane compare-exchange orders it, and the same swap puts the elements back: 10 VALU per
-// element instead of 24 with per-dword partner fetches.
-template <int LM>
-__device__ __forceinline__ void net_stage_swap(uint32_t (&k)[4][4], uint64_t asc)
+// in-lane compare-exchange orders it, and the same swap puts the elements back: 7.5 VALU per
+// element instead of 18 with per-dword partner fetches.
+template <int LM, int KD>
+__device__ __forceinline__ void net_stage_swap(uint32_t (&k)[KD][4], uint64_t asc)
 {
 #pragma unroll
     for (int q = 0; q < 4; q += 2)
     {
-        uint32_t a[4], b[4];
+        uint32_t a[KD], b[KD];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < KD; ++i)
         {
             const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(k[i][q], k[i][q + 1], false, false)
                                       : __builtin_amdgcn_permlane32_swap(k[i][q], k[i][q + 1], false, false);
             a[i] = t[0];
             b[i] = t[1];
         }
-        cx128_pair(a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], asc);
+        cxk_pair<KD>(a, b, asc);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < KD; ++i)
         {
             const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(a[i], b[i], false, false)
                                       : __builtin_amdgcn_permlane32_swap(a[i], b[i], false, false);
@@ -1619,8 +1656,8 @@ __device__ __forceinline__ void net_stage_swap(uint32_t (&k)[4][4], uint64_t asc
 // stage parameters are compile-time, so a phase is straight-line code with the keys in fixed
 // registers (a runtime stage loop made the compiler copy every key between register sets at each
 // stage join).
-template <int W, int SIZE, int J>
-__device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uint32_t e0)
+template <int W, int KD, int SIZE, int J>
+__device__ __forceinline__ void net_stage(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0)
 {
     if constexpr (J >= 256)
     {
@@ -1629,14 +1666,19 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uin
         job_sync<W>();
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], k[3][r]);
+            X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], KD == 4 ? k[KD - 1][r] : 0u);
         job_sync<W>();
         const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            const uint4 o = X[(e0 + r) ^ J];
-            cx128(k[0][r], k[1][r], k[2][r], k[3][r], o.x, o.y, o.z, o.w, keep_min);
+            const uint4    o4 = X[(e0 + r) ^ J];
+            const uint32_t ow[4] = {o4.x, o4.y, o4.z, o4.w};
+            uint32_t       o[KD];
+#pragma unroll
+            for (int i = 0; i < KD; ++i)
+                o[i] = ow[i];
+            cxk<KD>(k, r, o, keep_min);
         }
         if constexpr (J == 256)
         {
@@ -1644,19 +1686,21 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uin
             uint32_t a = ~0u;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                a &= k[0][r] & k[1][r] & k[2][r] & k[3][r];
+#pragma unroll
+                for (int i = 0; i < KD; ++i)
+                    a &= k[i][r];
             if (__builtin_amdgcn_ballot_w64(a != ~0u) == 0)
                 return;
         }
     }
 #ifndef BRA_NO_SWAP_STAGES
     else if constexpr (J == 64 || J == 128)
-        net_stage_swap<J / 4>(k, __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0));
+        net_stage_swap<J / 4, KD>(k, __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0));
 #endif
     else if constexpr (J >= 4)
     {
         const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
-        net_stage_lanes<J / 4>(k, keep_min);
+        net_stage_lanes<J / 4, KD>(k, keep_min);
     }
     else
     {
@@ -1668,19 +1712,32 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[4][4], JobLds<W>& S, uin
             if (q > r)
             {
                 const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & SIZE) == 0);
-                cx128_pair(k[0][r], k[1][r], k[2][r], k[3][r], k[0][q], k[1][q], k[2][q], k[3][q], asc);
+                uint32_t a[KD], b[KD];
+#pragma unroll
+                for (int i = 0; i < KD; ++i)
+                {
+                    a[i] = k[i][r];
+                    b[i] = k[i][q];
+                }
+                cxk_pair<KD>(a, b, asc);
+#pragma unroll
+                for (int i = 0; i < KD; ++i)
+                {
+                    k[i][r] = a[i];
+                    k[i][q] = b[i];
+                }
             }
         }
     }
     if constexpr (J > 1)
-        net_stage<W, SIZE, J / 2>(k, S, e0);
+        net_stage<W, KD, SIZE, J / 2>(k, S, e0);
 }
 
-template <int W, int SIZE>
-__device__ __forceinline__ void net_phase(uint32_t (&k)[4][4], JobLds<W>& S, uint32_t e0)
+template <int W, int KD, int SIZE>
+__device__ __forceinline__ void net_phase(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0)
 {
     if constexpr (SIZE <= 256 * W)
-        net_stage<W, SIZE, SIZE / 2>(k, S, e0);
+        net_stage<W, KD, SIZE, SIZE / 2>(k, S, e0);
 }
 
 // Bitonic sort of the job's 256*W slots (4 consecutive per lane, slot e = wj*256 + lane*4 + r)
@@ -1690,16 +1747,18 @@ __device__ __forceinline__ void net_phase(uint32_t (&k)[4][4], JobLds<W>& S, uin
 template <int W>
 __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], int P, JobLds<W>& S, int wj)
 {
+    constexpr int  KD   = JobGeom<W>::KD;
     const int      lane = lane_id();
     const uint32_t e0   = wj * 256 + lane * 4;
-    uint32_t       k[4][4];
+    uint32_t       k[KD][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         k[0][r] = (uint32_t) kl[r];
-        k[1][r] = (uint32_t) (kl[r] >> 32);
-        k[2][r] = (uint32_t) kh[r];
-        k[3][r] = (uint32_t) (kh[r] >> 32);
+        if constexpr (KD == 4)
+            k[1][r] = (uint32_t) (kl[r] >> 32);
+        k[KD - 2][r] = (uint32_t) kh[r];
+        k[KD - 1][r] = (uint32_t) (kh[r] >> 32);
     }
     // A wave whose slots all hold padding keys (all ones) skips the phases that stay inside the
     // wave (SIZE <= 256: no barriers, no data from other waves); any order of equal keys is
@@ -1711,7 +1770,9 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
         uint32_t a = ~0u;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            a &= k[0][r] & k[1][r] & k[2][r] & k[3][r];
+#pragma unroll
+            for (int i = 0; i < KD; ++i)
+                a &= k[i][r];
         dead = __builtin_amdgcn_ballot_w64(a != ~0u) == 0;
     }
     for (int size = 2; size <= P; size <<= 1)
@@ -1720,25 +1781,25 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
             continue;
         switch (size)
         {
-        case 2: net_phase<W, 2>(k, S, e0); break;
-        case 4: net_phase<W, 4>(k, S, e0); break;
-        case 8: net_phase<W, 8>(k, S, e0); break;
-        case 16: net_phase<W, 16>(k, S, e0); break;
-        case 32: net_phase<W, 32>(k, S, e0); break;
-        case 64: net_phase<W, 64>(k, S, e0); break;
-        case 128: net_phase<W, 128>(k, S, e0); break;
-        case 256: net_phase<W, 256>(k, S, e0); break;
-        case 512: net_phase<W, 512>(k, S, e0); break;
-        case 1024: net_phase<W, 1024>(k, S, e0); break;
-        case 2048: net_phase<W, 2048>(k, S, e0); break;
-        default: net_phase<W, 4096>(k, S, e0); break;
+        case 2: net_phase<W, KD, 2>(k, S, e0); break;
+        case 4: net_phase<W, KD, 4>(k, S, e0); break;
+        case 8: net_phase<W, KD, 8>(k, S, e0); break;
+        case 16: net_phase<W, KD, 16>(k, S, e0); break;
+        case 32: net_phase<W, KD, 32>(k, S, e0); break;
+        case 64: net_phase<W, KD, 64>(k, S, e0); break;
+        case 128: net_phase<W, KD, 128>(k, S, e0); break;
+        case 256: net_phase<W, KD, 256>(k, S, e0); break;
+        case 512: net_phase<W, KD, 512>(k, S, e0); break;
+        case 1024: net_phase<W, KD, 1024>(k, S, e0); break;
+        case 2048: net_phase<W, KD, 2048>(k, S, e0); break;
+        default: net_phase<W, KD, 4096>(k, S, e0); break;
         }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        kl[r] = ((uint64_t) k[1][r] << 32) | k[0][r];
-        kh[r] = ((uint64_t) k[3][r] << 32) | k[2][r];
+        kl[r] = (KD == 4) ? (((uint64_t) k[1][r] << 32) | k[0][r]) : (uint64_t) k[0][r];
+        kh[r] = ((uint64_t) k[KD - 1][r] << 32) | k[KD - 2][r];
     }
     job_sync<W>();
 }
@@ -1807,31 +1868,24 @@ __device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64
     return job_any<W>(any);
 }
 
-template <int W>
-struct JobGeom
-{
-    static constexpr int      LOGS  = (W == 1) ? 8 : (W == 2) ? 9 : (W == 4) ? 10 : (W == 8) ? 11 : 12;  // log2(256 * W)
-    static constexpr int      GBITS = LOGS;                                // group id bits (top of kh)
-    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;                  // slot bits (bottom of kl)
-    static constexpr uint32_t ADV   = (128 - GBITS - LOGS) / 8;            // whole rotation bytes per key
-    static constexpr uint32_t ADV1  = (128 - LOGS) / 8;                    // round 1: no group bits
-};
 
-// round-1 key: the rotation's 16 bytes from depth d-1, low LOGS bits = slot
+// round-1 key: the rotation's 12 bytes from depth d-1, low LOGS bits = slot
 template <int W>
 __device__ __forceinline__ void make_key1(uint32_t slot, uint64_t w0, uint64_t w1, uint64_t& kh, uint64_t& kl)
 {
-    kh = w0;
-    kl = (w1 & ~JobGeom<W>::SMASK) | slot;
+    using G = JobGeom<W>;
+    kh      = w0;
+    kl      = ((G::KD == 3 ? (w1 >> 32) : w1) & ~G::SMASK) | slot;
 }
 
-// key = group | the rotation's 16 bytes (w0:w1) shifted right by GBITS, low LOGS bits = slot
+// key = group | the rotation's bytes (w0:w1) shifted right by GBITS, low LOGS bits = slot
 template <int W>
 __device__ __forceinline__ void make_key(uint32_t grp, uint32_t slot, uint64_t w0, uint64_t w1, uint64_t& kh, uint64_t& kl)
 {
-    using G = JobGeom<W>;
-    kh      = ((uint64_t) grp << (64 - G::GBITS)) | (w0 >> G::GBITS);
-    kl      = (((w0 << (64 - G::GBITS)) | (w1 >> G::GBITS)) & ~G::SMASK) | slot;
+    using G          = JobGeom<W>;
+    kh               = ((uint64_t) grp << (64 - G::GBITS)) | (w0 >> G::GBITS);
+    const uint64_t l = (w0 << (64 - G::GBITS)) | (w1 >> G::GBITS);
+    kl               = ((G::KD == 3 ? (l >> 32) : l) & ~G::SMASK) | slot;
 }
 
 #ifdef BRA_PHASES
@@ -1888,7 +1942,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         const uint32_t c = wj * 256 + lane * 4 + r;
         pos[r]           = c;
         v[r]             = 0;
-        kh[r] = kl[r] = ~0ull;
+        kh[r] = ~0ull;
+        kl[r] = (G::KD == 3) ? 0xFFFFFFFFull : ~0ull;
         if (c < T)
         {
             // STRING payloads are the 64-bit MSD payloads in the key buffers (index in the low bits)
@@ -2040,7 +2095,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             else
             {
                 pos[r] = c;
-                kh[r] = kl[r] = ~0ull;
+                kh[r]  = ~0ull;
+                kl[r]  = (G::KD == 3) ? 0xFFFFFFFFull : ~0ull;
             }
         }
         job_sync<W>();
