@@ -914,7 +914,7 @@ __global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks
 //                4-dword register window): for every possible entry bit offset e < lmax (the true
 //                path enters the segment within lmax bits of its start) the exit offset past the
 //                segment end, the symbol count and whether the path dies (dead edge / out of data).
-//                The path from e = 0 records its codeword boundaries over the first 256 bits; a
+//                The path from e = 0 records its codeword boundaries over the first 512 bits; a
 //                path from e > 0 that lands on one of them has merged and takes its count from
 //                the boundary's rank -- Huffman paths resynchronise within a few codewords, while
 //                codes of near-equal lengths (uniform data) keep separate phases and are walked out.
@@ -930,7 +930,10 @@ __global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks
 constexpr uint32_t HD2_SEG   = 2048;  // bits per segment
 constexpr uint32_t HD2_LMAX  = 30;
 constexpr uint32_t HD2_TPB   = 256;
-constexpr uint32_t HD2_REFB  = 256;   // boundary bitmap of the reference path (bits from the segment start)
+#ifndef HD2_REFB_BITS
+#define HD2_REFB_BITS 512  // 64 / 128 / 256 / 512 / 1024: text decode 14.9 / 16.3 / 17.9 / 19.5 / 18.5 GB/s (registers)
+#endif
+constexpr uint32_t HD2_REFB  = HD2_REFB_BITS;  // boundary bitmap of the reference path (bits from the segment start)
 constexpr uint32_t HD2_STRD  = 32;    // transfer words per segment
 constexpr uint32_t HD2_TAB   = 2304;  // u32 words per block table
 
