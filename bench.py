@@ -192,14 +192,15 @@ def main():
                 result["crc"] = dmod.merge_crc(parts)
 
     # ---- find the dominant kernel (one untimed, fully profiled pass) ----
-    kernel_slots = [s for s in codec.SLOTS if not s.startswith("stage.")]
-    codec.prof_enable(codec.slot_mask(*codec.SLOTS))
+    kernel_slots = [s for s in codec.SLOTS if not s.startswith(("stage.", "dec."))]
+    enc_slots = [s for s in codec.SLOTS if not s.startswith("dec.")]
+    codec.prof_enable(codec.slot_mask(*enc_slots))
     step()
     torch.cuda.synchronize()
     prof0 = codec.prof_read()
     dominant = max(kernel_slots, key=lambda s: prof0[s][0])
     stage_slots = [s for s in codec.SLOTS if s.startswith("stage.")]
-    timed_slots = codec.SLOTS if args.profile_all else (dominant, *stage_slots)
+    timed_slots = enc_slots if args.profile_all else (dominant, *stage_slots)
     codec.prof_enable(codec.slot_mask(*timed_slots))
 
     for _ in range(args.warmup):
@@ -256,6 +257,24 @@ def main():
                     codec.decode(H, O, P, global_total, bs, out=out)
                 torch.cuda.synchronize()
                 secondary["decode_GBps"] = round(3 * global_total / (time.perf_counter() - t1) / 1e9, 4)
+                # decode roofline: stage times and the largest decode kernel, from one more decode
+                # with every decode slot timed (HIP events on the decode's stream)
+                dec_slots = [s for s in codec.SLOTS if s.startswith("dec.")]
+                codec.prof_enable(codec.slot_mask(*dec_slots))
+                codec.prof_reset()
+                codec.decode(H, O, P, global_total, bs, out=out)
+                torch.cuda.synchronize()
+                dp = codec.prof_read()
+                codec.prof_enable(0)
+                dk = max(codec.DECODE_KERNELS, key=lambda s: dp[s][0])
+                dms = dp[dk][0] / max(1, dp[dk][1])
+                dach = dp[dk][2] / max(1, dp[dk][1]) / (dms / 1e3) / 1e9 if dms > 0 else 0.0
+                secondary["decode_stage_ms"] = {s.split(".")[1]: round(dp[s][0], 3) for s in ("dec.huffman", "dec.rle", "dec.mtf", "dec.ibwt")}
+                secondary["decode_roofline"] = {
+                    "bound": "hbm", "kernel": dk, "achieved": round(dach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(dach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(dms, 4),
+                    "algorithmic_bytes_per_launch": int(dp[dk][2] / max(1, dp[dk][1])),
+                    "kernels_ms": {s: round(dp[s][0] / max(1, dp[s][1]), 4) for s in codec.DECODE_KERNELS}}
             del out
         if not args.no_secondary and world == 1 and len(batches) == 1:
             # PCIe-inclusive encode: pinned host input -> HBM, encode, headers + payload back to pinned host

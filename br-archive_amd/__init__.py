@@ -483,7 +483,10 @@ class BlockCodec:
              "mtf.lastocc", "mtf.scan", "mtf.encode",
              "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
              "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",
-             "chunks.frame", "chunks.crc")
+             "chunks.frame", "chunks.crc",
+             "dec.huffman", "dec.rle", "dec.mtf", "dec.ibwt",
+             "dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk")
+    DECODE_KERNELS = ("dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk")
 
     @classmethod
     def slot_mask(cls, *names) -> int:

@@ -48,7 +48,9 @@ const char* prof_name(int slot)
         "mtf.lastocc", "mtf.scan", "mtf.encode",
         "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
         "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",
-        "chunks.frame", "chunks.crc"};
+        "chunks.frame", "chunks.crc",
+        "dec.huffman", "dec.rle", "dec.mtf", "dec.ibwt",
+        "dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk"};
     return (slot >= 0 && slot < P_NSLOT) ? names[slot] : "";
 }
 
@@ -403,11 +405,25 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
     std::vector<uint32_t> esz(nb);
     for (uint32_t b = 0; b < nb; ++b)
         esz[b] = hh[b].huffman.encoded_size;
-    if (!huff_decode_device(c->huf, c->d_meta, esz.data(), nb, d_payload, d_payload_off, c->d_rle, d_rbase, c->d_status, s))
-        return -1;
+    {
+        BRA_PROF(P_DEC_HUF, s);
+        if (!huff_decode_device(c->huf, c->d_meta, esz.data(), nb, d_payload, d_payload_off, c->d_rle, d_rbase, c->d_status, s))
+            return -1;
+    }
     uint32_t* d_dec_size = c->d_hist;           // nb words
-    if (!rle_decode_device(c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, s))
-        return -1;
+    {
+        BRA_PROF(P_DEC_RLE, s);
+        if (!rle_decode_device(c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, s))
+            return -1;
+    }
+    if (g_prof)
+    {
+        // algorithmic bytes of the RLE decode: reads r, writes n
+        uint64_t r = 0;
+        for (uint32_t b = 0; b < nb; ++b)
+            r += rsz[b];
+        prof_bytes(P_DEC_RLED, (double) r + (double) N);
+    }
     std::vector<uint32_t> st(nb), dsz(nb);
     if (hipMemcpyAsync(st.data(), c->d_status, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(dsz.data(), d_dec_size, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
@@ -427,9 +443,16 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
     }
     if (!flex)
     {
-        if (!mtf_decode_device(c->mtf, c->d_mtf, c->d_L, c->d_tmp, hb.data(), nb, s) ||
-            !ibwt_device(c->ib, c->d_L, c->d_pi, c->d_blocks, hb.data(), nb, d_out, s))
-            return -1;
+        {
+            BRA_PROF(P_DEC_MTF, s);
+            if (!mtf_decode_device(c->mtf, c->d_mtf, c->d_L, c->d_tmp, hb.data(), nb, s))
+                return -1;
+        }
+        {
+            BRA_PROF(P_DEC_IBWT, s);
+            if (!ibwt_device(c->ib, c->d_L, c->d_pi, c->d_blocks, hb.data(), nb, d_out, s))
+                return -1;
+        }
         return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
     }
     // chunk stream: the decoded sizes define the geometry
@@ -544,7 +567,10 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_heade
     if (!dg.ok)
         return -1;
     hipStream_t s = stream ? (hipStream_t) stream : c->stream;
-    return decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
+    g_prof       = c->prof.mask ? &c->prof : nullptr;
+    const int rc = decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
+    g_prof       = nullptr;
+    return rc;
 }
 
 int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t prev, uint32_t* d_crc, void* stream)

@@ -1626,8 +1626,18 @@ bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint3
         return huff_decode_tree(w, d_meta, h_encoded_size, nblocks, d_payload, d_payload_off, d_out, d_out_base, d_status, s);
     const Hd2Task* dt = reinterpret_cast<const Hd2Task*>(w.tasks);
     if (nt)
+    {
+        BRA_PROF(P_DEC_HD_TRANS, s);
+        if (g_prof)
+        {
+            double hb = 0;  // algorithmic bytes: the payload, read once
+            for (uint32_t b = 0; b < nblocks; ++b)
+                hb += h_encoded_size[b];
+            prof_bytes(P_DEC_HD_TRANS, hb);
+        }
         hipLaunchKernelGGL(k_hd_trans, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
                            w.seg_base, w.trans);
+    }
     hipLaunchKernelGGL(k_hd_chain, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_meta, nblocks, w.seg_base, w.trans, w.seg_info,
                        d_status);
     if (nt)

@@ -21,6 +21,7 @@
 // blocks of >= 2^24 bytes, for callers that want the transform itself, and as the fallback when
 // the overflow pool runs out.
 #include "ibwt.h"
+#include "prof.h"
 
 #include <cstring>
 
@@ -773,7 +774,17 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
     BRA_HIP_CHECK(hipMemsetAsync(w.ctl + 300, 0, 4, s));
     hipLaunchKernelGGL(k_ib_scatter2, dim3(std::min<uint32_t>(nt, 16384)), dim3(64), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks, w.T);
     WalkArgs a{blk, d_pi, w.cum, w.ctl + 256, w.ctl, w.T, w.slot, w.pool, w.ctl + 300, w.pool_cap, w.ovl_next, w.m_next, w.m_len, w.m_ovf};
-    hipLaunchKernelGGL(k_ib_walk3, dim3(2048), dim3(256), 0, s, a);
+    {
+        BRA_PROF(P_DEC_IB_WALK, s);
+        if (g_prof)
+        {
+            double n = 0;  // algorithmic bytes: one 4-byte TL entry read and one output byte per element
+            for (uint32_t b = 0; b < nblocks; ++b)
+                n += h_blocks[b].len;
+            prof_bytes(P_DEC_IB_WALK, 5.0 * n);
+        }
+        hipLaunchKernelGGL(k_ib_walk3, dim3(2048), dim3(256), 0, s, a);
+    }
     hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
                        w.m_len, w.m_start, w.cyc);
     hipLaunchKernelGGL(k_ib_copy3, dim3(256, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, blk, w.cum, nblocks, w.m_start, w.m_len,

@@ -1041,8 +1041,18 @@ bool mtf_decode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, uin
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_dec_local2, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         attr = true;
     }
-    hipLaunchKernelGGL(k_mtf_dec_local2, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_tmp,
-                       w.tiling.d_pieces, nseg, perm);
+    {
+        BRA_PROF(P_DEC_MTF_LOCAL, s);
+        if (g_prof)
+        {
+            double n = 0;  // algorithmic bytes: ranks read, labels written
+            for (uint32_t b = 0; b < nblocks; ++b)
+                n += h_blocks[b].len;
+            prof_bytes(P_DEC_MTF_LOCAL, 2.0 * n);
+        }
+        hipLaunchKernelGGL(k_mtf_dec_local2, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_tmp,
+                           w.tiling.d_pieces, nseg, perm);
+    }
     hipLaunchKernelGGL(k_mtf_dec_compose, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count,
                        nblocks, perm);
     hipLaunchKernelGGL(k_mtf_dec_relabel, dim3(std::min<uint32_t>(nseg, 16384)), dim3(TPB), 0, s, d_tmp, d_out, w.tiling.d_pieces, nseg,

@@ -18,6 +18,8 @@ enum ProfSlot : int
     P_RLE_RUNS, P_RLE_LINK, P_RLE_SIZES, P_RLE_OFFSETS, P_RLE_WRITE,
     P_HUF_BUILD, P_HUF_OFFSETS, P_HUF_TILEBITS, P_HUF_TILESCAN, P_HUF_ZERO, P_HUF_PACK,
     P_FRAME, P_CRC,
+    P_DEC_HUF, P_DEC_RLE, P_DEC_MTF, P_DEC_IBWT,       // decode stages
+    P_DEC_HD_TRANS, P_DEC_RLED, P_DEC_MTF_LOCAL, P_DEC_IB_WALK,  // their largest kernels
     P_NSLOT
 };
 

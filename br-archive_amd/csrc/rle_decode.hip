@@ -17,6 +17,7 @@
 //      with their output offsets, and writes its output range: each lane finds the control of its
 //      16 output bytes (binary search + forward steps) and takes them from the staged window.
 // Everything stays in LDS; the next window's bytes are loaded while the current one is decoded.
+#include "prof.h"
 #include "rle.h"
 
 namespace bra {
@@ -295,6 +296,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
 bool rle_decode_device(const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
                        const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, hipStream_t s)
 {
+    BRA_PROF(P_DEC_RLED, s);
     hipLaunchKernelGGL(k_rled, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks, d_out,
                        d_out_base, d_out_cap, d_out_size);
     BRA_HIP_CHECK(hipGetLastError());
