@@ -694,14 +694,10 @@ struct ScanArgs
     const PackDesc* pk;        // STRING: packed key strings per block
 };
 
-constexpr uint32_t SMALL_MAX = JOB_MAX / 2;  // sub-buckets packed together into one wave job
-
-
 // One wave per bucket (SCAN_WAVES buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
-// per tile; the sub-buckets become wave jobs (<= JOB_MAX; consecutive ones of <= SMALL_MAX share
-// a job: digits of one run between larger sub-buckets are grouped by floor(prefix / SMALL_MAX),
-// so every job holds < JOB_MAX elements), workgroup jobs (<= mjob_max), next-level buckets (with
-// their tiles) or fallback groups.  The four waves' list slots are reserved with one atomic per
+// per tile; the sub-buckets become wave jobs (consecutive sub-buckets of <= JOB_MAX elements packed
+// greedily, <= JOB_MAX per job), workgroup jobs (<= mjob_max), next-level buckets (with their
+// tiles) or fallback groups.  The four waves' list slots are reserved with one atomic per
 // list per workgroup (jobs and workgroup jobs share a 64-bit atomic, so do buckets and tiles).
 #ifndef BRA_SCAN_WAVES
 #define BRA_SCAN_WAVES 4   // 16 and 8 measured slower (waves of one workgroup wait for its largest bucket)
@@ -721,6 +717,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
 {
     __shared__ uint32_t       key_s[SCAN_WAVES][256];
     __shared__ uint32_t       jlen_s[SCAN_WAVES][256];
+    __shared__ uint8_t        nx_s[SCAN_WAVES][256];
     __shared__ ScanWaveCounts cnt_s[SCAN_WAVES];
     __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
     const int                 lane = lane_id(), w = threadIdx.x >> 6;
@@ -811,58 +808,98 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
         if (active && lane == 0)
             a.nomove[bi] = nomove ? (nm_next ? 2 : 1) : 0;
-        bool big[4], med[4], mid[4], small[4], fin[4], nbn[4];
-        uint32_t xs[4], xb[4], xp[4];
+        bool big[4], med[4], fin[4], nbn[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            big[r]   = tot[r] > a.mjob_max;
-            med[r]   = tot[r] > JOB_MAX && !big[r];
-            mid[r]   = tot[r] > SMALL_MAX && tot[r] <= JOB_MAX;
-            small[r] = tot[r] > 0 && tot[r] <= SMALL_MAX;
-            fin[r]   = big[r] && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
-            nbn[r]   = big[r] && !fin[r];
-            xs[r]    = small[r] ? tot[r] : 0;
-            xb[r]    = (big[r] || med[r] || mid[r]) ? 1u : 0u;
-            xp[r]    = small[r] ? (uint32_t) (lane * 4 + r + 1) : 0u;
+            big[r] = tot[r] > a.mjob_max;
+            med[r] = tot[r] > JOB_MAX && !big[r];
+            fin[r] = big[r] && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
+            nbn[r] = big[r] && !fin[r];
         }
-        // ---- wave jobs: runs of small sub-buckets between larger ones, chopped by SMALL_MAX ----
-        uint32_t S[4], R0[4], runid[4], prevs[4], tmp4[4];
-        wave_excl_sum4(xs, S);
+        // ---- wave jobs: greedy packing of consecutive sub-buckets of <= JOB_MAX elements ----
+        // The non-empty sub-buckets form a list in digit order; a wave-job sub-bucket weighs its
+        // size, a larger one JOB_MAX + 1 (it never shares a job).  A job starting at entry i takes
+        // entries i .. next(i) - 1, next(i) = the first entry whose end weight exceeds the start
+        // weight + JOB_MAX (binary search on the weight prefix); the jobs are the chain from entry 0
+        // (one lane follows it: one step per job).  Greedy packing fills wave jobs to ~175 elements
+        // on text instead of ~124 with fixed windows of JOB_MAX / 2: 29 % fewer jobs, 21 % fewer
+        // network stages.
+        uint32_t* const Ew = key_s[w];   // end weight of each list entry
+        uint32_t* const Sw = jlen_s[w];  // first slot (bucket-relative) of each list entry
+        uint32_t        li[4], wt[4], wx[4], nlist;
+        {
+            uint32_t ne[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                ne[r] = tot[r] ? 1u : 0u;
+                wt[r] = tot[r] == 0 ? 0u : (tot[r] <= JOB_MAX ? tot[r] : JOB_MAX + 1u);
+            }
+            wave_excl_sum4(ne, li, &nlist);
+            wave_excl_sum4(wt, wx);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-            tmp4[r] = xb[r] ? S[r] : 0;
-        wave_excl_max4(tmp4, R0);
-        wave_excl_sum4(xb, runid);
-        wave_excl_max4(xp, prevs);
-        uint32_t key[4];
+            if (tot[r])
+            {
+                Ew[li[r]] = wx[r] + wt[r];
+                Sw[li[r]] = base[r];
+                nx_s[w][li[r]] = 0;
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t nxt[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            key[r]                    = (runid[r] << 20) | ((S[r] - R0[r]) / SMALL_MAX);
-            key_s[w][lane * 4 + r]  = key[r];
-            jlen_s[w][lane * 4 + r] = 0;
+            nxt[r] = li[r] + 1;
+            if (tot[r] && tot[r] <= JOB_MAX)
+            {
+                const uint32_t lim = wx[r] + JOB_MAX;
+                uint32_t       lo = li[r] + 1, hi = nlist;  // first entry in [lo, hi) with Ew > lim
+                while (lo < hi)
+                {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (Ew[m] > lim)
+                        hi = m;
+                    else
+                        lo = m + 1;
+                }
+                nxt[r] = lo;
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (tot[r])
+                Ew[li[r]] = nxt[r];  // the end weights are no longer needed: next(i) replaces them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0)
+            for (uint32_t c = 0; c < nlist; c = Ew[c])
+                nx_s[w][c] = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         bool     jstart[4];
-        uint32_t js[4], jex[4], jtot;
+        uint32_t js[4], jex[4], jtot, jlen[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            jstart[r] = mid[r] || (small[r] && (prevs[r] == 0 || key_s[w][prevs[r] - 1] != key[r]));
+            jstart[r] = tot[r] && tot[r] <= JOB_MAX && nx_s[w][li[r]];
             js[r]     = jstart[r] ? 1u : 0u;
+            jlen[r]   = jstart[r] ? (nxt[r] < nlist ? Sw[nxt[r]] : B.len) - base[r] : 0u;
         }
         wave_excl_sum4(js, jex, &jtot);
         uint32_t jidx[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-        {
-            jidx[r] = jex[r] + js[r] - 1u;
-            if (small[r] || mid[r])
-                atomicAdd(&jlen_s[w][jidx[r]], tot[r]);
-        }
+            jidx[r] = jex[r];
         // ---- workgroup jobs, next-level buckets, fallback groups ----
         uint32_t cm[4], cb[4], ct[4], cg[4], mex[4], bex[4], tex[4], gex[4], ntl[4];
         uint32_t melems = 0, enext = 0, gmem = 0, gmin = 0xFFFFFFFFu;
@@ -972,7 +1009,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
                 {
                     const uint32_t slot = base_s[w][0] + jidx[r];
                     if (slot < a.cap_jobs)
-                        a.jobs[slot] = Job{s0, jlen_s[w][jidx[r]], kd, obuf, B.block, B.gdepth, nd};
+                        a.jobs[slot] = Job{s0, jlen[r], kd, obuf, B.block, B.gdepth, nd};
                     else
                         atomicExch(&a.ctr->overflow, 1u);
                 }
