@@ -75,8 +75,11 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 // min waves per SIMD the job kernels are compiled for (wave jobs: 6, i.e. <= 80 VGPRs, 8 bytes of
 // spill, faster than the compiler's 84 VGPRs at 5; workgroup jobs: compiler choice, 5 -- forcing 6
 // spilled and measured no faster)
+#ifndef BRA_MJ_MERGE
+#define BRA_MJ_MERGE 1  // workgroup jobs: per-wave sorts + merge-path levels (0: bitonic phases through LDS)
+#endif
 #ifndef MJOB_MIN_WAVES
-#define MJOB_MIN_WAVES 1
+#define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
 #endif
 #ifndef JOB_MIN_WAVES
 #define JOB_MIN_WAVES 6
@@ -1777,8 +1780,68 @@ __device__ __forceinline__ void net_phase(uint32_t (&k)[KD][4], JobLds<W>& S, ui
         net_stage<W, KD, SIZE, SIZE / 2>(k, S, e0);
 }
 
+// 128-bit keys as uint4 (x lowest): a <= b
+__device__ __forceinline__ bool key_le(const uint4& a, const uint4& b)
+{
+    const uint64_t ah = ((uint64_t) a.w << 32) | a.z, bh = ((uint64_t) b.w << 32) | b.z;
+    const uint64_t al = ((uint64_t) a.y << 32) | a.x, bl = ((uint64_t) b.y << 32) | b.x;
+    return ah < bh || (ah == bh && al <= bl);
+}
+
+// One merge level of a workgroup job's sort: sorted runs of m slots (in LDS) merged pairwise into
+// runs of 2m.  Merge path: the lane owning output slots [e0, e0 + 4) finds how many of them come
+// from the left run with one binary search (co-rank), then merges its 4 outputs sequentially --
+// about 40 VALU per element and level instead of the ~230 of the bitonic phases it replaces
+// (log2(2m) compare-exchange stages, cross-wave ones through LDS with two barriers each).  Equal
+// keys (padding) take the left run first.
+template <int W, int KD>
+__device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0, uint32_t m)
+{
+    static_assert(KD == 4, "workgroup jobs sort 128-bit keys");
+    uint4* X = reinterpret_cast<uint4*>(S.kh);  // S.kh and S.kl back to back: 256*W 16-byte words
+    job_sync<W>();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], k[3][r]);
+    job_sync<W>();
+    const uint32_t base = e0 & ~(2 * m - 1), kk = e0 - base;
+    const uint4*   A    = X + base;
+    const uint4*   B    = X + base + m;
+    // a pair of runs that is all padding (the left run starts with the padding key) stays as it is
+    const uint4 a0 = A[0];
+    if ((a0.x & a0.y & a0.z & a0.w) != ~0u)
+    {
+        uint32_t lo = kk > m ? kk - m : 0u, hi = kk < m ? kk : m;  // i = outputs [0, kk) taken from A
+        while (lo < hi)
+        {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key_le(A[mid], B[kk - 1 - mid]))
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        uint32_t i = lo, j = kk - lo;
+        uint4    a = A[min(i, m - 1)], b = B[min(j, m - 1)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const bool ta = i < m && (j >= m || key_le(a, b));
+            const uint4 o = ta ? a : b;
+            k[0][r] = o.x, k[1][r] = o.y, k[2][r] = o.z, k[3][r] = o.w;
+            if (r < 3)
+            {
+                if (ta)
+                    a = A[min(++i, m - 1)];
+                else
+                    b = B[min(++j, m - 1)];
+            }
+        }
+    }
+}
+
 // Bitonic sort of the job's 256*W slots (4 consecutive per lane, slot e = wj*256 + lane*4 + r)
-// over the first P (power of two) slots.  Keys are unique (the slot is in the low bits).  The
+// over the first P (power of two) slots.  Workgroup jobs (W > 1, P > 256) sort every wave's 256
+// slots on their own and merge the sorted runs (merge_level).  Keys are unique (the slot is in the low bits).  The
 // network runs on dwords (no 64-bit register pairs to keep together); cross-wave stages exchange
 // whole keys through LDS as 16-byte words.
 template <int W>
@@ -1812,24 +1875,33 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
                 a &= k[i][r];
         dead = __builtin_amdgcn_ballot_w64(a != ~0u) == 0;
     }
+    // the in-wave phases sort each wave's slots ascending (directions from the wave-local slot)
+    const uint32_t el = (W > 1 && P > 256 && BRA_MJ_MERGE) ? (uint32_t) lane * 4 : e0;
     for (int size = 2; size <= P; size <<= 1)
     {
         if (dead && size <= 256)
             continue;
+        if constexpr (W > 1 && BRA_MJ_MERGE)
+            if (size > 256)
+            {
+                merge_level<W, KD>(k, S, e0, (uint32_t) size / 2);
+                continue;
+            }
+        const uint32_t e0w = el;
         switch (size)
         {
-        case 2: net_phase<W, KD, 2>(k, S, e0); break;
-        case 4: net_phase<W, KD, 4>(k, S, e0); break;
-        case 8: net_phase<W, KD, 8>(k, S, e0); break;
-        case 16: net_phase<W, KD, 16>(k, S, e0); break;
-        case 32: net_phase<W, KD, 32>(k, S, e0); break;
-        case 64: net_phase<W, KD, 64>(k, S, e0); break;
-        case 128: net_phase<W, KD, 128>(k, S, e0); break;
-        case 256: net_phase<W, KD, 256>(k, S, e0); break;
-        case 512: net_phase<W, KD, 512>(k, S, e0); break;
-        case 1024: net_phase<W, KD, 1024>(k, S, e0); break;
-        case 2048: net_phase<W, KD, 2048>(k, S, e0); break;
-        default: net_phase<W, KD, 4096>(k, S, e0); break;
+        case 2: net_phase<W, KD, 2>(k, S, e0w); break;
+        case 4: net_phase<W, KD, 4>(k, S, e0w); break;
+        case 8: net_phase<W, KD, 8>(k, S, e0w); break;
+        case 16: net_phase<W, KD, 16>(k, S, e0w); break;
+        case 32: net_phase<W, KD, 32>(k, S, e0w); break;
+        case 64: net_phase<W, KD, 64>(k, S, e0w); break;
+        case 128: net_phase<W, KD, 128>(k, S, e0w); break;
+        case 256: net_phase<W, KD, 256>(k, S, e0w); break;
+        case 512: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 512>(k, S, e0); break;
+        case 1024: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 1024>(k, S, e0); break;
+        case 2048: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 2048>(k, S, e0); break;
+        default: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 4096>(k, S, e0); break;
         }
     }
 #pragma unroll
