@@ -5,9 +5,10 @@
 //   k_huff_build     one wave per block: code lengths from the reference's frequency-sorted list
 //                    (bra_minHeap_insert :90-118 restated as: position 0 if the head's frequency is
 //                    larger, else max(1, lower_bound(f)); leaves inserted in symbol order :140-153;
-//                    merge = pop l, pop r, insert l+r :158-175), leaf depth by pointer jumping,
-//                    canonical codes in uint32 with wrap (:227-261), bit count and encoded size
-//                    (:389-395).  Single-leaf trees get length 1 (:201-207).
+//                    merge = pop l, pop r, insert l+r :158-175) kept in registers, leaf depth by
+//                    pointer jumping, canonical codes in uint32 with wrap (:227-261, closed form +
+//                    per-length ranks), bit count and encoded size (:389-395).  Single-leaf trees
+//                    get length 1 (:201-207).
 //   k_huff_offsets   exclusive scan of the encoded sizes -> byte offset of each block's payload
 //   k_huff_tilebits  bits of each 4096-symbol tile of a block's RLE output
 //   k_huff_tilescan  per block: bit offset of every tile
@@ -29,10 +30,13 @@ constexpr int TPB = 256;
 // ------------------------------------------------------------------------------------------------
 // code lengths + canonical codes (one wave per block)
 // ------------------------------------------------------------------------------------------------
+// Whole-wave lane shifts (DPP wave_shr:1 / wave_shl:1): lane i gets lane i - 1 / i + 1; the lane
+// without a source keeps 0.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x138, 0xF, 0xF, false); }
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v) { return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x130, 0xF, 0xF, false); }
+
 struct BuildLds
 {
-    uint32_t list_f[1024];   // frequencies of the list entries, list occupies [head, head+len)
-    uint16_t list_id[1024];
     uint32_t node_f[512];
     uint16_t parent[512];
     uint32_t cnt[260];
@@ -75,73 +79,107 @@ __global__ void __launch_bounds__(64) k_huff_build(const uint32_t* __restrict__ 
                 }
         }
         __syncthreads();
-        uint32_t head = 0, len = 0;
-        auto insert = [&](uint32_t id, uint32_t f) {
-            // position = 0 if empty or head.f > f, else max(1, #entries with freq < f)
-            uint32_t lt = 0;  // wave-uniform: ballot popcounts, no cross-lane reduction through LDS
-            for (uint32_t j0 = 0; j0 < len; j0 += 64)
-            {
-                const uint32_t j = j0 + lane;
-                lt += (uint32_t) __builtin_popcountll(__builtin_amdgcn_ballot_w64(j < len && S.list_f[head + j] < f));
-            }
-            uint32_t p;
-            if (len == 0 || S.list_f[head] > f)
-                p = 0;
-            else
-                p = lt > 1 ? lt : 1;
-            // shift [p, len) right by one (read everything first, then write)
-            uint32_t vf[4], vi[4];
-            const uint32_t m = len - p;
+        // The frequency-sorted list lives in registers: position j = 64 r + lane (at most 256
+        // entries).  An insert or a merge is ballots + lane shuffles -- no LDS round trips or
+        // barriers per step (the LDS list cost 0.35 ms per 256-block batch, one wave per block
+        // on an otherwise idle GPU).
+        uint32_t LF[4] = {0, 0, 0, 0}, LI[4] = {0, 0, 0, 0}, len = 0;
+        const auto lt_count = [&](uint32_t f, uint32_t from) {  // entries in [from, len) with frequency < f
+            uint32_t c = 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
             {
-                const uint32_t j = p + lane + 64 * r;
-                if (j < len)
-                {
-                    vf[r] = S.list_f[head + j];
-                    vi[r] = S.list_id[head + j];
-                }
+                if (64u * r >= len)
+                    break;
+                const uint32_t j = 64u * r + lane;
+                c += (uint32_t) __builtin_popcountll(__builtin_amdgcn_ballot_w64(j >= from && j < len && LF[r] < f));
             }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-                const uint32_t j = p + lane + 64 * r;
-                if (j < len)
-                {
-                    S.list_f[head + j + 1]  = vf[r];
-                    S.list_id[head + j + 1] = (uint16_t) vi[r];
-                }
-            }
-            if (lane == 0)
-            {
-                S.list_f[head + p]  = f;
-                S.list_id[head + p] = (uint16_t) id;
-            }
-            __syncthreads();
-            ++len;
-            (void) m;
+            return c;
         };
+        // leaves in symbol order (:140-153): position 0 if the head's frequency is larger, else
+        // max(1, entries with a smaller frequency) (:90-118); entries from p on move up by one
         for (uint32_t id = 0; id < leaves; ++id)
-            insert(id, S.node_f[id]);
+        {
+            const uint32_t f     = S.node_f[id];
+            const uint32_t headf = __builtin_amdgcn_readlane(LF[0], 0);
+            const uint32_t lt    = lt_count(f, 0);
+            const uint32_t p     = (len == 0 || headf > f) ? 0u : (lt > 1u ? lt : 1u);
+            uint32_t       uF[4], uI[4], cF[4], cI[4];
+            const int      nr = (int) (len / 64u) + 1;  // registers holding the list after the insert
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                if (r >= nr)
+                    break;
+                uF[r] = wave_shr1(LF[r]);
+                uI[r] = wave_shr1(LI[r]);
+                cF[r] = r ? (uint32_t) __builtin_amdgcn_readlane(LF[r > 0 ? r - 1 : 0], 63) : 0u;
+                cI[r] = r ? (uint32_t) __builtin_amdgcn_readlane(LI[r > 0 ? r - 1 : 0], 63) : 0u;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                if (r >= nr)
+                    break;
+                const uint32_t j  = 64u * r + lane;
+                const uint32_t sF = lane ? uF[r] : cF[r], sI = lane ? uI[r] : cI[r];
+                LF[r]             = j > p ? sF : (j == p ? f : LF[r]);
+                LI[r]             = j > p ? sI : (j == p ? id : LI[r]);
+            }
+            ++len;
+        }
+        // merges (:158-175): pop the two head entries, insert their sum by the same rule
         uint32_t nodes = leaves;
         while (len > 1)
         {
-            const uint32_t l = S.list_id[head], r = S.list_id[head + 1];
-            const uint32_t f = S.list_f[head] + S.list_f[head + 1];
-            head += 2;
-            len -= 2;
+            const uint32_t f  = __builtin_amdgcn_readlane(LF[0], 0) + __builtin_amdgcn_readlane(LF[0], 1);
+            const uint32_t l  = __builtin_amdgcn_readlane(LI[0], 0), rt = __builtin_amdgcn_readlane(LI[0], 1);
             const uint32_t id = nodes++;
             if (lane == 0)
             {
-                S.node_f[id] = f;
                 S.parent[id] = 0xFFFF;
                 S.parent[l]  = (uint16_t) id;
-                S.parent[r]  = (uint16_t) id;
+                S.parent[rt] = (uint16_t) id;
             }
-            __syncthreads();
-            insert(id, f);
+            // the list after the pops is old positions [2, len); new[j] = old[j + 2] below the
+            // insert position p, the new node at p, old[j + 1] above
+            const uint32_t n2    = len - 2;
+            const uint32_t headf = __builtin_amdgcn_readlane(LF[0], 2);
+            const uint32_t lt    = lt_count(f, 2);
+            const uint32_t p     = (n2 == 0 || headf > f) ? 0u : (lt > 1u ? lt : 1u);
+            uint32_t       d2F[4], d1F[4], d2I[4], d1I[4], n0F[4], n1F[4], n0I[4], n1I[4];
+            const int      nr = (int) ((len - 1) / 64u) + 1;  // registers holding the list before the pops
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                if (r >= nr)
+                    break;
+                d1F[r] = wave_shl1(LF[r]);
+                d2F[r] = wave_shl1(d1F[r]);
+                d1I[r] = wave_shl1(LI[r]);
+                d2I[r] = wave_shl1(d1I[r]);
+                const int q = r < 3 ? r + 1 : 3;
+                n0F[r] = r < 3 ? (uint32_t) __builtin_amdgcn_readlane(LF[q], 0) : 0u;
+                n1F[r] = r < 3 ? (uint32_t) __builtin_amdgcn_readlane(LF[q], 1) : 0u;
+                n0I[r] = r < 3 ? (uint32_t) __builtin_amdgcn_readlane(LI[q], 0) : 0u;
+                n1I[r] = r < 3 ? (uint32_t) __builtin_amdgcn_readlane(LI[q], 1) : 0u;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                if (r >= nr)
+                    break;
+                const uint32_t j  = 64u * r + lane;
+                const uint32_t aF = lane < 62 ? d2F[r] : (lane == 62 ? n0F[r] : n1F[r]);
+                const uint32_t aI = lane < 62 ? d2I[r] : (lane == 62 ? n0I[r] : n1I[r]);
+                const uint32_t bF = lane < 63 ? d1F[r] : n0F[r];
+                const uint32_t bI = lane < 63 ? d1I[r] : n0I[r];
+                LF[r]             = j < p ? aF : (j == p ? f : bF);
+                LI[r]             = j < p ? aI : (j == p ? id : bI);
+            }
+            len = n2 + 1;
         }
+        __syncthreads();
         // depth of every node by pointer jumping (root has parent 0xFFFF, depth 0)
         uint32_t anc[8], dep[8];
 #pragma unroll
@@ -217,20 +255,53 @@ __global__ void __launch_bounds__(64) k_huff_build(const uint32_t* __restrict__ 
             bits += (uint64_t) h[r] * S.len_s[lane * 4 + r];
         for (int d = 32; d > 0; d >>= 1)
             bits += shfl_xor64(bits, d);
+        // canonical codes (:227-261) in uint32 with wrap: first code of length l =
+        // sum_{k < l} cnt[k] << (l - k) (terms shifted by >= 32 vanish), then each symbol adds its
+        // rank among the symbols of its length (symbol order); one ballot round per distinct length
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t l = (uint32_t) lane * 4 + r + 1;
+            uint32_t       c = 0;
+            for (uint32_t k = l > 32 ? l - 31 : 1; k < l; ++k)
+                c += S.cnt[k] << (l - k);
+            S.next[l] = c;
+        }
+        __syncthreads();
+        {
+            uint32_t L[4], code[4] = {0, 0, 0, 0};
+            bool     todo[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                L[r]    = S.len_s[lane * 4 + r];
+                todo[r] = L[r] != 0;
+            }
+            const uint64_t below = (1ull << lane) - 1ull;
+            for (;;)
+            {
+                const uint32_t cand = todo[0] ? L[0] : todo[1] ? L[1] : todo[2] ? L[2] : todo[3] ? L[3] : 0u;
+                const uint64_t any  = __builtin_amdgcn_ballot_w64(cand != 0);
+                if (!any)
+                    break;
+                const uint32_t L0 = __builtin_amdgcn_readlane(cand, (uint32_t) __builtin_ctzll(any));
+                uint32_t       before = 0, own = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    before += (uint32_t) __builtin_popcountll(__builtin_amdgcn_ballot_w64(L[r] == L0) & below);
+                const uint32_t first = S.next[L0];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (L[r] == L0)
+                    {
+                        code[r] = first + before + own++;
+                        todo[r] = false;
+                    }
+            }
+            reinterpret_cast<uint4*>(codes + (size_t) b * 256)[lane] = make_uint4(code[0], code[1], code[2], code[3]);
+        }
         if (lane == 0)
         {
-            uint32_t code = 0;
-            for (int l = 1; l <= 256; ++l)
-            {
-                code <<= 1;
-                S.next[l] = code;
-                code += S.cnt[l];
-            }
-            for (int s = 0; s < 256; ++s)
-            {
-                const uint32_t L = S.len_s[s];
-                codes[(size_t) b * 256 + s] = L ? S.next[L]++ : 0;
-            }
             HuffMetaRec& M  = meta[b];
             M.orig_size     = rle_size[b];
             const uint32_t bc = (uint32_t) bits;  // bra_huffman.c:390-392 accumulates in uint32
