@@ -120,26 +120,70 @@ __device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st,
     tbl[owner * TSTRIDE + lane_id()] = start_table_dword(st);
 }
 
-// Lane l's dword of a segment's start table (entries 4l .. 4l+3, little-endian).
+// Stage (SIZE, J) of a bitonic network over 256 unique 32-bit keys, 4 per lane (slot 4 lane + r),
+// ascending, and recursively the rest of its merge phase: partners J >= 4 slots away sit J / 4
+// lanes away (DPP / permlane, xlane), closer ones in the same lane.  A compare-exchange of 32-bit
+// keys is a min, a max and a select.
+template <int SIZE, int J>
+__device__ __forceinline__ void sort256_stage(uint32_t (&k)[4])
+{
+    const uint32_t e0 = (uint32_t) lane_id() * 4;
+    if constexpr (J >= 4)
+    {
+        const bool keep_min = ((e0 & SIZE) == 0) == ((e0 & J) == 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t o = xlane<J / 4>(k[r]);
+            k[r]             = keep_min ? min(k[r], o) : max(k[r], o);
+        }
+    }
+    else
+    {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const int q = r ^ J;
+            if (q > r)
+            {
+                const bool     asc = ((e0 + r) & SIZE) == 0;
+                const uint32_t lo = min(k[r], k[q]), hi = max(k[r], k[q]);
+                k[r]              = asc ? lo : hi;
+                k[q]              = asc ? hi : lo;
+            }
+        }
+    }
+    if constexpr (J > 1)
+        sort256_stage<SIZE, J / 2>(k);
+}
+
+template <int SIZE>
+__device__ __forceinline__ void sort256_phases(uint32_t (&k)[4])
+{
+    sort256_stage<SIZE, SIZE / 2>(k);
+    if constexpr (SIZE < 256)
+        sort256_phases<SIZE * 2>(k);
+}
+
+// Lane l's dword of a segment's start table (entries 4l .. 4l+3, little-endian): the symbols by
+// decreasing last occurrence, then the unseen ones by increasing value.  32-bit sort keys: seen
+// symbol c: (0xFFFFFE - last occurrence) << 8 | c (occurrences are block positions < 2^24 - 1),
+// unseen: 0xFFFFFF00 | c.  (A generic 64-bit key/value sort with LDS permutes here cost about a
+// third of the wave kernel's time on uniform random data.)
 __device__ __forceinline__ uint32_t start_table_dword(const int32_t* __restrict__ st)
 {
-    // K(c) = last-occurrence time + 256 for seen symbols, 255 - c for unseen: the table is the
-    // symbols by decreasing K.  Sort ascending by (2^40 - K) << 8 | c.
-    const int lane = lane_id();
-    uint64_t  k[4];
-    uint32_t  v[4];
-    const int4 tv = reinterpret_cast<const int4*>(st)[lane];
+    const int  lane = lane_id();
+    const int4 tv   = reinterpret_cast<const int4*>(st)[lane];
     const int32_t tt[4] = {tv.x, tv.y, tv.z, tv.w};
+    uint32_t   k[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        const uint32_t c = lane * 4 + r;
-        const uint64_t K = tt[r] >= 0 ? (uint64_t) tt[r] + 256u : (uint64_t) (255u - c);
-        k[r]             = (((1ull << 40) - K) << 8) | c;
-        v[r]             = c;
+        const uint32_t c = (uint32_t) lane * 4 + r;
+        k[r]             = tt[r] >= 0 ? ((0xFFFFFEu - (uint32_t) tt[r]) << 8) | c : 0xFFFFFF00u | c;
     }
-    wave_bitonic_sort4(k, v, 256);
-    return (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((v[3] & 0xFF) << 24);
+    sort256_phases<2>(k);
+    return (k[0] & 0xFF) | ((k[1] & 0xFF) << 8) | ((k[2] & 0xFF) << 16) | ((k[3] & 0xFF) << 24);
 }
 
 // Shift one table dword up by one entry: entry 0 becomes the top entry of the previous dword.
