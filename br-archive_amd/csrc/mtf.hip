@@ -683,6 +683,9 @@ __device__ __forceinline__ uint32_t count_less(uint32_t key, uint32_t q, uint64_
     return (uint32_t) __popc(ll) + (uint32_t) __popc(lh);
 }
 
+#ifndef BRA_MTF_REP_LOOP
+#define BRA_MTF_REP_LOOP 4  // repeats in a 64-symbol chunk counted one ballot each up to this many (random data: 0/4/8/16 -> 2.05/2.04/2.05/2.20 ms)
+#endif
 static_assert(MTF_SEG_ENC == 1024, "k_mtf_encode_wave stages a segment as 64 lanes x 16 bytes");
 
 __global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
@@ -750,7 +753,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restri
                 const uint64_t fb = Fm & below;
                 rank              = p0 + (uint32_t) __popcll(fb) - count_less<8>(p0, p0, fb);
             }
-            if (__popcll(Am) > 16)
+            if (__popcll(Am) > BRA_MTF_REP_LOOP)
             {
                 // many repeats: #{k in (j, i): nxt_k < i}, nxt in [1, 64] -> 7 bits
                 const uint64_t in_ji = below & (rep ? ~((2ull << j) - 1ull) : 0ull);
