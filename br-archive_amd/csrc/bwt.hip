@@ -75,6 +75,9 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 // min waves per SIMD the job kernels are compiled for (wave jobs: 6, i.e. <= 80 VGPRs, 8 bytes of
 // spill, faster than the compiler's 84 VGPRs at 5; workgroup jobs: compiler choice, 5 -- forcing 6
 // spilled and measured no faster)
+#ifndef BRA_JOB_PREFETCH
+#define BRA_JOB_PREFETCH 1  // wave jobs: next job's descriptor and payloads loaded ahead
+#endif
 #ifndef BRA_MJ_MERGE
 #define BRA_MJ_MERGE 1  // workgroup jobs: per-wave sorts + merge-path levels (0: bitonic phases through LDS)
 #endif
@@ -82,7 +85,7 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
 #endif
 #ifndef JOB_MIN_WAVES
-#define JOB_MIN_WAVES 6
+#define JOB_MIN_WAVES 5  // 6 spills with the payload prefetch (wave jobs 2.24 -> 2.14 ms with prefetch at 5; 2.53 spilling at 6)
 #endif
 
 enum : uint32_t { MODE_STRING = 0, MODE_RANK = 1 };
@@ -2015,7 +2018,7 @@ __device__ unsigned long long g_phase[2][8];
 #endif
 
 template <uint32_t MODE, int W>
-__device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj)
+__device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj, const uint64_t* pre = nullptr)
 {
     PH_T(t_start);
 #ifdef BRA_PHASES
@@ -2056,7 +2059,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         if (c < T)
         {
             // STRING payloads are the 64-bit MSD payloads in the key buffers (index in the low bits)
-            v[r] = (MODE == MODE_RANK) ? V[J.start + c] : (uint32_t) K[J.start + c] & 0xFFFFFFu;
+            v[r] = (MODE == MODE_RANK) ? V[J.start + c] : (uint32_t) (pre ? pre[r] : K[J.start + c]) & 0xFFFFFFu;
             if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (mode %u buf %u slot %u)", v[r] & 0xFFFFFFu, BD.len, MODE, J.buf,
                             J.start + c))
                 v[r] = 0;
@@ -2251,6 +2254,44 @@ __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
         return job_claim(a, xs, c, a.jq_chunk, first, end) ? first : ~0u;
     };
     uint32_t j = dyn ? next(~0u) : (R.first < R.end ? R.first : ~0u);
+#if BRA_JOB_PREFETCH
+    // STRING mode: the next job's descriptor and payloads are loaded before the current job runs
+    // (their latency overlaps the current job's key gathers)
+    const auto load_pay = [&](const Job& J, uint64_t (&p)[4]) {
+        const uint64_t* K = J.buf ? a.key1 : a.key0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = lane_id() * 4 + r;
+            p[r]             = c < J.len ? K[J.start + c] : 0ull;
+        }
+    };
+    if (MODE == MODE_STRING)
+    {
+        Job      J = j != ~0u ? a.jobs[j] : Job{};
+        uint64_t pc[4];
+        if (j != ~0u)
+            load_pay(J, pc);
+        while (j != ~0u)
+        {
+            const uint32_t jn = next(j);
+            Job            Jn{};
+            uint64_t       pn[4] = {0, 0, 0, 0};
+            if (jn != ~0u)
+            {
+                Jn = a.jobs[jn];
+                load_pay(Jn, pn);
+            }
+            job_run<MODE, 1>(a, J, lds[wl], 0, pc);
+            J = Jn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                pc[r] = pn[r];
+            j = jn;
+        }
+        return;
+    }
+#endif
     while (j != ~0u)
     {
         job_run<MODE, 1>(a, a.jobs[j], lds[wl], 0);
