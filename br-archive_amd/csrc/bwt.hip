@@ -69,6 +69,9 @@ constexpr uint32_t CSTRIDE    = 256 + 16;  // digit-counter copies (TileStagePN,
 #define BRA_SCATTER_NC 4
 #endif
 constexpr int      SCATTER_NC = BRA_SCATTER_NC;
+#ifndef BRA_HIST_NC
+#define BRA_HIST_NC 4  // counter copies of the MSD histogram (copy = lane & (NC - 1))
+#endif
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
@@ -563,7 +566,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
 {
     const uint32_t ntiles = dev_count(&lv->n_tiles_next);
     __shared__ uint32_t h[256];
-    __shared__ uint32_t hc[SCATTER_NC * CSTRIDE];  // per-copy counters (copy = lane & (NC - 1), see TileStagePN)
+    __shared__ uint32_t hc[BRA_HIST_NC * CSTRIDE];  // per-copy counters (copy = lane & (NC - 1), see TileStagePN)
     if (MODE == MODE_STRING && BRA_HIST_PIPE)
     {
         // software-pipelined over the workgroup's tiles: the next tile's descriptor and payloads
@@ -606,10 +609,10 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
             uint4          wn;
             load(pn, Dn, wn);
 #pragma unroll
-            for (int c = 0; c < SCATTER_NC; ++c)
+            for (int c = 0; c < BRA_HIST_NC; ++c)
                 hc[c * CSTRIDE + threadIdx.x] = 0;
             __syncthreads();
-            const uint32_t cp   = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
+            const uint32_t cp   = (uint32_t) (lane_id() & (BRA_HIST_NC - 1)) * CSTRIDE;
             const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i)
@@ -618,7 +621,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
             __syncthreads();
             uint32_t tot = 0;
 #pragma unroll
-            for (int c = 0; c < SCATTER_NC; ++c)
+            for (int c = 0; c < BRA_HIST_NC; ++c)
                 tot += hc[c * CSTRIDE + threadIdx.x];
             tile_hist[(size_t) D.t * 256 + threadIdx.x] = tot;
             p = pn;
