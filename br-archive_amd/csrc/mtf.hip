@@ -379,6 +379,44 @@ __device__ __noinline__ uint32_t count_below(const uint32_t (&R)[NRD], uint32_t 
     return n;
 }
 
+#ifndef BRA_MTF_REG_FLAT
+#define BRA_MTF_REG_FLAT 1  // one branch-free path over the 8 table registers (0: 16-entry fast path + per-register branches)
+#endif
+#if BRA_MTF_REG_FLAT
+// One MTF step on the 32-entry register table: the symbol's position p = 4 k + b from the first
+// register holding a zero byte of R ^ c (k = 8: not among the first 32 entries -- a first
+// occurrence), then every register below k shifts up by one byte (v_alignbit) and register k
+// shifts its bytes 0..b (a bitfield insert), all branch-free.  Post-BWT text rarely has all 64
+// lanes of a wave inside the first 16 entries at once (P(rank < 16)^64), so a fast path for them
+// rarely ran and the per-register branches cost more than they saved.
+__device__ __forceinline__ uint32_t mtf_step_reg(uint32_t (&R)[NRD], uint32_t c)
+{
+    const uint32_t cc = c * 0x01010101u;
+    uint32_t       k = NRD, zz = 0;
+#pragma unroll
+    for (int q = NRD - 1; q >= 0; --q)
+    {
+        const uint32_t z = haszero8(R[q] ^ cc);
+        k                = z ? (uint32_t) q : k;
+        zz               = z ? z : zz;
+    }
+    const uint32_t b    = (uint32_t) __builtin_ctz(zz | 0x80000000u) >> 3;  // 3 when not found
+    const uint32_t part = b >= 3 ? 0xFFFFFFFFu : (1u << (8 * b + 8)) - 1u;  // bytes 0..b of register k
+    uint32_t       rank;
+    if (__builtin_amdgcn_ballot_w64(k == NRD))
+        rank = k < NRD ? k * 4 + b : MTF_REG + c - count_below(R, c);
+    else
+        rank = k * 4 + b;
+#pragma unroll
+    for (int q = NRD - 1; q >= 0; --q)
+    {
+        const uint32_t sh = q ? __builtin_amdgcn_alignbit(R[q], R[q - 1], 24) : (R[0] << 8) | c;
+        const uint32_t m  = (uint32_t) q < k ? 0xFFFFFFFFu : ((uint32_t) q == k ? part : 0u);
+        R[q]              = (sh & m) | (R[q] & ~m);
+    }
+    return rank;
+}
+#else
 __device__ __forceinline__ uint32_t mtf_step_reg(uint32_t (&R)[NRD], uint32_t c)
 {
     const uint32_t cc = c * 0x01010101u;
@@ -439,6 +477,7 @@ __device__ __forceinline__ uint32_t mtf_step_reg(uint32_t (&R)[NRD], uint32_t c)
     }
     return rank;
 }
+#endif
 
 // The first MTF_REG entries of a segment's start table for a block of <= MTF_REG distinct symbols,
 // built by one wave: the seen symbols (last occurrence >= 0, at most MTF_REG of them) ordered by
