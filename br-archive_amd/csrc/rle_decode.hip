@@ -60,12 +60,13 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                                                  const uint64_t* __restrict__ out_base, const uint64_t* __restrict__ out_cap,
                                                  uint32_t* __restrict__ out_size)
 {
-    __shared__ uint4    win4[(RD_WIN + RD_HALO) / 16];
+    __shared__ uint4    win4[1 + (RD_WIN + RD_HALO) / 16];  // one 16-byte pad in front: unaligned output reads start up to 15 bytes early
     __shared__ uint16_t NX[RD_WAVES][RD_SUB];  // successor (sub-window position; >= len: exit) / later: chain positions
     __shared__ uint32_t SM[RD_WAVES][RD_SUB];  // output bytes to the exit / later: output offsets of the chain
     __shared__ uint32_t sub_entry[RD_WAVES], sub_out[RD_WAVES], sub_tot[RD_WAVES];
     __shared__ uint32_t sh_E, sh_O;
-    const uint8_t* win  = reinterpret_cast<const uint8_t*>(win4);
+    const uint8_t*  win   = reinterpret_cast<const uint8_t*>(win4 + 1);
+    const uint32_t* win32 = reinterpret_cast<const uint32_t*>(win4 + 1);
     const int      lane = lane_id();
     const uint32_t k    = threadIdx.x >> 6;  // this wave's sub-window
     const uint64_t below = (1ull << lane) - 1ull;
@@ -96,7 +97,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             {
                 const uint32_t t = threadIdx.x + h * RD_TPB;
                 if (t < RD_LOAD)
-                    win4[t] = pf[h];
+                    win4[1 + t] = pf[h];
             }
             __syncthreads();
             // prefetch the next window while this one is decoded
@@ -246,7 +247,11 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                     uint32_t dn = idx + 1 < ncon ? SM[k][idx + 1] : 0xFFFFFFFFu;
                     uint32_t wv[4] = {0, 0, 0, 0};
                     const uint32_t nb = min(16u, tot - o0);
-                    for (uint32_t j = 0; j < nb; ++j)
+                    // one piece per control covering part of the lane's 16 bytes: a run fills its
+                    // bytes with one value, a literal copies a 16-byte unaligned LDS read (5 dwords
+                    // + alignbyte) positioned so that byte j of it is output byte j; bytes outside
+                    // [j, j + n) are kept by a bitfield insert
+                    for (uint32_t j = 0; j < nb;)
                     {
                         const uint32_t o = o0 + j;
                         while (o >= dn)
@@ -258,8 +263,36 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                         }
                         const uint32_t at = sb + p;
                         const uint32_t c  = win[at];
-                        const uint32_t v  = win[at + 1 + (c < 128u ? o - d : 0u)];
-                        wv[j >> 2] |= v << (8 * (j & 3));
+                        const uint32_t n  = min(dn - o, nb - j);
+                        uint32_t       v[4];
+                        if (c > 128u)
+                        {
+                            const uint32_t r = win[at + 1] * 0x01010101u;
+                            v[0] = v[1] = v[2] = v[3] = r;
+                        }
+                        else
+                        {
+                            const int32_t  base = (int32_t) (at + 1 + (o - d)) - (int32_t) j;  // >= -15
+                            const int32_t  a4   = (base >> 2);                               // floor
+                            const uint32_t sh   = (uint32_t) base & 3u;
+                            uint32_t       W[5];
+#pragma unroll
+                            for (int i = 0; i < 5; ++i)
+                                W[i] = win32[a4 + i];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                v[i] = __builtin_amdgcn_alignbyte(W[i + 1], W[i], sh);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                        {
+                            const int32_t  lo8 = min(max((int32_t) j - 4 * i, 0), 4), hi8 = min(max((int32_t) (j + n) - 4 * i, 0), 4);
+                            const uint32_t mh  = hi8 >= 4 ? 0xFFFFFFFFu : (1u << (8 * hi8)) - 1u;
+                            const uint32_t ml  = lo8 >= 4 ? 0xFFFFFFFFu : (1u << (8 * lo8)) - 1u;
+                            const uint32_t m   = mh & ~ml;
+                            wv[i]              = (v[i] & m) | (wv[i] & ~m);
+                        }
+                        j += n;
                     }
                     const uint64_t a = (uint64_t) ob0 + o0;  // block output offset
                     uint8_t*       q = dst + a;
