@@ -58,16 +58,49 @@ __device__ __forceinline__ uint32_t split_step(uint32_t n)
 __global__ void __launch_bounds__(TPB) k_ib_hist(const uint8_t* __restrict__ L, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                  uint32_t* __restrict__ th)
 {
-    __shared__ uint32_t h[256];
+    // 16 consecutive bytes per thread, one LDS atomic per run of equal bytes (BWT output is
+    // run-heavy: one atomic per byte made the lanes of a run serialise on one counter), 4 counter
+    // copies by lane
+    constexpr uint32_t HS = 256 + 16;
+    __shared__ uint32_t h[4 * HS];
+    const uint32_t      cp = (uint32_t) (lane_id() & 3) * HS;
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
-        h[threadIdx.x] = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            h[q * HS + threadIdx.x] = 0;
         __syncthreads();
         const Piece P = tiles[t];
-        for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
-            atomicAdd(&h[L[P.off + i]], 1u);
+        for (uint32_t i0 = threadIdx.x * 16; i0 < P.len; i0 += TPB * 16)
+        {
+            const uint8_t* src = L + P.off + i0;
+            uint32_t       w[4] = {0, 0, 0, 0};
+            const uint32_t n    = min(16u, P.len - i0);
+            if (n == 16 && (((uintptr_t) src) & 15) == 0)
+            {
+                const uint4 v = *reinterpret_cast<const uint4*>(src);
+                w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+            }
+            else
+                for (uint32_t j = 0; j < n; ++j)
+                    w[j >> 2] |= (uint32_t) src[j] << (8 * (j & 3));
+            uint32_t prev = w[0] & 0xFFu, run = 1;
+            for (uint32_t j = 1; j < n; ++j)
+            {
+                const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                if (c == prev)
+                    ++run;
+                else
+                {
+                    atomicAdd(&h[cp + prev], run);
+                    prev = c;
+                    run  = 1;
+                }
+            }
+            atomicAdd(&h[cp + prev], run);
+        }
         __syncthreads();
-        th[(size_t) t * 256 + threadIdx.x] = h[threadIdx.x];
+        th[(size_t) t * 256 + threadIdx.x] = h[threadIdx.x] + h[HS + threadIdx.x] + h[2 * HS + threadIdx.x] + h[3 * HS + threadIdx.x];
         __syncthreads();
     }
 }
@@ -102,19 +135,31 @@ __global__ void __launch_bounds__(64) k_ib_scatter(const uint8_t* __restrict__ L
                                                    uint32_t* __restrict__ T)
 {
     __shared__ uint32_t cnt[256];
+    __shared__ uint4    tb4[ITILE / 16];  // the tile's bytes, loaded once (a byte load per step was a global round trip per 64 positions)
+    const uint8_t*      tb   = reinterpret_cast<const uint8_t*>(tb4);
     const int           lane = lane_id();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const Piece P = tiles[t];
         for (int i = lane; i < 256; i += 64)
             cnt[i] = th[(size_t) t * 256 + i];
+        const uint8_t* src = L + P.off;
+        if (P.len == ITILE && (((uintptr_t) src) & 15) == 0)
+        {
+#pragma unroll
+            for (uint32_t q = 0; q < ITILE / 16 / 64; ++q)
+                tb4[q * 64 + lane] = reinterpret_cast<const uint4*>(src)[q * 64 + lane];
+        }
+        else
+            for (uint32_t i = lane; i < P.len; i += 64)
+                reinterpret_cast<uint8_t*>(tb4)[i] = src[i];
         __syncthreads();
         const uint64_t boff = blocks[P.block].off;
         for (uint32_t base = 0; base < P.len; base += 64)
         {
             const uint32_t i     = base + lane;
             const bool     valid = i < P.len;
-            const uint32_t c     = valid ? L[P.off + i] : 0xFFFFFFFFu;
+            const uint32_t c     = valid ? tb[i] : 0xFFFFFFFFu;
             uint64_t       m     = __ballot(valid);
 #pragma unroll
             for (int bit = 0; bit < 8; ++bit)
@@ -283,19 +328,31 @@ __global__ void __launch_bounds__(64) k_ib_scatter2(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ TL)
 {
     __shared__ uint32_t cnt[256];
+    __shared__ uint4    tb4[ITILE / 16];  // the tile's bytes, loaded once (a byte load per step was a global round trip per 64 positions)
+    const uint8_t*      tb   = reinterpret_cast<const uint8_t*>(tb4);
     const int           lane = lane_id();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const Piece P = tiles[t];
         for (int i = lane; i < 256; i += 64)
             cnt[i] = th[(size_t) t * 256 + i];
+        const uint8_t* src = L + P.off;
+        if (P.len == ITILE && (((uintptr_t) src) & 15) == 0)
+        {
+#pragma unroll
+            for (uint32_t q = 0; q < ITILE / 16 / 64; ++q)
+                tb4[q * 64 + lane] = reinterpret_cast<const uint4*>(src)[q * 64 + lane];
+        }
+        else
+            for (uint32_t i = lane; i < P.len; i += 64)
+                reinterpret_cast<uint8_t*>(tb4)[i] = src[i];
         __syncthreads();
         const uint64_t boff = blocks[P.block].off;
         for (uint32_t base = 0; base < P.len; base += 64)
         {
             const uint32_t i     = base + lane;
             const bool     valid = i < P.len;
-            const uint32_t c     = valid ? L[P.off + i] : 0xFFFFFFFFu;
+            const uint32_t c     = valid ? tb[i] : 0xFFFFFFFFu;
             uint64_t       m     = __ballot(valid);
 #pragma unroll
             for (int bit = 0; bit < 8; ++bit)
