@@ -15,7 +15,7 @@
 //        lanes that finish claim the next splitter at once, so no lane idles on a long hop;
 //   k_ib_chain3  one workgroup per block ranks the splitter list from the primary splitter by
 //        pointer jumping in LDS -> output offset of every hop (and the primary cycle's length);
-//   k_ib_copy3   one wave per hop copies its staged bytes to their output offset.
+//   k_ib_copy4   one lane per hop streams its staged bytes to their output offset.
 // A primary index on a cycle shorter than n (a periodic block) makes the output periodic with that
 // cycle length, exactly like the reference (k_ib_repeat).  The round-1 two-walk kernels remain for
 // blocks of >= 2^24 bytes, for callers that want the transform itself, and as the fallback when
@@ -558,10 +558,12 @@ constexpr uint32_t IB_CH_TPB = 1024;
 __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ pi,
                                                          const uint32_t* __restrict__ cum, uint32_t nblocks,
                                                          const uint32_t* __restrict__ hop_next, const uint32_t* __restrict__ hop_len,
-                                                         uint32_t* __restrict__ start, uint32_t* __restrict__ cyc)
+                                                         uint32_t* __restrict__ start, uint32_t* __restrict__ cyc, uint32_t* __restrict__ order,
+                                                         uint32_t* __restrict__ cnt)
 {
     __shared__ uint16_t nx[IB_MAXS];
     __shared__ uint32_t R[IB_MAXS];
+    __shared__ uint16_t C[IB_MAXS];  // hops from q to the end of the chain (its rank from the end)
     __shared__ uint32_t sh_tot;
     constexpr uint16_t  END = 0xFFFF;
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
@@ -575,6 +577,7 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
             const uint32_t h = hop_next[base + q];
             nx[q]            = h == 0xFFFFFFFFu ? END : (uint16_t) h;
             R[q]             = hop_len[base + q];
+            C[q]             = R[q] ? 1 : 0;  // hops that produce output (unused splitter slots have none)
         }
         __syncthreads();
         for (uint32_t q = threadIdx.x; q < nn; q += IB_CH_TPB)
@@ -586,17 +589,19 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
             ++rounds;
         for (uint32_t r = 0; r <= rounds; ++r)
         {
-            uint32_t nn2[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB], rr[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB];
+            uint32_t nn2[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB], rr[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB], cc[(IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB];
 #pragma unroll
             for (uint32_t u = 0; u < (IB_MAXS + IB_CH_TPB - 1) / IB_CH_TPB; ++u)
             {
                 const uint32_t q = threadIdx.x + u * IB_CH_TPB;
                 nn2[u]           = END;
                 rr[u]            = 0;
+                cc[u]            = 0;
                 if (q < nn && nx[q] != END)
                 {
                     nn2[u] = nx[nx[q]];
                     rr[u]  = R[nx[q]];
+                    cc[u]  = C[nx[q]];
                 }
             }
             __syncthreads();
@@ -608,6 +613,7 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
                 {
                     nx[q] = (uint16_t) nn2[u];
                     R[q] += rr[u];
+                    C[q] = (uint16_t) (C[q] + cc[u]);
                 }
             }
             __syncthreads();
@@ -616,58 +622,104 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
         {
             sh_tot = R[s0];
             cyc[b] = min(R[s0], B.len);
+            cnt[b] = C[s0];
         }
         __syncthreads();
-        const uint32_t tot = sh_tot;
+        const uint32_t tot = sh_tot, ctot = C[s0];
         for (uint32_t q = threadIdx.x; q < nn; q += IB_CH_TPB)
+        {
             start[base + q] = (nx[q] == END && hop_len[base + q] != 0) ? tot - R[q] : 0xFFFFFFFFu;
+            if (nx[q] == END && hop_len[base + q] != 0 && C[q] <= ctot)
+                order[base + ctot - C[q]] = q;  // the chain's hops in output order
+        }
         __syncthreads();
     }
 }
 
-// One wave per hop: staged bytes -> out[start ...].
-__global__ void __launch_bounds__(256) k_ib_copy3(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ cum, uint32_t nblocks,
+// Lane-per-hop copy: hops average S = 64 bytes, so a wave per hop left most lanes idle and paid
+// three dependent global round trips per 64 bytes.  A lane streams its slot (16-byte aligned) into
+// the output with aligned dword stores (alignbyte of consecutive source dwords; the bytes of the
+// first and last partial dwords go one at a time, the neighbouring hops own the rest of them).
+__device__ __forceinline__ void copy_bytes_al(uint8_t* dst, const uint32_t* src32, uint32_t n)
+{
+    // 64 source bytes per round as four independent 16-byte loads (a dependent dword load per
+    // step serialised the loop on memory latency); the destination gets aligned dwords built with
+    // alignbyte, its partial first and last dwords byte by byte
+    const uint32_t a = (uint32_t) ((uintptr_t) dst & 3u), h = (4u - a) & 3u;  // h: bytes before the first aligned dword
+    const uint4*   s4 = reinterpret_cast<const uint4*>(src32);
+    uint32_t       carry = 0;  // source dword just below the current round (for alignbyte)
+    for (uint32_t r0 = 0; r0 < n; r0 += 64)
+    {
+        uint32_t w[17];
+        w[0] = carry;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+        {
+            const uint4 v = s4[(r0 >> 4) + k];
+            w[1 + 4 * k] = v.x, w[2 + 4 * k] = v.y, w[3 + 4 * k] = v.z, w[4 + 4 * k] = v.w;
+        }
+        carry = w[16];
+        // output byte i (0 <= i < n) = source byte i; aligned destination dwords start at i = h + 4 m
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+        {
+            // destination dword at offset lo = r0 + 4 (m - 1) + h (h > 0: source dwords w[m], w[m + 1],
+            // shifted by h bytes) or r0 + 4 m (h == 0: source dword w[m + 1])
+            const uint32_t i = r0 + (uint32_t) m * 4;
+            const int32_t  lo = h ? (int32_t) (i + h) - 4 : (int32_t) i;
+            const uint32_t v  = h ? __builtin_amdgcn_alignbyte(w[m + 1], w[m], h) : w[m + 1];
+            if (lo >= 0 && (uint32_t) lo + 4 <= n)
+                *reinterpret_cast<uint32_t*>(dst + lo) = v;
+            else
+                for (int t = 0; t < 4; ++t)
+                    if (lo + t >= 0 && (uint32_t) (lo + t) < n)
+                        dst[lo + t] = (uint8_t) (v >> (8 * t));
+        }
+        if (h)
+        {
+            // the destination dword [r0 + 64 + h - 4, r0 + 64 + h) needs the next round's first
+            // source dword: it is written there (as m = 0 of the next round) or, past the end,
+            // its bytes below n are written here
+            const uint32_t lo = r0 + 64 + h - 4;
+            if (r0 + 64 >= n)
+                for (uint32_t t = 0; t < 4; ++t)
+                    if (lo + t < n)
+                        dst[lo + t] = (uint8_t) (w[16] >> (8 * (h + t)));
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ib_copy4(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ cum, const uint32_t* __restrict__ cnt,
+                                                  const uint32_t* __restrict__ order, uint32_t nblocks,
                                                   const uint32_t* __restrict__ start, const uint32_t* __restrict__ hop_len,
                                                   const uint32_t* __restrict__ hop_ovf, const uint32_t* __restrict__ ovl_next,
                                                   const uint8_t* __restrict__ slots, const uint8_t* __restrict__ pool, uint32_t pool_cap,
                                                   uint8_t* __restrict__ out)
 {
-    const int      lane  = lane_id();
-    const uint32_t wpg   = blockDim.x / 64;
     for (uint32_t b = blockIdx.y; b < nblocks; b += gridDim.y)
     {
         const IbBlk    B    = blk[b];
         const uint32_t base = cum[b], nn = cum[b + 1] - base, cap = 4u << B.shift;
         uint8_t*       ob   = out + B.off;
-        for (uint32_t q = blockIdx.x * wpg + (threadIdx.x >> 6); q < nn; q += gridDim.x * wpg)
+        const uint32_t nc = cnt[b];
+        for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nc && r < nn; r += gridDim.x * blockDim.x)
         {
+            // hops in output order: neighbouring lanes write neighbouring output ranges (whole
+            // lines per store instruction; in splitter order every 64-byte hop landed at a random
+            // place and its partial lines cost a read-modify-write each)
+            const uint32_t q  = order[base + r];
             const uint32_t st = start[base + q];
-            if (st == 0xFFFFFFFFu)
+            if (st == 0xFFFFFFFFu || st >= B.len)
                 continue;
-            const uint32_t len = hop_len[base + q];
-            const uint32_t n1  = min(len, cap);
-            const uint8_t* src = slots + B.tslot + (size_t) q * cap;
-            for (uint32_t o = lane * 4; o < n1; o += 256)
-            {
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(src + o);
-#pragma unroll
-                for (uint32_t h = 0; h < 4; ++h)
-                    if (o + h < n1 && st + o + h < B.len)
-                        ob[st + o + h] = (uint8_t) (v >> (8 * h));
-            }
+            const uint32_t len = min(hop_len[base + q], B.len - st);
+            copy_bytes_al(ob + st, reinterpret_cast<const uint32_t*>(slots + B.tslot + (size_t) q * cap), min(len, cap));
             uint32_t c = len > cap ? hop_ovf[base + q] : 0xFFFFFFFFu;
             for (uint32_t o0 = cap; o0 < len && c < pool_cap; o0 += IB_CHUNK)
             {
                 const uint8_t* cs = pool + (size_t) c * IB_CHUNK;
-                const uint32_t o  = o0 + lane * 4;
-                if (o < len)
-                {
-                    const uint32_t v = *reinterpret_cast<const uint32_t*>(cs + lane * 4);
-#pragma unroll
-                    for (uint32_t h = 0; h < 4; ++h)
-                        if (o + h < len && st + o + h < B.len)
-                            ob[st + o + h] = (uint8_t) (v >> (8 * h));
-                }
+                const uint32_t m  = min(IB_CHUNK, len - o0);
+                for (uint32_t j = 0; j < m; ++j)
+                    ob[st + o0 + j] = cs[j];
                 c = ovl_next[c];
             }
         }
@@ -716,7 +768,7 @@ void IbwtWorkspace::release()
     (void) hipFree(start);
     (void) hipFree(cyc);
     for (void* p : {(void*) blk, (void*) cum, (void*) ctl, (void*) m_next, (void*) m_len, (void*) m_ovf, (void*) m_start, (void*) ovl_next,
-                    (void*) slot, (void*) pool})
+                    (void*) slot, (void*) pool, (void*) m_order, (void*) m_cnt})
         (void) hipFree(p);
     *this = IbwtWorkspace{};
 }
@@ -743,7 +795,7 @@ bool IbwtWorkspace::reserve_main(uint32_t nblocks, uint32_t nsplit, uint64_t slo
     {
         cap_mb           = 0;
         const uint32_t c = nblocks + 64;
-        if (!dev_alloc(blk, (uint64_t) c * 4) || !dev_alloc(cum, c) || !dev_alloc(ctl, 512))
+        if (!dev_alloc(blk, (uint64_t) c * 4) || !dev_alloc(cum, c) || !dev_alloc(ctl, 512) || !dev_alloc(m_cnt, c))
             return false;
         cap_mb = c;
     }
@@ -752,7 +804,8 @@ bool IbwtWorkspace::reserve_main(uint32_t nblocks, uint32_t nsplit, uint64_t slo
         cap_ms           = 0;
         const uint32_t c = nsplit + nsplit / 8 + 64;
         const uint32_t pc = c / 8 + 256;  // overflow chunks (hops longer than 4 S: ~2 % of them)
-        if (!dev_alloc(m_next, c) || !dev_alloc(m_len, c) || !dev_alloc(m_ovf, c) || !dev_alloc(m_start, c) || !dev_alloc(ovl_next, pc) ||
+        if (!dev_alloc(m_next, c) || !dev_alloc(m_len, c) || !dev_alloc(m_ovf, c) || !dev_alloc(m_start, c) || !dev_alloc(m_order, c) ||
+            !dev_alloc(ovl_next, pc) ||
             !dev_alloc(pool, (uint64_t) pc * IB_CHUNK))
             return false;
         cap_ms   = c;
@@ -843,8 +896,8 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
         hipLaunchKernelGGL(k_ib_walk3, dim3(2048), dim3(256), 0, s, a);
     }
     hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
-                       w.m_len, w.m_start, w.cyc);
-    hipLaunchKernelGGL(k_ib_copy3, dim3(256, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, blk, w.cum, nblocks, w.m_start, w.m_len,
+                       w.m_len, w.m_start, w.cyc, w.m_order, w.m_cnt);
+    hipLaunchKernelGGL(k_ib_copy4, dim3(16, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, blk, w.cum, w.m_cnt, w.m_order, nblocks, w.m_start, w.m_len,
                        w.m_ovf, w.ovl_next, w.slot, w.pool, w.pool_cap, d_out);
     hipLaunchKernelGGL(k_ib_repeat, dim3(64, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_blocks, nblocks, w.cyc, d_out);
     BRA_HIP_CHECK(hipGetLastError());
