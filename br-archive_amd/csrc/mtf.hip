@@ -27,49 +27,55 @@ __device__ __forceinline__ uint32_t haszero8(uint32_t x) { return (x - 0x0101010
 // ------------------------------------------------------------------------------------------------
 // encode
 // ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_barrier_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave per segment (1024 symbols = 16 per lane, one 16-byte load): each lane keeps only the
+// last byte of every run of equal bytes inside its 16 and max-updates the segment's 256 LDS
+// entries; the state row goes out as one 16-byte store per lane.  (A workgroup per segment with a
+// 4-byte load per thread was bound by its load -> atomics -> barrier -> store latency chain.)
 __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__ in, const Piece* __restrict__ segs, uint32_t nseg,
                                                      int32_t* __restrict__ state)
 {
-    __shared__ int32_t lo[256];
-    for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x)
+    __shared__ int32_t lo_s[TPB / 64][256];
+    const int      lane = lane_id();
+    const uint32_t wave = threadIdx.x >> 6;
+    int32_t*       lo   = lo_s[wave];
+    for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
     {
-        lo[threadIdx.x] = -1;
-        __syncthreads();
-        const Piece    P = segs[s];
-        const uint8_t* p = in + P.off;
-        if (P.len == 4 * TPB && (P.off & 3) == 0)
+        const Piece P = segs[s];
+        reinterpret_cast<int4*>(lo)[lane] = make_int4(-1, -1, -1, -1);
+        const uint8_t* p    = in + P.off;
+        const uint32_t i0   = (uint32_t) lane * 16;
+        uint32_t       w[4] = {0, 0, 0, 0};
+        const uint32_t n    = P.len > i0 ? min(16u, P.len - i0) : 0u;
+        if (n == 16 && (((uintptr_t) (p + i0)) & 15) == 0)
         {
-            const uint32_t w    = reinterpret_cast<const uint32_t*>(p)[threadIdx.x];
-            const int32_t  base = (int32_t) threadIdx.x * 4;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-            {
-                const uint32_t c = (w >> (8 * i)) & 0xFF;
-                if (i == 3 || c != ((w >> (8 * i + 8)) & 0xFF))
-                    atomicMax(&lo[c], base + i);
-            }
-        }
-        else if (P.len == 8 * TPB && (P.off & 7) == 0)
-        {
-            // 8 consecutive bytes per thread: only the last byte of each equal run inside them
-            // updates LDS (post-BWT input is run-heavy, and same-address LDS atomics serialise)
-            const uint2    q    = reinterpret_cast<const uint2*>(p)[threadIdx.x];
-            const uint64_t w    = ((uint64_t) q.y << 32) | q.x;
-            const int32_t  base = (int32_t) threadIdx.x * 8;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-            {
-                const uint32_t c = (uint32_t) (w >> (8 * i)) & 0xFF;
-                if (i == 7 || c != ((uint32_t) (w >> (8 * i + 8)) & 0xFF))
-                    atomicMax(&lo[c], base + i);
-            }
+            const uint4 v = *reinterpret_cast<const uint4*>(p + i0);
+            w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
         }
         else
-            for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
-                atomicMax(&lo[p[i]], (int32_t) i);
-        __syncthreads();
-        state[(size_t) s * 256 + threadIdx.x] = lo[threadIdx.x] >= 0 ? (int32_t) P.start + lo[threadIdx.x] : -1;
-        __syncthreads();
+            for (uint32_t j = 0; j < n; ++j)
+                w[j >> 2] |= (uint32_t) p[i0 + j] << (8 * (j & 3));
+        wave_barrier_lds();
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j)
+        {
+            const uint32_t c  = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            const uint32_t cn = (w[(j + 1) >> 2 & 3] >> (8 * ((j + 1) & 3))) & 0xFFu;
+            if (j < n && (j + 1 == n || c != cn))
+                atomicMax(&lo[c], (int32_t) (i0 + j));
+        }
+        wave_barrier_lds();
+        const int4 v = reinterpret_cast<const int4*>(lo)[lane];
+        const int32_t st = (int32_t) P.start;
+        reinterpret_cast<int4*>(state + (size_t) s * 256)[lane] =
+            make_int4(v.x >= 0 ? st + v.x : -1, v.y >= 0 ? st + v.y : -1, v.z >= 0 ? st + v.z : -1, v.w >= 0 ? st + v.w : -1);
+        wave_barrier_lds();
     }
 }
 
@@ -84,14 +90,16 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
         int32_t        run = -1;
         const uint32_t c   = threadIdx.x;
         uint32_t       k   = 0;
-        for (; k + 8 <= ns; k += 8)
+        // 32 segment rows in flight per round (the scan is a chain of load latencies: 8 per round
+        // took 0.13 ms per batch)
+        for (; k + 32 <= ns; k += 32)
         {
-            int32_t v[8];
+            int32_t v[32];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 32; ++u)
                 v[u] = state[(size_t) (s0 + k + u) * 256 + c];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 32; ++u)
             {
                 state[(size_t) (s0 + k + u) * 256 + c] = run;
                 run                                    = max(run, v[u]);
@@ -1071,7 +1079,7 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     int32_t* st = reinterpret_cast<int32_t*>(w.state);
     {
         BRA_PROF(P_MTF_LASTOCC, s);
-        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(nseg, 65536)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
+        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
     }
     {
         BRA_PROF(P_MTF_SCAN, s);
