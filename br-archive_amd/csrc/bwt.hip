@@ -335,9 +335,22 @@ __global__ void __launch_bounds__(TPB) k_alpha(const uint8_t* __restrict__ in, c
         {
             const uint4    q    = reinterpret_cast<const uint4*>(p)[threadIdx.x];
             const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+            if (!__builtin_amdgcn_ballot_w64(((q.x | q.y | q.z | q.w) & 0x80808080u) != 0))
+            {
+                // the whole wave's bytes are < 128 (text): 4 mask words, half the selects
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                add((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+                for (int i = 0; i < 16; ++i)
+                {
+                    const uint32_t v = (w[i >> 2] >> (8 * (i & 3))) & 0x7Fu;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        m[k] |= ((v >> 5) == (uint32_t) k) ? (1u << (v & 31)) : 0u;
+                }
+            }
+            else
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    add((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
         }
         else
             for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
