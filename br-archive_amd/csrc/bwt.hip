@@ -1826,9 +1826,10 @@ __device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, 
     const uint32_t base = e0 & ~(2 * m - 1), kk = e0 - base;
     const uint4*   A    = X + base;
     const uint4*   B    = X + base + m;
-    // a pair of runs that is all padding (the left run starts with the padding key) stays as it is
-    const uint4 a0 = A[0];
-    if ((a0.x & a0.y & a0.z & a0.w) != ~0u)
+    // a pair whose right run is all padding (it starts with the padding key; then so is the left
+    // run if it does too) is already merged: it stays as it is
+    const uint4 b0 = B[0];
+    if ((b0.x & b0.y & b0.z & b0.w) != ~0u)
     {
         uint32_t lo = kk > m ? kk - m : 0u, hi = kk < m ? kk : m;  // i = outputs [0, kk) taken from A
         while (lo < hi)
