@@ -1220,7 +1220,15 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
     uint8_t*     win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageL0));  // TILE + 48 bytes, 16-aligned
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    // XCD-major tile order: workgroup w runs on XCD w % 8 and takes tiles from the XCD's contiguous
+    // eighth of the list, so the neighbouring output runs that adjacent tiles write to one digit's
+    // sub-bucket meet in the same L2 (in list order they went to eight different L2s and reached
+    // HBM as partial lines)
+    const bool     xm  = gridDim.x >= 8 && (gridDim.x & 7) == 0;
+    const uint32_t per = xm ? div_up(ntiles, 8u) : ntiles;
+    const uint32_t t0  = xm ? (blockIdx.x & 7) * per : 0u;
+    const uint32_t t1  = min(ntiles, t0 + per);
+    for (uint32_t t = t0 + (xm ? blockIdx.x >> 3 : blockIdx.x); t < t1; t += xm ? gridDim.x >> 3 : gridDim.x)
     {
         const L0Tile    T   = tiles[t];
         const BlockDesc B   = blocks[T.block];
@@ -3345,7 +3353,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
-        hipLaunchKernelGGL(k_l0_scatter, dim3(std::min<uint32_t>(nt0, grid)), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, w.packed, d_blocks,
+        hipLaunchKernelGGL(k_l0_scatter, dim3(nt0 >= 8 ? std::min<uint32_t>(nt0, grid) & ~7u : nt0), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, w.packed, d_blocks,
                            w.pkd, w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
