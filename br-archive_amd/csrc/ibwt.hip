@@ -113,11 +113,35 @@ __global__ void __launch_bounds__(TPB) k_ib_scan(const uint32_t* __restrict__ fi
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint32_t t0 = first[b], nt = count[b], c = threadIdx.x;
-        uint32_t       tot = 0;
-        for (uint32_t i = 0; i < nt; ++i)
+        uint32_t       tot = 0, i = 0;
+        // 16 tile rows in flight per round (one dependent load per tile made this a latency chain)
+        for (; i + 16 <= nt; i += 16)
+        {
+            uint32_t h[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                h[u] = th[(size_t) (t0 + i + u) * 256 + c];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                tot += h[u];
+        }
+        for (; i < nt; ++i)
             tot += th[(size_t) (t0 + i) * 256 + c];
         uint32_t run = block256_exclusive_sum(tot, tmp);
-        for (uint32_t i = 0; i < nt; ++i)
+        for (i = 0; i + 16 <= nt; i += 16)
+        {
+            uint32_t h[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                h[u] = th[(size_t) (t0 + i + u) * 256 + c];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+            {
+                th[(size_t) (t0 + i + u) * 256 + c] = run;
+                run += h[u];
+            }
+        }
+        for (; i < nt; ++i)
         {
             const size_t   o = (size_t) (t0 + i) * 256 + c;
             const uint32_t h = th[o];
