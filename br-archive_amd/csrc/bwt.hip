@@ -2108,7 +2108,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
 #endif
                 uint64_t      w0, w1;
-                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, depth - 1), w0, w1);
+                // workgroup jobs are single sub-buckets: byte d-1 is shared, the key starts at d
+                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, W > 1 ? depth : depth - 1), w0, w1);
 #endif
                 make_key1<W>(c, w0, w1, kh[r], kl[r]);
                 v[r] = ((uint32_t) lb << 24) | idx;
@@ -2144,7 +2145,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         km[r] = kl[r] & ~G::SMASK;
     }
     if (MODE == MODE_STRING)
-        depth += G::ADV1 - 1;
+        depth += (W > 1) ? G::ADV1 : G::ADV1 - 1;
     for (;;)
     {
         PH_T(t_r0);
