@@ -1031,7 +1031,9 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
                 {
                     const uint32_t slot = base_s[w][0] + jidx[r];
                     if (slot < a.cap_jobs)
-                        a.jobs[slot] = Job{s0, jlen[r], kd, obuf, B.block, B.gdepth, nd};
+                        // STRING: the kd field of a job flags a single sub-bucket (its keys can start at
+                        // the first unshared byte; jobs do not use kd otherwise)
+                        a.jobs[slot] = Job{s0, jlen[r], MODE == MODE_STRING ? (nxt[r] == li[r] + 1 ? 1u : 0u) : kd, obuf, B.block, B.gdepth, nd};
                     else
                         atomicExch(&a.ctr->overflow, 1u);
                 }
@@ -2067,6 +2069,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     bool            tied[4];
     uint32_t        T     = J.len;
     uint32_t        depth = (MODE == MODE_STRING) ? J.d : J.gdepth;
+    const bool      single = MODE == MODE_STRING && (W > 1 || J.kd == 1u);
     if (!BRA_DCHECK(T <= 256u * W && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job mode %u W %d start %u len %u block %u off %llu blen %u",
                     MODE, W, J.start, T, J.block, (unsigned long long) BD.off, BD.len))
         T = 0;
@@ -2108,8 +2111,9 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
 #endif
                 uint64_t      w0, w1;
-                // workgroup jobs are single sub-buckets: byte d-1 is shared, the key starts at d
-                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, W > 1 ? depth : depth - 1), w0, w1);
+                // a single sub-bucket (every workgroup job, flagged wave jobs) shares byte d-1: its
+                // key starts at d
+                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, single ? depth : depth - 1), w0, w1);
 #endif
                 make_key1<W>(c, w0, w1, kh[r], kl[r]);
                 v[r] = ((uint32_t) lb << 24) | idx;
@@ -2145,7 +2149,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         km[r] = kl[r] & ~G::SMASK;
     }
     if (MODE == MODE_STRING)
-        depth += (W > 1) ? G::ADV1 : G::ADV1 - 1;
+        depth += single ? G::ADV1 : G::ADV1 - 1;
     for (;;)
     {
         PH_T(t_r0);
