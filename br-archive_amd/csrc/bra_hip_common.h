@@ -230,6 +230,22 @@ __device__ __forceinline__ void wave_max_scan4(uint32_t (&x)[4])
         x[r] = max(x[r], ex);
 }
 
+// XCD-major tile ranges: workgroup w runs on XCD w % 8 and walks the XCD's contiguous eighth of
+// the tile list, so neighbouring tiles (whose outputs share boundary lines) run on one XCD and
+// meet in its L2.  Plain round robin when the grid is not a multiple of 8.
+struct XcdTiles
+{
+    uint32_t t, end, step;
+};
+__device__ __forceinline__ XcdTiles xcd_tiles(uint32_t ntiles)
+{
+    if (gridDim.x < 8 || (gridDim.x & 7) != 0)
+        return XcdTiles{blockIdx.x, ntiles, gridDim.x};
+    const uint32_t per = (ntiles + 7u) / 8u, t0 = (blockIdx.x & 7u) * per;
+    return XcdTiles{t0 + (blockIdx.x >> 3), min(ntiles, t0 + per), gridDim.x >> 3};
+}
+__host__ __device__ inline uint32_t xcd_grid(uint32_t g) { return g >= 8 ? g & ~7u : g; }
+
 // Value of x held by lane (lane ^ LM), LM in {1, 2, 4, 8, 16, 32}, without going through LDS:
 // DPP quad permutes / row rotate inside a row of 16 (one instruction each), xor 4 as two row shifts
 // writing complementary bank masks (lanes with bit 2 clear take lane + 4, the others lane - 4), and

@@ -453,7 +453,8 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
     __shared__ uint32_t tmp[8];
     __shared__ uint32_t img[PACK_WORDS];
     constexpr int       PT = RLE_TILE / TPB;
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    const XcdTiles X = xcd_tiles(ntiles);  // the boundary words two tiles OR into stay in one L2
+    for (uint32_t t = X.t; t < X.end; t += X.step)
     {
         const uint32_t nbits = tbits[t];
         if (nbits == 0)
@@ -1589,7 +1590,7 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
     }
     {
         BRA_PROF(P_HUF_PACK, s);
-        hipLaunchKernelGGL(k_huff_pack, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.codes, w.tbits, w.tbit0, words);
+        hipLaunchKernelGGL(k_huff_pack, dim3(xcd_grid(grid)), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.codes, w.tbits, w.tbit0, words);
     }
     BRA_HIP_CHECK(hipGetLastError());
     return true;

@@ -436,7 +436,8 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
     __shared__ uint8_t  stage[RLE_TILE + RLE_TILE / 64 + 64];
     constexpr int       HC = 4, HS = 256 + 16;  // histogram copies (lane & 3), 16 banks apart: output bytes are skewed
     __shared__ uint32_t h[HC * HS];
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    const XcdTiles X = xcd_tiles(ntiles);
+    for (uint32_t t = X.t; t < X.end; t += X.step)
     {
         const Piece    P = tiles[t];
         const TileOff  O = to[t];
@@ -513,7 +514,7 @@ bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_
     }
     {
         BRA_PROF(P_RLE_WRITE, s);
-        hipLaunchKernelGGL(k_rle_write, dim3(grid), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, link, offs, d_rle_base, d_out, d_hist);
+        hipLaunchKernelGGL(k_rle_write, dim3(xcd_grid(grid)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nt, link, offs, d_rle_base, d_out, d_hist);
     }
     if (g_prof && g_prof->mask)
     {
