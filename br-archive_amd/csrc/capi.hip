@@ -413,7 +413,7 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
     uint32_t* d_dec_size = c->d_hist;           // nb words
     {
         BRA_PROF(P_DEC_RLE, s);
-        if (!rle_decode_device(c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, s))
+        if (!rle_decode_device(c->rle, rsz.data(), c->d_rle, d_rbase, c->d_rle_size, nb, c->d_mtf, d_outb, d_outcap, d_dec_size, s))
             return -1;
     }
     if (g_prof)
@@ -1204,7 +1204,7 @@ static bool rle_decode_one(bra_gpu_ctx_s* c, const uint8_t* buf, size_t buf_size
         hipMemcpyAsync(c->d_aux, &zero, 8, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemcpyAsync(c->d_rle_size, &sz, 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return false;
-    if (!rle_decode_device(c->d_io, c->d_rle_base, c->d_rle_size, 1, c->d_tmp, c->d_aux, c->d_rle_cap, c->d_status, c->stream))
+    if (!rle_decode_device(c->rle, &sz, c->d_io, c->d_rle_base, c->d_rle_size, 1, c->d_tmp, c->d_aux, c->d_rle_cap, c->d_status, c->stream))
         return false;
     return download(c, dec_size, c->d_status, 4);
 }

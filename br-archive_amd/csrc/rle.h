@@ -18,7 +18,10 @@ struct RleWorkspace
     void*    gaps = nullptr;
     void*    offs = nullptr;
     uint32_t cap  = 0;
+    void*    dmap = nullptr;  // decode: segment entry maps and segment states
+    uint64_t dmap_cap = 0;
     bool     reserve(uint32_t ntiles);
+    bool     reserve_decode(uint64_t bytes);
     void     release();
 };
 
@@ -27,10 +30,11 @@ struct RleWorkspace
 bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_blocks, uint32_t nblocks, const uint64_t* d_rle_base,
                        uint8_t* d_out, uint32_t* d_rle_size, uint32_t* d_hist, hipStream_t s);
 
-// Decode: block b's stream is at d_in + d_in_base[b] (d_in_size[b] bytes); output goes to
+// Decode: block b's stream is at d_in + d_in_base[b] (d_in_size[b] bytes; h_in_size: the same
+// sizes on the host, used to split long streams into segments decoded in parallel); output goes to
 // d_out + d_out_base[b] (capacity d_out_cap[b]; writes past it are dropped).  d_out_size[b] =
 // decoded size, 0 on a malformed stream (bra_rle_decode_compute_size semantics).
-bool rle_decode_device(const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
+bool rle_decode_device(RleWorkspace& w, const uint32_t* h_in_size, const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
                        const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, hipStream_t s);
 
 }  // namespace bra

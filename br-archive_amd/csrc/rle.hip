@@ -543,9 +543,24 @@ bool RleWorkspace::reserve(uint32_t ntiles)
     return true;
 }
 
+bool RleWorkspace::reserve_decode(uint64_t bytes)
+{
+    if (bytes <= dmap_cap)
+        return true;
+    dmap_cap         = 0;
+    const uint64_t c = bytes + bytes / 4 + 4096;
+    if (!dev_alloc_bytes(dmap, c))
+        return false;
+    dmap_cap = c;
+    return true;
+}
+
 void RleWorkspace::release()
 {
     tiling.release();
+    (void) hipFree(dmap);
+    dmap     = nullptr;
+    dmap_cap = 0;
     (void) hipFree(runs);
     (void) hipFree(link);
     (void) hipFree(gaps);

@@ -17,6 +17,15 @@
 //      with their output offsets, and writes its output range: each lane finds the control of its
 //      16 output bytes (binary search + forward steps) and takes them from the staged window.
 // Everything stays in LDS; the next window's bytes are loaded while the current one is decoded.
+//
+// Few long streams (e.g. 32 blocks of 8 MiB) would leave most CUs idle, so such batches split every
+// stream into segments of whole windows, one workgroup each, in three launches:
+//   a. k_rled<MAP>: for each of the RD_NENT entry offsets a chain can have into the segment (the
+//      last control before it steps at most 129 bytes), its exit into the next segment and its
+//      output bytes -- phase 1 as above plus phase 2 run by one lane per entry;
+//   b. k_rled_link: one lane per block chains its segments through the maps: every segment's
+//      entry and output offset, and the decoded size / error check;
+//   c. k_rled<DEC>: the decode above, each segment from its entry.
 #include "prof.h"
 #include "rle.h"
 
@@ -31,6 +40,7 @@ constexpr uint32_t RD_PER   = RD_SUB / 64;          // positions per lane
 constexpr uint32_t RD_WIN   = RD_WAVES * RD_SUB;    // 16 KiB window
 constexpr uint32_t RD_HALO  = 256;                  // a literal's payload runs up to 128 bytes past its window
 constexpr uint32_t RD_LOAD  = (RD_WIN + RD_HALO) / 16;  // 16-byte loads per window (<= 2 per thread)
+constexpr uint32_t RD_NENT  = 129;                  // entry offsets into a segment: [0, 128]
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -55,10 +65,20 @@ __device__ __forceinline__ uint4 load16(const uint8_t* __restrict__ src, uint32_
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Segments of a batch: block b's segment j (j < nseg) starts at stream offset j * seg_bytes (a
+// multiple of RD_WIN); nseg == 1: whole blocks, entry 0, the decoded size written here.
+struct RledSeg
+{
+    uint32_t nseg, seg_bytes;
+    uint2*   map;    // MAP: [(b * nseg + j) * RD_NENT + entry] = (exit offset past the segment's last window, output bytes)
+    uint2*   state;  // [b * nseg + j] = (entry offset, block output offset) (k_rled_link)
+};
+
+template <bool MAP>
 __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_base,
                                                  const uint32_t* __restrict__ in_size, uint32_t nblocks, uint8_t* __restrict__ out,
                                                  const uint64_t* __restrict__ out_base, const uint64_t* __restrict__ out_cap,
-                                                 uint32_t* __restrict__ out_size)
+                                                 uint32_t* __restrict__ out_size, RledSeg sg)
 {
     __shared__ uint4    win4[1 + (RD_WIN + RD_HALO) / 16];  // one 16-byte pad in front: unaligned output reads start up to 15 bytes early
     __shared__ uint16_t NX[RD_WAVES][RD_SUB];  // successor (sub-window position; >= len: exit) / later: chain positions
@@ -70,26 +90,35 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
     const int      lane = lane_id();
     const uint32_t k    = threadIdx.x >> 6;  // this wave's sub-window
     const uint64_t below = (1ull << lane) - 1ull;
-    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    const uint64_t nunits = (uint64_t) nblocks * sg.nseg;
+    for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x)
     {
+        const uint32_t b    = (uint32_t) (u / sg.nseg);
+        const uint32_t seg0 = (uint32_t) (u % sg.nseg) * sg.seg_bytes;
         const uint8_t* src  = in + in_base[b];
         const uint32_t size = in_size[b];
+        if (sg.nseg > 1 && seg0 >= size)
+            continue;  // no such segment (uniform over the workgroup)
+        const uint32_t seg1 = sg.nseg > 1 ? min(size, seg0 + sg.seg_bytes) : size;
         uint8_t*       dst  = out + out_base[b];
         const uint64_t cap  = out_cap[b];
-        if (threadIdx.x == 0)
+        // MAP: lane t < RD_NENT follows the chain entering the segment at offset t
+        uint32_t me = threadIdx.x, mo = 0;
+        if (!MAP && threadIdx.x == 0)
         {
-            sh_E = 0;
-            sh_O = 0;
+            const uint2 st = sg.nseg > 1 ? sg.state[u] : make_uint2(0, 0);
+            sh_E           = st.x;
+            sh_O           = st.y;
         }
-        // prefetch window 0
+        // prefetch the segment's first window
         uint4 pf[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
         {
             const uint32_t t = threadIdx.x + h * RD_TPB;
-            pf[h]            = t < RD_LOAD ? load16(src, size, t * 16) : make_uint4(0, 0, 0, 0);
+            pf[h]            = t < RD_LOAD ? load16(src, size, seg0 + t * 16) : make_uint4(0, 0, 0, 0);
         }
-        for (uint32_t w0 = 0; w0 < size; w0 += RD_WIN)
+        for (uint32_t w0 = seg0; w0 < seg1; w0 += RD_WIN)
         {
             __syncthreads();  // previous window fully consumed
 #pragma unroll
@@ -101,7 +130,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             }
             __syncthreads();
             // prefetch the next window while this one is decoded
-            if (w0 + RD_WIN < size)
+            if (w0 + RD_WIN < seg1)
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
                 {
@@ -166,6 +195,26 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             __syncthreads();
 
             // ---- 2. entries and output offsets of the sub-windows ----
+            if (MAP)
+            {
+                // every entry's chain through the 16 sub-windows
+                if (threadIdx.x < RD_NENT)
+                {
+                    uint32_t e = me;
+                    for (uint32_t q = 0; q < RD_WAVES; ++q)
+                    {
+                        const uint32_t qb = q * RD_SUB;
+                        const uint32_t ql = rem > qb ? min(RD_SUB, rem - qb) : 0u;
+                        if (e - qb < ql)
+                        {
+                            mo += SM[q][e - qb];
+                            e = qb + NX[q][e - qb];
+                        }
+                    }
+                    me = e - RD_WIN;
+                }
+                continue;  // the loop head's barrier orders these reads before the next window's writes
+            }
             if (threadIdx.x == 0)
             {
                 uint32_t e = sh_E, o = sh_O;  // e: window offset of the next control
@@ -312,7 +361,12 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (MAP)
+        {
+            if (threadIdx.x < RD_NENT)
+                sg.map[u * RD_NENT + threadIdx.x] = make_uint2(me, mo);
+        }
+        else if (sg.nseg == 1 && threadIdx.x == 0)
         {
             // the chain must end exactly at the end of the stream (sh_E = its overshoot past the
             // window holding the stream end, measured from that window's end: recompute it)
@@ -324,14 +378,82 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
     }
 }
 
+// One lane per block: chain the segments through their entry maps (a segment ends with a whole
+// window, so the exit offset past it is the next segment's entry, in [0, 128] for a stream that
+// continues), record each segment's entry and output offset, and the decoded size (0 unless the
+// chain ends exactly at the end of the stream, as in k_rled).
+__global__ void k_rled_link(const uint32_t* __restrict__ in_size, uint32_t nblocks, uint32_t* __restrict__ out_size, RledSeg sg)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t size = in_size[b];
+    if (size == 0)
+    {
+        out_size[b] = 0;
+        return;
+    }
+    const uint32_t nj = (size - 1) / sg.seg_bytes + 1;  // <= nseg (the host sized nseg for the largest stream)
+    uint32_t       e = 0, o = 0;
+    bool           ok = true;
+    for (uint32_t j = 0; j < nj; ++j)
+    {
+        const uint64_t u = (uint64_t) b * sg.nseg + j;
+        if (e >= RD_NENT)
+        {
+            ok = false;  // only a malformed stream's chain can skip past a segment's first 129 bytes
+            e  = 0;
+        }
+        sg.state[u]   = make_uint2(e, o);
+        const uint2 m = sg.map[u * RD_NENT + e];
+        o += m.y;
+        e = m.x;
+    }
+    const uint32_t last_w0 = ((size - 1) / RD_WIN) * RD_WIN;
+    const uint32_t over    = (e + RD_WIN) - (size - last_w0);
+    out_size[b]            = (!ok || over != 0) ? 0u : o;
+}
+
 }  // namespace
 
-bool rle_decode_device(const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size, uint32_t nblocks, uint8_t* d_out,
-                       const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size, hipStream_t s)
+bool rle_decode_device(RleWorkspace& w, const uint32_t* h_in_size, const uint8_t* d_in, const uint64_t* d_in_base, const uint32_t* d_in_size,
+                       uint32_t nblocks, uint8_t* d_out, const uint64_t* d_out_base, const uint64_t* d_out_cap, uint32_t* d_out_size,
+                       hipStream_t s)
 {
     BRA_PROF(P_DEC_RLED, s);
-    hipLaunchKernelGGL(k_rled, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks, d_out,
-                       d_out_base, d_out_cap, d_out_size);
+    // segments (about RD_TARGET_WG workgroups over the batch) only when the blocks alone would leave
+    // at least half of the 256 CUs idle: the map pass costs about as much as the decode itself
+    // (256 x 1 MiB text: 2.13 ms whole blocks, 3.26 ms in segments; 32 x 8 MiB sym16: 21.2 -> 4.0 ms)
+    constexpr uint32_t RD_TARGET_WG = 512, RD_SEG_MAX_BLOCKS = 128;
+    uint32_t           maxsz        = 0;
+    for (uint32_t b = 0; h_in_size && b < nblocks; ++b)
+        maxsz = std::max(maxsz, h_in_size[b]);
+    RledSeg sg{1, 0, nullptr, nullptr};
+    if (h_in_size && nblocks <= RD_SEG_MAX_BLOCKS && maxsz > 2 * RD_WIN)
+    {
+        const uint32_t want = div_up(RD_TARGET_WG, nblocks);
+        const uint32_t wins = div_up(maxsz, RD_WIN);
+        const uint32_t per  = std::max(4u, div_up(wins, std::min(want, wins)));  // windows per segment (>= 64 KiB: short link chains)
+        sg.seg_bytes        = per * RD_WIN;
+        sg.nseg             = div_up(maxsz, sg.seg_bytes);
+    }
+    if (sg.nseg > 1)
+    {
+        const uint64_t units = (uint64_t) nblocks * sg.nseg;
+        if (!w.reserve_decode(units * (RD_NENT + 1) * sizeof(uint2)))
+            return false;
+        sg.map   = static_cast<uint2*>(w.dmap);
+        sg.state = sg.map + units * RD_NENT;
+        const uint32_t g = (uint32_t) std::min<uint64_t>(units, 65535);
+        hipLaunchKernelGGL(k_rled<true>, dim3(g), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks, d_out, d_out_base, d_out_cap,
+                           d_out_size, sg);
+        hipLaunchKernelGGL(k_rled_link, dim3(div_up(nblocks, 64u)), dim3(64), 0, s, d_in_size, nblocks, d_out_size, sg);
+        hipLaunchKernelGGL(k_rled<false>, dim3(g), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks, d_out, d_out_base, d_out_cap,
+                           d_out_size, sg);
+    }
+    else
+        hipLaunchKernelGGL(k_rled<false>, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks,
+                           d_out, d_out_base, d_out_cap, d_out_size, sg);
     BRA_HIP_CHECK(hipGetLastError());
     return true;
 }

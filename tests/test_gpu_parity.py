@@ -59,6 +59,34 @@ def test_kat_rle(bra):
     assert bra.rle_decode(bytes([0xFE])) is None
 
 
+def test_rle_decode_segmented(bra, orc):
+    """Streams longer than two 16 KiB windows are decoded in segments chained through per-entry exit
+    maps (csrc/rle_decode.hip): literal-heavy, run-heavy and mixed streams, no-op controls and
+    literals across segment boundaries, truncated / overlong / random streams -- decoded bytes and
+    bra_rle_decode_compute_size against the oracle (bra_rle.c:122-224)."""
+    rng = np.random.default_rng(11)
+    lit = rng.integers(0, 256, 700_000, dtype=np.uint8).tobytes()
+    runs = np.repeat(rng.integers(0, 4, 40_000, dtype=np.uint8), rng.integers(1, 200, 40_000)).tobytes()
+    mixed = b"".join(lit[i:i + 300] + runs[i:i + 900] for i in range(0, 300_000, 1200))
+    streams = [orc.rle_encode(x) for x in (lit, runs, mixed, bytes(4 << 20))]
+    # -128 no-ops around the segment boundaries (multiples of 64 KiB) and a 128-byte literal
+    # whose successor lands exactly 128 bytes into a segment
+    s = bytearray(orc.rle_encode(lit[:200_000]))
+    s[65536 - 3:65536 - 3] = bytes([0x80] * 5)
+    streams.append(bytes(s))
+    s = bytearray(orc.rle_encode(runs[:150_000]))
+    pos = 131072 - 1
+    s[pos:pos] = bytes([127]) + lit[:128]
+    streams.append(bytes(s))
+    bad = [streams[0][:-1], streams[1] + bytes([0xFE]), streams[2][:-5] + bytes([0x7F])]
+    bad += [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (40_000, 70_001, 300_000, 300_001)]
+    for x in streams + bad:
+        ref = orc.rle_decode(x)
+        assert bra.rle_decode_compute_size(x) == (len(ref) if ref is not None else 0), len(x)
+        assert bra.rle_decode(x) == ref, len(x)
+    assert all(orc.rle_decode(x) is not None for x in streams[:4])
+
+
 def test_kat_huffman(bra):
     h = bra.huffman_encode(b"BANANA")
     assert (h.orig_size, h.encoded_size) == (6, 2)
