@@ -999,6 +999,9 @@ __global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks
 //   k_hd_tail2   per block: the reference's end-of-stream walk (:455-498) on the intervals.
 // Any block that is not clean sends the batch to the tree-walking path above.
 // ------------------------------------------------------------------------------------------------
+#ifndef HD2_PAIRS
+#define HD2_PAIRS 1  // k_hd_trans walks the entries > 0 two at a time (3 or 4 in lockstep measured slower: occupancy)
+#endif
 constexpr uint32_t HD2_SEG   = 2048;  // bits per segment
 constexpr uint32_t HD2_LMAX  = 30;
 constexpr uint32_t HD2_TPB   = 256;
@@ -1141,10 +1144,11 @@ __device__ __forceinline__ void hd2_load_tables(const uint32_t* __restrict__ T, 
     __syncthreads();
 }
 
-// One codeword from the left-justified 32 bits v: length and symbol, false on a dead edge.
-__device__ __forceinline__ bool hd2_dec(const Hd2Lds& L, uint32_t v, uint32_t& len, uint32_t& sym)
+// One codeword from the left-justified 32 bits v and its primary LUT entry e = L.lut[v >> 21]:
+// length and symbol, false on a dead edge.
+__device__ __forceinline__ bool hd2_dec_e(const Hd2Lds& L, uint32_t v, uint32_t e, uint32_t& len, uint32_t& sym)
 {
-    const uint32_t e = L.lut[v >> 21], kind = e >> 13;
+    const uint32_t kind = e >> 13;
     if (kind == 0)
     {
         len = (e >> 8) & 31u;
@@ -1161,6 +1165,12 @@ __device__ __forceinline__ bool hd2_dec(const Hd2Lds& L, uint32_t v, uint32_t& l
             return true;
         }
     return false;
+}
+
+// One codeword from the left-justified 32 bits v: length and symbol, false on a dead edge.
+__device__ __forceinline__ bool hd2_dec(const Hd2Lds& L, uint32_t v, uint32_t& len, uint32_t& sym)
+{
+    return hd2_dec_e(L, v, L.lut[v >> 21], len, sym);
 }
 
 // The bits of one block seen through a 4-dword window (MSB-first, byte-swapped dwords).  Block bit p
@@ -1195,9 +1205,11 @@ struct BitWin
             W[3] = ld((wb >> 5) + 3);
             o -= 32;
         }
-        const uint32_t i = o >> 5, sh = o & 31;
-        const uint32_t a = i == 0 ? W[0] : i == 1 ? W[1] : W[2];
-        const uint32_t c = i == 0 ? W[1] : i == 1 ? W[2] : W[3];
+        // o < 64 here (a codeword moves p by <= 30 bits): dword o >> 5 is W[0] or W[1]; the choice
+        // is made with masks (a select chain was turned into an indexed scratch load)
+        const uint32_t m = 0u - (o >> 5), sh = o & 31;
+        const uint32_t a = W[0] ^ ((W[0] ^ W[1]) & m);
+        const uint32_t c = W[1] ^ ((W[1] ^ W[2]) & m);
         return (uint32_t) ((((uint64_t) a << 32) | c) >> (32 - sh));
     }
 };
@@ -1264,6 +1276,75 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
         }
         const uint32_t c0 = c, r0 = (bad << 31) | (((p - stop) & 31u) << 16);
         out[0]               = r0 | c0;
+#if HD2_PAIRS
+        // the other entries two at a time in lockstep: both paths' window loads and LUT reads are
+        // issued before either result is used (one path's step is a dependent load chain)
+        for (uint32_t e = 1; e < nent; e += 2)
+        {
+            const bool two = e + 1 < nent;
+            BitWin     WA = hd2_win(payload, payload_off[b], nbytes), WB = hd2_win(payload, payload_off[b], nbytes);
+            uint32_t   pa = s + e, pb = s + (two ? e + 1 : e), ca = 0, cb = 0, ra = 0, rb = 0;
+            bool       la = true, lb = two;
+            WA.init(pa);
+            WB.init(pb);
+            // end / merge checks of one path (registers only)
+            const auto check = [&](uint32_t pq, uint32_t cq, uint32_t& rq, bool& lq) __attribute__((always_inline)) {
+                if (!lq)
+                    return;
+                if (pq >= stop)
+                {
+                    rq = (((pq - stop) & 31u) << 16) | cq;
+                    lq = false;
+                    return;
+                }
+                const uint32_t d = pq - s;
+                if (d < HD2_REFB)
+                {
+                    uint32_t wsel = 0;
+#pragma unroll
+                    for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                        wsel = (d >> 5) == (uint32_t) i ? bm[i] : wsel;
+                    if ((wsel >> (d & 31)) & 1u)
+                    {
+                        uint32_t rank = 0;
+#pragma unroll
+                        for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                        {
+                            const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
+                            rank += (uint32_t) __popc(bm[i] & m);
+                        }
+                        rq = r0 | (cq + c0 - rank);
+                        lq = false;
+                    }
+                }
+            };
+            const auto advance = [&](uint32_t v, uint32_t le, uint32_t& pq, uint32_t& cq, uint32_t& rq, bool& lq) __attribute__((always_inline)) {
+                if (!lq)
+                    return;
+                uint32_t len, sym;
+                if (!hd2_dec_e(L, v, le, len, sym) || len > nbits - pq)
+                {
+                    rq = (1u << 31) | (((pq - stop) & 31u) << 16) | cq;
+                    lq = false;
+                    return;
+                }
+                pq += len;
+                ++cq;
+            };
+            while (la || lb)
+            {
+                check(pa, ca, ra, la);
+                check(pb, cb, rb, lb);
+                const uint32_t va = WA.peek(pa), vb = WB.peek(pb);
+                const uint32_t ea = L.lut[va >> 21], eb = L.lut[vb >> 21];
+                advance(va, ea, pa, ca, ra, la);
+                advance(vb, eb, pb, cb, rb, lb);
+            }
+            out[e] = ra;
+            if (two)
+                out[e + 1] = rb;
+        }
+#else
         for (uint32_t e = 1; e < nent; ++e)
         {
             W.init(s + e);
@@ -1276,16 +1357,20 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
                 const uint32_t d = p - s;
                 if (d < HD2_REFB)
                 {
-                    uint32_t hit = 0, rank = 0;
+                    // hit test on the one bitmap word (a select chain), the rank only on a hit
+                    uint32_t wsel = 0;
 #pragma unroll
                     for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                        wsel = (d >> 5) == (uint32_t) i ? bm[i] : wsel;
+                    if ((wsel >> (d & 31)) & 1u)
                     {
-                        const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
-                        rank += (uint32_t) __popc(bm[i] & m);
-                        hit |= (d >> 5) == (uint32_t) i ? (bm[i] >> (d & 31)) & 1u : 0u;
-                    }
-                    if (hit)
-                    {
+                        uint32_t rank = 0;
+#pragma unroll
+                        for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                        {
+                            const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
+                            rank += (uint32_t) __popc(bm[i] & m);
+                        }
                         out[e] = r0 | (c + c0 - rank);
                         merged = true;
                         break;
@@ -1302,6 +1387,7 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
             if (!merged)
                 out[e] = (bad << 31) | (((p - stop) & 31u) << 16) | c;
         }
+#endif
     }
 }
 
