@@ -1823,6 +1823,9 @@ __device__ __forceinline__ bool key_le(const uint4& a, const uint4& b)
 // about 40 VALU per element and level instead of the ~230 of the bitonic phases it replaces
 // (log2(2m) compare-exchange stages, cross-wave ones through LDS with two barriers each).  Equal
 // keys (padding) take the left run first.
+#ifndef BRA_MERGE_ARY
+#define BRA_MERGE_ARY 2  // co-rank search arity (2: binary)
+#endif
 template <int W, int KD>
 __device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0, uint32_t m)
 {
@@ -1842,6 +1845,32 @@ __device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, 
     if ((b0.x & b0.y & b0.z & b0.w) != ~0u)
     {
         uint32_t lo = kk > m ? kk - m : 0u, hi = kk < m ? kk : m;  // i = outputs [0, kk) taken from A
+#if BRA_MERGE_ARY > 2
+        // K-ary search: K - 1 independent probe pairs per step (fewer dependent LDS round trips)
+        constexpr uint32_t K = BRA_MERGE_ARY;
+        while (lo < hi)
+        {
+            const uint32_t len = hi - lo;
+            uint32_t       q[K - 1];
+            bool           pr[K - 1];
+#pragma unroll
+            for (uint32_t t = 0; t < K - 1; ++t)
+            {
+                q[t]  = lo + ((t + 1) * len) / K;
+                pr[t] = key_le(A[q[t]], B[kk - 1 - q[t]]);
+            }
+            uint32_t nlo = q[K - 2] + 1, nhi = hi;  // all probes true: past the last one
+#pragma unroll
+            for (int t = K - 2; t >= 0; --t)
+                if (!pr[t])
+                {
+                    nhi = q[t];
+                    nlo = t ? q[t - 1] + 1 : lo;
+                }
+            lo = nlo;
+            hi = nhi;
+        }
+#else
         while (lo < hi)
         {
             const uint32_t mid = (lo + hi) >> 1;
@@ -1850,6 +1879,7 @@ __device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, 
             else
                 hi = mid;
         }
+#endif
         uint32_t i = lo, j = kk - lo;
         uint4    a = A[min(i, m - 1)], b = B[min(j, m - 1)];
 #pragma unroll
