@@ -233,6 +233,40 @@ def test_batch_duplicated_regions(bra, codec, orc, bs, x):
     _encode_check(bra, codec, orc, _dup_blocks(rng, bs, x, text), bs)
 
 
+def _alphabet_block(rng, bs: int, vals: np.ndarray) -> np.ndarray:
+    """A block over the byte values vals, Zipf-weighted, with a 300-byte phrase repeated 6 times (ties
+    that go past the first MSD levels)."""
+    w = 1.0 / np.arange(1, vals.size + 1)
+    blk = vals[rng.choice(vals.size, bs, p=w / w.sum())].astype(np.uint8)
+    if bs >= 4096:
+        ph = blk[:300].copy()
+        for j in range(6):
+            at = int(rng.integers(0, bs - 300))
+            blk[at: at + 300] = ph
+    return blk
+
+
+@pytest.mark.parametrize("bs", [65536, 512 << 10])
+def test_batch_alphabets(bra, codec, orc, bs):
+    """Packed key strings (b = ceil(log2 |alphabet|) bits per character, csrc/bwt.hip k_alpha/k_pack):
+    alphabet sizes on both sides of every power of two, non-contiguous value sets, sets entirely at
+    or above 128 (the 4-mask-word path covers only bytes below 128), one byte >= 128 among text --
+    every block against the oracle."""
+    rng = np.random.default_rng(bs ^ 0x5EED)
+    sizes = [2, 3, 4, 5, 8, 9, 16, 17, 32, 33, 64, 65, 127, 128, 129, 200, 255, 256] if bs == 65536 else [2, 9, 33, 129, 256]
+    blocks = []
+    for k in sizes:
+        blocks.append(_alphabet_block(rng, bs, np.sort(rng.choice(256, k, replace=False))))
+    blocks.append(_alphabet_block(rng, bs, np.array([0, 255])))
+    blocks.append(_alphabet_block(rng, bs, np.arange(128, 256)))
+    blocks.append(_alphabet_block(rng, bs, np.array([7, 200, 201])))
+    t = bra.synth_fill(0, bs, bs, first_block=9).copy()
+    t[bs // 3] = 0xE9  # one byte >= 128 inside text
+    blocks.append(t)
+    data = np.concatenate(blocks + [_alphabet_block(rng, bs // 3 + 5, np.arange(40, 45))])
+    _encode_check(bra, codec, orc, data, bs)
+
+
 def test_config1_tiled_block(bra, codec, golden):
     import torch
 
