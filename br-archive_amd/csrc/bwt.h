@@ -13,4 +13,8 @@ void          bwt_workspace_destroy(BwtWorkspace* w);
 bool bwt_encode_device(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s);
 
+// BWT of one block of any length >= 1 (bwt_large.hip: prefix doubling with rocPRIM radix sorts), used
+// by the single-block C-ABI for blocks of 2^24 bytes or more; synchronises the stream.
+bool bwt_encode_large(const uint8_t* d_in, uint32_t n, uint8_t* d_L, uint32_t* d_pi, hipStream_t s);
+
 }  // namespace bra

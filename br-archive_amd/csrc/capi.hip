@@ -1046,6 +1046,9 @@ bool bra_bwt_encode2(const uint8_t* buf, const bra_bwt_index_t buf_size, bra_bwt
     auto hb = one_block(buf_size);
     if (!ensure_block_arrays(c, 1) || !grow(c->d_L, c->cap_L, (uint64_t) buf_size + 16))
         return false;
+    if (buf_size >= (1u << 24))  // past the batched path's 24-bit rotation indices
+        return bwt_encode_large(c->d_io, buf_size, c->d_L, c->d_pi, c->stream) && download(c, primary_index, c->d_pi, 4) &&
+               download(c, out_buf, c->d_L, buf_size);
     if (hipMemcpyAsync(c->d_blocks, hb.data(), sizeof(BlockDesc), hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return false;
     if (!bwt_encode_device(c->bwt, c->d_io, c->d_blocks, hb.data(), 1, c->d_L, c->d_pi, c->stream))

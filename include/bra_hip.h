@@ -51,7 +51,8 @@ typedef struct bra_io_chunk_header_t
 /* ---- Part 1: reference encoder ABI ---------------------------------------------------------- */
 /* replaces src/encoders/bra_bwt.h:42  (bra_bwt.c:57-71)   */
 uint8_t* bra_bwt_encode(const uint8_t* buf, const bra_bwt_index_t buf_size, bra_bwt_index_t* primary_index);
-/* replaces src/encoders/bra_bwt.h:63  (bra_bwt.c:73-108)  */
+/* replaces src/encoders/bra_bwt.h:63  (bra_bwt.c:73-108); any length >= 1 (blocks of 2^24 bytes or
+   more take the prefix-doubling path of csrc/bwt_large.hip) */
 bool bra_bwt_encode2(const uint8_t* buf, const bra_bwt_index_t buf_size, bra_bwt_index_t* primary_index, uint8_t* out_buf);
 /* replaces src/encoders/bra_bwt.h:93  (bra_bwt.c:110-131) */
 uint8_t* bra_bwt_decode(const uint8_t* buf, const bra_bwt_index_t buf_size, const bra_bwt_index_t primary_index);

@@ -342,3 +342,24 @@ def test_huffman_code_lengths_over_32(bra):
     assert (ch.orig_size, ch.encoded_size) == (g["orig_size"], g["encoded_size"])
     assert hashlib.sha256(ch.data).hexdigest() == g["payload_sha256"]
     assert bra.huffman_decode(ch.lengths, ch.orig_size, ch.encoded_size, ch.data) is None
+
+
+def test_bwt_single_block_past_2_24(bra, orc):
+    """bra_bwt_encode2 on blocks of 2^24 bytes or more (csrc/bwt_large.hip; the reference takes any
+    u32 length, bra_bwt.c:73-108): text and uniform random blocks against the oracle, a periodic
+    block's pi against its closed form (the start of rotation 0's group of identical rotations),
+    all-zero bytes, and round trips through bra_bwt_decode2."""
+    n = (1 << 24) + 3
+    for kind in (0, 1):
+        x = bra.synth_fill(kind, n, n).tobytes()
+        L, pi = bra.bwt_encode(x)
+        assert (L, pi) == orc.bwt_encode(x), kind
+        assert bra.bwt_decode(L, pi) == x, kind
+    p = b"abracadabra"
+    k = (17 << 20) // len(p)
+    x = p * k
+    L, pi = bra.bwt_encode(x)
+    assert pi == k * sum(p[i:] + p[:i] < p for i in range(len(p)))
+    assert bra.bwt_decode(L, pi) == x
+    L, pi = bra.bwt_encode(bytes(1 << 24))
+    assert (L, pi) == (bytes(1 << 24), 0)
