@@ -725,6 +725,9 @@ struct ScanArgs
 #define BRA_SCAN_WAVES 4   // 16 and 8 measured slower (waves of one workgroup wait for its largest bucket)
 #endif
 constexpr int SCAN_WAVES = BRA_SCAN_WAVES;
+#ifndef BRA_SCAN_PREFETCH
+#define BRA_SCAN_PREFETCH 0  // 1: prefetch the next pass's bucket descriptor
+#endif
 #ifndef BRA_SCAN_MIN_WAVES
 #define BRA_SCAN_MIN_WAVES 1  // min waves per SIMD the scan is compiled for (1: compiler choice, 143 VGPRs)
 #endif  // buckets (waves) per scan workgroup
@@ -744,13 +747,28 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
     __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
     const int                 lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t            nbuckets = a.lin ? dev_count(&a.lin->n_big) : a.nbuckets;
-    for (uint32_t b0 = blockIdx.x * SCAN_WAVES; b0 < nbuckets; b0 += gridDim.x * SCAN_WAVES)
+    const uint32_t            bstride  = gridDim.x * SCAN_WAVES;
+#if BRA_SCAN_PREFETCH
+    // the next pass's bucket descriptor is loaded while this pass works (one dependent round trip
+    // less per bucket: descriptor -> tile rows)
+    Bucket Bn{};
+    if (blockIdx.x * SCAN_WAVES + w < nbuckets)
+        Bn = a.buckets[blockIdx.x * SCAN_WAVES + w];
+#endif
+    for (uint32_t b0 = blockIdx.x * SCAN_WAVES; b0 < nbuckets; b0 += bstride)
     {
         const uint32_t bi     = b0 + w;
         const bool     active = bi < nbuckets;
         Bucket         B{};
+#if BRA_SCAN_PREFETCH
+        if (active)
+            B = Bn;
+        if (bi + bstride < nbuckets)
+            Bn = a.buckets[bi + bstride];
+#else
         if (active)
             B = a.buckets[bi];
+#endif
 #ifdef BRA_DEBUG
         if (active && lane == 0)
         {
