@@ -1110,7 +1110,8 @@ bool bra_mtf_encode2(const uint8_t* buf, const size_t buf_size, uint8_t* out_buf
     bra_gpu_ctx_s* c = lease.ctx;
     if (!c || !upload(c, buf, buf_size) || !grow(c->d_mtf, c->cap_mtf, (uint64_t) buf_size + 16))
         return false;
-    // blocks larger than 2^24 are fine for MTF: the segment scan is exact at any length
+    // blocks of 2^24 bytes or more: the segment scan is exact at any length; start tables whose
+    // last occurrences pass 24 bits take the two-pass sort (mtf.hip start_table_dword)
     std::vector<BlockDesc> hb{BlockDesc{0, (uint32_t) buf_size, 0}};
     if (!mtf_encode_device(c->mtf, c->d_io, c->d_mtf, hb.data(), 1, c->stream))
         return false;

@@ -175,7 +175,8 @@ __device__ __forceinline__ void sort256_phases(uint32_t (&k)[4])
 
 // Lane l's dword of a segment's start table (entries 4l .. 4l+3, little-endian): the symbols by
 // decreasing last occurrence, then the unseen ones by increasing value.  32-bit sort keys: seen
-// symbol c: (0xFFFFFE - last occurrence) << 8 | c (occurrences are block positions < 2^24 - 1),
+// symbol c: (0xFFFFFE - last occurrence) << 8 | c (occurrences are block positions < 2^24 - 2; larger
+// ones take a two-pass form below),
 // unseen: 0xFFFFFF00 | c.  (A generic 64-bit key/value sort with LDS permutes here cost about a
 // third of the wave kernel's time on uniform random data.)
 __device__ __forceinline__ uint32_t start_table_dword(const int32_t* __restrict__ st)
@@ -189,6 +190,29 @@ __device__ __forceinline__ uint32_t start_table_dword(const int32_t* __restrict_
     {
         const uint32_t c = (uint32_t) lane * 4 + r;
         k[r]             = tt[r] >= 0 ? ((0xFFFFFEu - (uint32_t) tt[r]) << 8) | c : 0xFFFFFF00u | c;
+    }
+    if (__builtin_expect(__any(tv.x >= 0xFFFFFE || tv.y >= 0xFFFFFE || tv.z >= 0xFFFFFE || tv.w >= 0xFFFFFE), 0))
+    {
+        // a position past 24 bits (single-block C-ABI buffers of 2^24 bytes or more): order by
+        // D = 2^31 - 1 - last occurrence (unseen: 2^32 - 1), then c, as two passes over 24-bit
+        // digits -- the low 24 bits of D first, then its high 8 bits with the first pass's rank as
+        // the tie-break (bitonic sorts are not stable; the rank makes the second pass exact)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = (uint32_t) lane * 4 + r;
+            const uint32_t D = tt[r] >= 0 ? 0x7FFFFFFFu - (uint32_t) tt[r] : 0xFFFFFFFFu;
+            k[r]             = (D & 0xFFFFFFu) << 8 | c;
+        }
+        sort256_phases<2>(k);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c  = k[r] & 0xFFu;
+            const int32_t  tc = st[c];
+            const uint32_t D  = tc >= 0 ? 0x7FFFFFFFu - (uint32_t) tc : 0xFFFFFFFFu;
+            k[r]              = (D >> 24) << 16 | ((uint32_t) lane * 4 + r) << 8 | c;
+        }
     }
     sort256_phases<2>(k);
     return (k[0] & 0xFF) | ((k[1] & 0xFF) << 8) | ((k[2] & 0xFF) << 16) | ((k[3] & 0xFF) << 24);

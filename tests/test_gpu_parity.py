@@ -363,3 +363,20 @@ def test_bwt_single_block_past_2_24(bra, orc):
     assert bra.bwt_decode(L, pi) == x
     L, pi = bra.bwt_encode(bytes(1 << 24))
     assert (L, pi) == (bytes(1 << 24), 0)
+
+
+def test_single_block_stages_past_2_24(bra, orc):
+    """The MTF / RLE / Huffman single-block C-ABI and their inverses on a 20 MiB block (past the
+    batched path's 2^24 block limit), against the oracle: text and uniform random MTF inputs."""
+    n = 20 << 20
+    for kind in (0, 1):
+        x = bra.synth_fill(kind, n, n).tobytes()
+        m = bra.mtf_encode(x)
+        assert m == orc.mtf_encode(x), kind
+        assert bra.mtf_decode(m) == x, kind
+        r = bra.rle_encode(m)
+        assert r == orc.rle_encode(m), kind
+        assert bra.rle_decode_compute_size(r) == n and bra.rle_decode(r) == m, kind
+        h = bra.huffman_encode(r)
+        assert (bytes(h.lengths), h.orig_size, h.encoded_size, h.data) == orc.huffman_encode(r), kind
+        assert bra.huffman_decode(h.lengths, h.orig_size, h.encoded_size, h.data) == r, kind
