@@ -380,3 +380,12 @@ def test_single_block_stages_past_2_24(bra, orc):
         h = bra.huffman_encode(r)
         assert (bytes(h.lengths), h.orig_size, h.encoded_size, h.data) == orc.huffman_encode(r), kind
         assert bra.huffman_decode(h.lengths, h.orig_size, h.encoded_size, h.data) == r, kind
+
+
+def test_batch_max_block_size(bra, codec, orc):
+    """The batched path at its largest block, 2^24 - 1 bytes (24-bit rotation indices at their
+    maximum): uniform random bytes and text, every stage against the oracle, plus the round trip."""
+    bs = (1 << 24) - 1
+    rng = np.random.default_rng(24)
+    _encode_check(bra, codec, orc, rng.integers(0, 256, bs, dtype=np.uint8), bs)
+    _encode_check(bra, codec, orc, bra.synth_fill(0, bs, bs, first_block=3), bs)
