@@ -389,3 +389,22 @@ def test_batch_max_block_size(bra, codec, orc):
     rng = np.random.default_rng(24)
     _encode_check(bra, codec, orc, rng.integers(0, 256, bs, dtype=np.uint8), bs)
     _encode_check(bra, codec, orc, bra.synth_fill(0, bs, bs, first_block=3), bs)
+
+
+def test_rle_run_and_literal_boundaries(bra, orc):
+    """PackBits control boundaries (bra_rle.c:60-120): runs and literal stretches of every length
+    1..300 (the 128-byte literal cap and the 256-byte run cap, BRA_MAX_RLE_COUNTS), back to back
+    and interleaved, encode against the oracle and decode back."""
+    rng = np.random.default_rng(128)
+    parts = []
+    for L in range(1, 301):
+        parts.append(bytes([L % 251]) * L)                      # a run of L equal bytes
+        lit = bytearray(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+        for i in range(1, L):                                   # no two neighbours equal: a pure literal
+            if lit[i] == lit[i - 1]:
+                lit[i] = (lit[i] + 1) & 0xFF
+        parts.append(bytes(lit))
+    for x in (b"".join(parts), b"".join(parts[::2]), b"".join(parts[1::2]), bytes(256), bytes(257), bytes(129), bytes(128)):
+        r = bra.rle_encode(x)
+        assert r == orc.rle_encode(x), len(x)
+        assert bra.rle_decode(r) == x, len(x)
