@@ -408,3 +408,30 @@ def test_rle_run_and_literal_boundaries(bra, orc):
         r = bra.rle_encode(x)
         assert r == orc.rle_encode(x), len(x)
         assert bra.rle_decode(r) == x, len(x)
+
+
+def test_single_block_small_and_full_alphabet(bra, orc):
+    """The single-block ABI chain on crafted small inputs against the oracle: 1-3 bytes, every byte
+    value once (ascending, descending, shuffled), each value repeated, Huffman alphabets of exactly
+    1 / 2 / 255 / 256 symbols with Fibonacci-skewed counts."""
+    rng = np.random.default_rng(256)
+    inputs = [b"\x00", b"\xff", b"ab", b"ba", b"aba", bytes(range(256)), bytes(range(255, -1, -1)),
+              rng.permutation(256).astype(np.uint8).tobytes(), bytes(np.repeat(np.arange(256, dtype=np.uint8), 3))]
+    fib = [1, 1]
+    while len(fib) < 20:
+        fib.append(fib[-1] + fib[-2])
+    for k in (1, 2, 255, 256):
+        vals = rng.permutation(256)[:k].astype(np.uint8)
+        counts = [fib[i % 20] for i in range(k)]
+        inputs.append(rng.permutation(np.repeat(vals, counts)).astype(np.uint8).tobytes())
+    for x in inputs:
+        L, pi = bra.bwt_encode(x)
+        assert (L, pi) == orc.bwt_encode(x), x[:8]
+        m = bra.mtf_encode(L)
+        assert m == orc.mtf_encode(L)
+        r = bra.rle_encode(m)
+        assert r == orc.rle_encode(m)
+        h = bra.huffman_encode(r)
+        assert (bytes(h.lengths), h.orig_size, h.encoded_size, h.data) == orc.huffman_encode(r)
+        assert bra.huffman_decode(h.lengths, h.orig_size, h.encoded_size, h.data) == r
+        assert bra.rle_decode(r) == m and bra.mtf_decode(m) == L and bra.bwt_decode(L, pi) == x
