@@ -95,7 +95,8 @@ def cpu_sample_sizes(nb, bs, threads):
 
 def cpu_baseline(data_np, bs, threads, gpu_chunks):
     """The reference encoders on host cores (one block per task; ctypes drops the GIL), on a bounded
-    sample of the benchmark's own blocks: single-threaded, then `threads` workers."""
+    sample of the benchmark's own blocks: single-threaded, then `threads` workers (skipped when the
+    sample is one block, e.g. configs[0]'s single 64 KiB block)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import Oracle, Reference, have_ref
@@ -106,11 +107,14 @@ def cpu_baseline(data_np, bs, threads, gpu_chunks):
     t0 = time.perf_counter()
     one = [impl.encode_block(b) for b in blocks[:n1]]
     dt1 = time.perf_counter() - t0
-    threads = max(1, min(threads, nm))
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        many = list(ex.map(impl.encode_block, blocks[:nm]))
-    dtm = time.perf_counter() - t0
+    if nm > 1:
+        threads = max(1, min(threads, nm))
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            many = list(ex.map(impl.encode_block, blocks[:nm]))
+        dtm = time.perf_counter() - t0
+    else:
+        threads, many, dtm = 1, one, dt1
     chunks = many if nm >= n1 else one
     same = all((c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) == g for c, g in zip(chunks, gpu_chunks))
     return {
@@ -121,10 +125,70 @@ def cpu_baseline(data_np, bs, threads, gpu_chunks):
         "sample": f"{nm} x {bs} B blocks of the benchmark input, one block per task on {threads} threads ({dtm:.2f} s wall); "
                   f"{cpu_model()}, {os.cpu_count()} host CPUs visible, {CPU_SHARE} per GPU on this box",
         "single_thread": {"value": round(n1 * bs / dt1 / 1e9, 6), "unit": "GB/s", "cores": 1,
-                          "sample": f"{n1} x {bs} B blocks, {dt1:.2f} s"},
+                          "sample": f"{n1} x {bs} B blocks, {dt1:.2f} s", "seconds_per_block": round(dt1 / n1, 4)},
         "bit_exact_vs_gpu": bool(same),
         "blocks_checked": len(chunks),
     }
+
+
+def block_digest(pi, lens, osz, esz, payload) -> str:
+    """sha256(pi u32 LE || bra_huffman_t || payload): the per-block digest of tests/golden/digests.json."""
+    import hashlib
+
+    h = hashlib.sha256()
+    h.update(pi.to_bytes(4, "little") + lens + osz.to_bytes(4, "little") + esz.to_bytes(4, "little") + payload)
+    return h.hexdigest()
+
+
+def reference_digests(kind, bs, nbg):
+    """Per-global-block reference digests for this workload from tests/golden/digests.json (made
+    from the reference's own encoders by tests/golden/make_digests.py), or None when no workload
+    there covers blocks 0..nbg-1 of this kind and block size."""
+    path = os.path.join(ROOT, "tests", "golden", "digests.json")
+    if not os.path.exists(path):
+        return None
+    best = None
+    for w in json.load(open(path)).values():
+        if (w["kind"], w["block_size"], w["first_block"], w["stride"]) == (KINDS[kind], bs, 0, 1) and w["nblocks"] >= nbg:
+            if best is None or w["nblocks"] < best["nblocks"]:
+                best = w
+    return best
+
+
+def check_vs_reference(H, O, P, kind, bs, nbg, global_total, world, threads):
+    """Rank 0's check of the ASSEMBLED global stream (every rank's blocks) against the reference:
+    every block against the committed reference digests when they cover the workload, and a
+    sample of blocks spread over the global range (all ranks' shards) re-encoded live by the
+    reference encoders (oracle/_ref) on this host."""
+    import numpy as np
+
+    bra = importlib.import_module("br-archive_amd")
+    hdr_h, off_h, pay_h = H.cpu().numpy(), O.cpu().numpy(), P.cpu().numpy()
+
+    def chunk(b):
+        pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
+        return pi, lens, osz, esz, pay_h[off_h[b]:off_h[b] + esz].tobytes()
+
+    res = {}
+    w = reference_digests(kind, bs, nbg)
+    if w is not None and global_total == nbg * bs:
+        bad = [b for b in range(nbg) if block_digest(*chunk(b)) != w["sha256"][b]]
+        res["digests"] = {"blocks": nbg, "mismatches": len(bad), "bit_exact": not bad, "first_bad": bad[:4],
+                          "source": "tests/golden/digests.json (reference src/encoders, every block)"}
+    if world > 1:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import Oracle, Reference, have_ref
+
+        impl = Reference() if have_ref() else Oracle()
+        sample = sorted({int(x) for x in np.linspace(0, nbg - 1, num=min(nbg, 2 * world))})
+        ins = [bra.synth_block(KINDS[kind], b, min(bs, global_total - b * bs)) for b in sample]
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            refs = list(ex.map(impl.encode_block, ins))
+        same = all((c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) == chunk(b) for c, b in zip(refs, sample))
+        res["live"] = {"blocks": sample, "bit_exact": bool(same), "ranks": sorted({b % world for b in sample}),
+                       "source": "oracle/_ref/libbraref.so" if have_ref() else "oracle port"}
+    return res
 
 
 def main():
@@ -248,7 +312,7 @@ def main():
             torch.cuda.synchronize()
             crc_dec = codec.chunks_crc32c(out, H, bs)
             mine_ok = all(torch.equal(out[g * bs:g * bs + min(bs, global_total - g * bs)], d[i * bs:i * bs + min(bs, my_bytes - i * bs)])
-                          for i, g in enumerate(my_blocks[:64]))
+                          for i, g in enumerate(my_blocks))
             check = bool(crc_dec == result["crc"] and mine_ok)
             secondary["crc32c_chunk_stream"] = f"{result['crc']:08x}"
             if not args.no_secondary and world == 1:
@@ -344,15 +408,20 @@ def main():
         if args.profile_all:
             line["kernels"] = {k: {"ms": round(v[0] / max(1, v[1]), 4), "launches": v[1], "GBps": round(v[2] / max(v[0], 1e-9) / 1e6, 1)}
                                for k, v in prof.items() if v[1]}
-        # traffic from a committed PMC profile of the same kernel and workload (profiles/pmc_summary.json)
+        # traffic: HBM bytes per launch of the same kernel slot on the same workload (input kind and
+        # block size) from the committed rocprofv3 PMC passes (profiles/pmc_summary.json)
         pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
         if os.path.exists(pmc):
             try:
-                k = json.load(open(pmc)).get("kernels", {}).get(dominant)
-                if k and k.get("workload") == line["config"]["workload"]:
+                wl = json.load(open(pmc)).get("workloads", {}).get(f"{args.kind}_{bs}", {})
+                k = wl.get("kernels", {}).get(dominant)
+                if k:
                     line["roofline"]["traffic"] = k.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
+                    line["roofline"]["traffic_source"] = f"profiles/pmc_summary.json workloads.{args.kind}_{bs} ({wl.get('source', '?')})"
+            except (OSError, ValueError, AttributeError):
                 pass
+        if not args.no_check:
+            line["reference_check"] = check_vs_reference(H, O, P, args.kind, bs, nbg, global_total, world, args.cpu_threads)
         if world == 1 and not args.no_cpu_baseline:
             gpu_chunks = []
             pay_h = P.cpu().numpy()

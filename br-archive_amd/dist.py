@@ -104,9 +104,18 @@ def merge_crc(parts) -> int:
     return v
 
 
-def assemble(codec, parts, round_robin: bool = True):
-    """Device assembly on rank 0: (headers [N, 268], offsets [N + 1], payload) in global block order."""
-    return codec.assemble_shards([(h, o, p) for h, o, p, _ in parts], round_robin=round_robin)
+def assemble(codec, parts, round_robin: bool = True, stream=None):
+    """Device assembly on rank 0: (headers [N, 268], offsets [N + 1], payload) in global block order.
+
+    The assembly kernels run on `stream` (default: torch's current stream).  That is the stream the
+    RCCL receives were made to wait on (`Work.wait()` in ChunkGather orders the current stream after
+    the P2P kernels; it does not block the host), so the kernels read the peers' receive buffers
+    only after they have arrived."""
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(parts[0][0].device)
+    return codec.assemble_shards([(h, o, p) for h, o, p, _ in parts], round_robin=round_robin, stream=stream)
 
 
 def assemble_host(parts, round_robin: bool = True):

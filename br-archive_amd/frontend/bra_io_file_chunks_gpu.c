@@ -11,8 +11,11 @@
  * and writes the returned chunk records to the temporary file.  The STORED fallback (:268-278),
  * the meta entry update (:280-297) and the copy into the archive are the reference's sequence.
  * Decoding parses the records of a batch on the host, hands them to bra_gpu_decompress_chunks_host
- * and folds me->crc32 the way the reference does per chunk (:396-397).  There is no CPU encoder
- * here: without a GPU the calls fail and log, like every other entry point of libbra_hip.so.
+ * and folds me->crc32 the way the reference does per chunk (:396-397).  When a batch holds a bad
+ * record, its records are decoded again one at a time through the per-chunk entry points of
+ * libbra_hip.so, so dst receives the same prefix of good chunks and the log the same message as
+ * the reference's loop.  There is no CPU encoder here: without a GPU the calls fail and log, like
+ * every other entry point of libbra_hip.so.
  */
 #include <lib_bra_defs.h>
 #include <lib_bra_private.h>
@@ -32,23 +35,39 @@
 
 #include <assert.h>
 #include <inttypes.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
-#define CHUNK_SIZE   ((uint64_t) BRA_MAX_CHUNK_SIZE)
-#define BATCH_CHUNKS 256u /* 64 MiB of input per device call */
+#define CHUNK_SIZE ((uint64_t) BRA_MAX_CHUNK_SIZE)
+#ifndef BATCH_CHUNKS
+#define BATCH_CHUNKS 256u /* 64 MiB of input per device call (tests build a 2-chunk variant) */
+#endif
 
-/* One device context for the front end, on the device current when lib_bra first compresses. */
+/* One device context for the front end, created once (pthread_once) on the device current when
+ * lib_bra first compresses or decompresses, and destroyed at process exit. */
+static bra_gpu_ctx_t*  g_front_ctx  = NULL;
+static pthread_once_t  g_front_once = PTHREAD_ONCE_INIT;
+
+static void front_ctx_destroy(void)
+{
+    bra_gpu_ctx_destroy(g_front_ctx);
+    g_front_ctx = NULL;
+}
+
+static void front_ctx_create(void)
+{
+    g_front_ctx = bra_gpu_ctx_create(-1);
+    if (g_front_ctx != NULL)
+        atexit(front_ctx_destroy);
+}
+
 static bra_gpu_ctx_t* front_ctx(void)
 {
-    static bra_gpu_ctx_t* ctx = NULL;
-    if (ctx == NULL)
-    {
-        ctx = bra_gpu_ctx_create(-1);
-        if (ctx == NULL)
-            bra_log_critical("no GPU context for the chunk loop (libbra_hip.so)");
-    }
-    return ctx;
+    pthread_once(&g_front_once, front_ctx_create);
+    if (g_front_ctx == NULL)
+        bra_log_critical("no GPU context for the chunk loop (libbra_hip.so)");
+    return g_front_ctx;
 }
 
 /* ---- chunk headers: 3-byte little-endian pi, then the packed bra_huffman_t (:59-95) ---- */
@@ -230,6 +249,55 @@ static bool chunk_decoded_size(const bra_io_chunk_header_t* h, const uint8_t* pa
     return true;
 }
 
+/* The records [0, recs) of a batch decoded one at a time through the per-chunk entry points (the
+ * reference's loop body, :355-405): dst receives every chunk before the first bad one, and the
+ * failure is logged with the reference's message.  Used only after the batched decode failed.
+ * tmp holds 2 * CHUNK_SIZE bytes. */
+static bool decode_records_serial(bra_io_file_t* dst, const char* fn, const uint8_t* stream, uint32_t recs, bra_meta_entry_t* me, uint64_t* orig,
+                                  uint8_t* tmp)
+{
+    const uint64_t hsz = BRA_BWT_INDEX_BYTES + sizeof(bra_huffman_t);
+    uint64_t       p   = 0;
+    for (uint32_t r = 0; r < recs; ++r)
+    {
+        bra_io_chunk_header_t h = {.primary_index = 0};
+        h.primary_index         = (bra_bwt_index_t) stream[p] | (bra_bwt_index_t) stream[p + 1] << 8 | (bra_bwt_index_t) stream[p + 2] << 16;
+        memcpy(&h.huffman, stream + p + BRA_BWT_INDEX_BYTES, sizeof(bra_huffman_t));
+        uint32_t       huf_s = 0;
+        uint8_t* const huf   = bra_huffman_decode(&h.huffman, stream + p + hsz, &huf_s);
+        if (huf == NULL)
+        {
+            bra_log_error("unable to decode huffman file: %s ", fn);
+            return false;
+        }
+        uint8_t*   rle = NULL;
+        size_t     s   = 0;
+        const bool rok = bra_rle_decode(huf, huf_s, &rle, &s);
+        free(huf);
+        if (!rok)
+        {
+            bra_log_error("unable to decode RLE in %s", fn);
+            return false;
+        }
+        *orig += s;
+        if (h.primary_index >= s || s > CHUNK_SIZE)
+        {
+            bra_log_error("invalid primary index (%u) for chunk size %zu in %s", h.primary_index, s, fn);
+            free(rle);
+            return false;
+        }
+        bra_mtf_decode2(rle, s, tmp);
+        free(rle);
+        bra_bwt_decode2(tmp, (bra_bwt_index_t) s, h.primary_index, NULL, tmp + CHUNK_SIZE);
+        me->crc32 = bra_crc32c(&h, sizeof(bra_io_chunk_header_t), me->crc32);
+        me->crc32 = bra_crc32c(tmp + CHUNK_SIZE, s, me->crc32);
+        if (dst != NULL && !bra_io_file_write(dst, tmp + CHUNK_SIZE, s))
+            return false;
+        p += hsz + h.huffman.encoded_size;
+    }
+    return true;
+}
+
 bool bra_io_file_chunks_decompress_file(bra_io_file_t* dst, bra_io_file_t* src, const uint64_t data_size, bra_meta_entry_t* me, const bool decode)
 {
     assert(src != NULL && me != NULL);
@@ -239,54 +307,61 @@ bool bra_io_file_chunks_decompress_file(bra_io_file_t* dst, bra_io_file_t* src, 
     // decoded output (the headers bound every chunk by BRA_MAX_CHUNK_SIZE)
     const uint64_t rec_max  = sizeof(bra_huffman_t) + BRA_BWT_INDEX_BYTES + CHUNK_SIZE;
     const uint64_t scap     = (uint64_t) BATCH_CHUNKS * rec_max;
-    const uint64_t ocap     = (uint64_t) BATCH_CHUNKS * CHUNK_SIZE;
+    const uint64_t ocap     = (uint64_t) (BATCH_CHUNKS < 2 ? 2 : BATCH_CHUNKS) * CHUNK_SIZE;
     uint8_t*       stream   = ok ? (uint8_t*) malloc(scap) : NULL;
     uint8_t*       decoded  = (ok && decode) ? (uint8_t*) malloc(ocap) : NULL;
     uint64_t       orig     = 0;
     ok                      = ok && stream != NULL && (!decode || decoded != NULL);
     for (uint64_t done = 0; ok && done < data_size;)
     {
-        // read up to BATCH_CHUNKS records (header, check, payload) into the stream buffer
+        // read up to BATCH_CHUNKS records (header, check, payload) into the stream buffer; a bad
+        // header or a failed read ends the batch after the good records before it
         uint64_t fill = 0;
         uint32_t recs = 0;
-        while (ok && recs < BATCH_CHUNKS && done + fill < data_size)
+        bool     bad  = false;
+        while (!bad && recs < BATCH_CHUNKS && done + fill < data_size)
         {
             bra_io_chunk_header_t h = {.primary_index = 0};
-            ok = bra_io_file_chunks_read_header(src, &h);
-            if (ok && !header_valid(&h))
+            bad = !bra_io_file_chunks_read_header(src, &h);
+            if (!bad && !header_valid(&h))
             {
                 bra_log_error("chunk header not valid in %s", src->fn);
-                ok = false;
+                bad = true;
             }
-            if (!ok)
+            if (bad)
                 break;
             uint8_t* rec = stream + fill;
             rec[0] = (uint8_t) h.primary_index, rec[1] = (uint8_t) (h.primary_index >> 8), rec[2] = (uint8_t) (h.primary_index >> 16);
             memcpy(rec + BRA_BWT_INDEX_BYTES, &h.huffman, sizeof(bra_huffman_t));
             const uint64_t hsz = BRA_BWT_INDEX_BYTES + sizeof(bra_huffman_t);
-            ok                 = bra_io_file_read(src, rec + hsz, h.huffman.encoded_size);
-            if (ok && !decode)
+            bad                = !bra_io_file_read(src, rec + hsz, h.huffman.encoded_size);
+            if (!bad && !decode && !chunk_decoded_size(&h, rec + hsz, &orig))
             {
-                ok = chunk_decoded_size(&h, rec + hsz, &orig);
-                if (!ok)
-                    bra_log_error("unable to decode huffman file: %s ", src->fn);
+                bra_log_error("unable to decode huffman file: %s ", src->fn);
+                bad = true;
             }
+            if (bad)
+                break;
             fill += hsz + h.huffman.encoded_size;
             ++recs;
         }
-        if (ok && decode)
+        if (decode && recs > 0)
         {
+            // the reference writes every chunk before a bad record: decode the good ones first
             uint64_t  osz = 0;
-            const int rc  = bra_gpu_decompress_chunks_host(ctx, stream, fill, (uint32_t) CHUNK_SIZE, decoded, ocap, &osz, me->crc32, &me->crc32, 0);
-            if (rc != 0)
+            uint32_t  crc = me->crc32;
+            const int rc  = bad ? -1 : bra_gpu_decompress_chunks_host(ctx, stream, fill, (uint32_t) CHUNK_SIZE, decoded, ocap, &osz, me->crc32, &crc, 0);
+            if (rc == 0)
             {
-                bra_log_error("unable to decode chunks in %s", src->fn);
-                ok = false;
+                me->crc32 = crc;
+                orig += osz;
+                if (dst != NULL)
+                    ok = bra_io_file_write(dst, decoded, (size_t) osz);
             }
-            orig += osz;
-            if (ok && dst != NULL)
-                ok = bra_io_file_write(dst, decoded, (size_t) osz);
+            else
+                ok = decode_records_serial(dst, src->fn, stream, recs, me, &orig, decoded) && !bad;
         }
+        ok = ok && !bad;
         done += fill;
     }
     if (ok && orig <= data_size)

@@ -24,6 +24,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from oracle import ReferenceLib  # noqa: E402
 from test_chunks import _case_input  # noqa: E402
 
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+from make_chunks_golden import patch_stream  # noqa: E402
+
 
 def main():
     lib = ReferenceLib(sys.argv[1])
@@ -40,7 +43,19 @@ def main():
             with tempfile.TemporaryDirectory() as d:
                 dok, dec, dcrc = lib.decompress_file(stream, d)
             rec.update(decodes=bool(dok and dec == data), decode_crc=dcrc if dok else None)
+            if not dok:
+                rec.update(decode_prefix_size=len(dec), decode_prefix_sha256=hashlib.sha256(dec).hexdigest())
         out[name] = rec
+    # decode-only cases: a patched stream; the decoder must fail after writing the same prefix
+    for name, spec in sorted(json.load(open(os.path.join(ROOT, "tests", "golden", "chunks_decode.json"))).items()):
+        data = _case_input(golden[spec["base"]])
+        with tempfile.TemporaryDirectory() as d:
+            ok, dst, _, _, _ = lib.compress_file(data, d)
+        stream = patch_stream(dst[8:], spec["patch_chunk"], spec["patch_pi"])
+        with tempfile.TemporaryDirectory() as d:
+            dok, dec, dcrc = lib.decompress_file(stream, d)
+        out[name] = {"stream_sha256": hashlib.sha256(stream).hexdigest(), "decodes": bool(dok and dec == data),
+                     "decode_crc": dcrc if dok else None, "decode_prefix_size": len(dec), "decode_prefix_sha256": hashlib.sha256(dec).hexdigest()}
     with open(sys.argv[2], "w") as f:
         json.dump(out, f)
 

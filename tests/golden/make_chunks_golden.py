@@ -47,6 +47,23 @@ PART_CASES = [
     ("mixed_text_random", {"parts": [[0, 2 * 262144, 0], [1, 262144, 0], [0, 100000, 3]]}),
     ("lorem_txt", {"file": "lorem.txt"}),
 ]
+# Decode-only cases: a case's reference stream with one chunk header patched.  The reference's loop
+# writes every chunk before the bad one, then fails (lib_bra_io_file_chunks.c:340-411); the fixture
+# pins that prefix (`ref_decode_prefix_size` / `_sha256`) and the verdict.
+#   text_600000_bad_pi -- chunk 2 (75712 B) gets primary index 100000: the header is valid
+#                         (pi < BRA_MAX_CHUNK_SIZE) but pi >= the decoded size (:385-389).
+# (written to tests/golden/chunks_decode.json)
+DECODE_CASES = [
+    ("text_600000_bad_pi", {"base": "text_600000", "patch_chunk": 2, "patch_pi": 100000}),
+]
+
+
+def patch_stream(stream: bytes, chunk: int, pi: int) -> bytes:
+    """The chunk stream with record `chunk`'s 3-byte primary index set to pi."""
+    pos = 0
+    for _ in range(chunk):
+        pos += 267 + int.from_bytes(stream[pos + 263: pos + 267], "little")
+    return stream[:pos] + pi.to_bytes(3, "little") + stream[pos + 3:]
 
 
 def synth(kind: int, total: int) -> bytes:
@@ -106,10 +123,28 @@ def main():
                 pos += 267 + esizes[-1]
             rec.update(stream_size=tsz, stream_sha256=hashlib.sha256(stream).hexdigest(), chunk_crcs=crcs, encoded_sizes=esizes,
                        ref_decodes=dok and dec == data, ref_decode_crc=dcrc if dok else None)
+            if not dok:
+                rec.update(ref_decode_prefix_size=len(dec), ref_decode_prefix_sha256=hashlib.sha256(dec).hexdigest())
         out[name] = rec
         print(name, {k: v for k, v in rec.items() if k != "chunk_crcs"}, flush=True)
     with open(os.path.join(ROOT, "tests", "golden", "chunks.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
+    dec_out = {}
+    for name, spec in DECODE_CASES:
+        base = dict(cases)[spec["base"]]
+        data = case_input(base)
+        with tempfile.TemporaryDirectory() as d:
+            ok, dst, _, _, _ = R.compress_file(data, d)
+        assert ok, name
+        stream = patch_stream(dst[8:], spec["patch_chunk"], spec["patch_pi"])
+        with tempfile.TemporaryDirectory() as d:
+            dok, dec, dcrc = R.decompress_file(stream, d)
+        rec = dict(spec, stream_sha256=hashlib.sha256(stream).hexdigest(), ref_decodes=bool(dok and dec == data),
+                   ref_decode_crc=dcrc if dok else None, ref_decode_prefix_size=len(dec), ref_decode_prefix_sha256=hashlib.sha256(dec).hexdigest())
+        dec_out[name] = rec
+        print(name, rec, flush=True)
+    with open(os.path.join(ROOT, "tests", "golden", "chunks_decode.json"), "w") as f:
+        json.dump(dec_out, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -2,6 +2,7 @@
 
 Run in the build container (where /root/reference exists):
     make -C oracle ref && python tests/golden/make_digests.py
+    ONLY=text_1MiB_x2048,sym16_8MiB_x256 python tests/golden/make_digests.py   # some workloads only
 
 For each BASELINE workload below, every block of the deterministic synthetic input
 (br-archive_amd/csrc/bra_synth.c, the same bytes bench.py encodes on one GPU) goes through the
@@ -26,11 +27,15 @@ sys.path.insert(0, ROOT)
 from oracle import Reference, have_ref  # noqa: E402
 
 # name -> (synth kind, block size, blocks): BASELINE configs[1] (text), configs[2] (random) at the
-# 256 MiB single-GPU size, configs[4] (sym16 8 MiB blocks) at its per-GPU share of 2 GiB / 8.
+# 256 MiB single-GPU size, configs[4] (sym16 8 MiB blocks) at its per-GPU share of 2 GiB / 8, and
+# the two 8-GPU configurations at their FULL global shape: configs[3] = 2048 x 1 MiB text blocks
+# (2 GiB; rank r of 8 encodes blocks r, r + 8, ...) and configs[4] = 256 x 8 MiB sym16 blocks.
 WORKLOADS = {
     "text_1MiB_x256": (0, 1 << 20, 256),
     "random_1MiB_x256": (1, 1 << 20, 256),
     "sym16_8MiB_x32": (2, 8 << 20, 32),
+    "text_1MiB_x2048": (0, 1 << 20, 2048),
+    "sym16_8MiB_x256": (2, 8 << 20, 256),
 }
 
 
@@ -45,14 +50,18 @@ def main():
         sys.exit("oracle/_ref/libbraref.so missing: run `make -C oracle ref` where /root/reference exists")
     bra = importlib.import_module("br-archive_amd")
     ref = Reference()
-    out = {}
+    path = os.path.join(ROOT, "tests", "golden", "digests.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    only = [w for w in os.environ.get("ONLY", "").split(",") if w]
     threads = int(os.environ.get("THREADS", os.cpu_count() or 8))
     for name, (kind, bs, nb) in WORKLOADS.items():
+        if only and name not in only:
+            continue
         t0 = time.time()
-        data = bra.synth_fill(kind, bs * nb, bs)
 
         def one(b):
-            ch = ref.encode_block(data[b * bs:(b + 1) * bs].tobytes())
+            # one block at a time (a 2 GiB workload is never held whole)
+            ch = ref.encode_block(bra.synth_fill(kind, bs, bs, first_block=b).tobytes())
             return ch.primary_index, ch.encoded_size, digest(ch.primary_index, ch.lengths, ch.orig_size, ch.encoded_size, ch.payload)
 
         with ThreadPoolExecutor(threads) as ex:
@@ -62,8 +71,8 @@ def main():
             "pi": [r[0] for r in res], "encoded_size": [r[1] for r in res], "sha256": [r[2] for r in res],
         }
         print(f"{name}: {nb} blocks in {time.time() - t0:.1f} s", flush=True)
-    with open(os.path.join(ROOT, "tests", "golden", "digests.json"), "w") as f:
-        json.dump(out, f, indent=0, sort_keys=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=0, sort_keys=True)
 
 
 if __name__ == "__main__":

@@ -7,7 +7,10 @@ Two builds made by oracle/Makefile (target gpulib) from the reference's own lib_
     libbra_hip.so;
   * libbralib_gpu.so    -- lib_bra without src/encoders/*.c and without lib_bra_io_file_chunks.c,
     plus the batched front end br-archive_amd/frontend/bra_io_file_chunks_gpu.c (one device call
-    per 256 chunks).
+    per 256 chunks);
+  * libbralib_gpu_b2.so -- the same front end built with BATCH_CHUNKS=2, so every multi-chunk
+    case spans several batches (the CRC combine across batches, decode batches that end at the
+    batch limit, the serial error path after a failed batch).
 Both must reproduce tests/golden/chunks.json (the reference lib_bra's own tmpfile bytes, entry
 CRCs, STORED decisions, decoder verdicts and decode CRCs) exactly.  Each build runs in its own
 process (tests/frontend_driver.py).
@@ -23,9 +26,10 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "chunks.json")))
+DECODE = json.load(open(os.path.join(ROOT, "tests", "golden", "chunks_decode.json")))
 
 
-@pytest.mark.parametrize("lib", ["libbralib_hipenc.so", "libbralib_gpu.so"])
+@pytest.mark.parametrize("lib", ["libbralib_hipenc.so", "libbralib_gpu.so", "libbralib_gpu_b2.so"])
 def test_lib_bra_chunk_loop_on_gpu(lib, tmp_path):
     path = os.path.join(ROOT, "oracle", "_ref", lib)
     assert os.path.exists(path), f"{lib} not built (make -C oracle gpulib where the reference tree exists)"
@@ -44,3 +48,10 @@ def test_lib_bra_chunk_loop_on_gpu(lib, tmp_path):
         assert o["decodes"] == g["ref_decodes"], name
         if g["ref_decodes"]:
             assert o["decode_crc"] == g["ref_decode_crc"], name
+        else:  # the reference wrote every chunk before the bad record: so must the drop-in
+            assert (o["decode_prefix_size"], o["decode_prefix_sha256"]) == (g["ref_decode_prefix_size"], g["ref_decode_prefix_sha256"]), name
+    for name, g in DECODE.items():
+        o = got[name]
+        assert o["stream_sha256"] == g["stream_sha256"], name
+        assert o["decodes"] == g["ref_decodes"], name
+        assert (o["decode_prefix_size"], o["decode_prefix_sha256"]) == (g["ref_decode_prefix_size"], g["ref_decode_prefix_sha256"]), name
