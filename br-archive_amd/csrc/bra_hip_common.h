@@ -369,6 +369,40 @@ __device__ __forceinline__ void cx96_pair(uint32_t& a0, uint32_t& a1, uint32_t& 
     b0 = m0, b1 = m1, b2 = m2;
 }
 
+// 64-bit keys as two dwords (k0 lowest): the job sort network's keys (the rotation's packed bits
+// above the slot bits).  Two subtractions, one xnor, two selects.
+__device__ __forceinline__ void cx64(uint32_t& k0, uint32_t& k1, uint32_t o0, uint32_t o1, uint64_t keep_min)
+{
+    uint32_t t;
+    asm volatile(
+        "v_sub_co_u32 %[t], vcc, %[o0], %[k0]\n\t"
+        "v_subb_co_u32 %[t], vcc, %[o1], %[k1], vcc\n\t"
+        "s_xnor_b64 vcc, vcc, %[km]\n\t"
+        "v_cndmask_b32 %[k0], %[k0], %[o0], vcc\n\t"
+        "v_cndmask_b32 %[k1], %[k1], %[o1], vcc"
+        : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1)
+        : [o0] "v"(o0), [o1] "v"(o1), [km] "s"(keep_min)
+        : "vcc");
+}
+
+__device__ __forceinline__ void cx64_pair(uint32_t& a0, uint32_t& a1, uint32_t& b0, uint32_t& b1, uint64_t asc)
+{
+    uint32_t t, n0, n1, m0, m1;
+    asm volatile(
+        "v_sub_co_u32 %[t], vcc, %[b0], %[a0]\n\t"
+        "v_subb_co_u32 %[t], vcc, %[b1], %[a1], vcc\n\t"
+        "s_xnor_b64 vcc, vcc, %[asc]\n\t"
+        "v_cndmask_b32 %[n0], %[a0], %[b0], vcc\n\t"
+        "v_cndmask_b32 %[m0], %[b0], %[a0], vcc\n\t"
+        "v_cndmask_b32 %[n1], %[a1], %[b1], vcc\n\t"
+        "v_cndmask_b32 %[m1], %[b1], %[a1], vcc"
+        : [t] "=&v"(t), [n0] "=&v"(n0), [n1] "=&v"(n1), [m0] "=&v"(m0), [m1] "=&v"(m1)
+        : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1), [asc] "s"(asc)
+        : "vcc");
+    a0 = n0, a1 = n1;
+    b0 = m0, b1 = m1;
+}
+
 template <int LM>
 __device__ __forceinline__ uint64_t xlane64(uint64_t x)
 {

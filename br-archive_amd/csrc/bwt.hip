@@ -81,14 +81,11 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_JOB_PREFETCH
 #define BRA_JOB_PREFETCH 1  // wave jobs: next job's descriptor and payloads loaded ahead
 #endif
-#ifndef BRA_MJ_MERGE
-#define BRA_MJ_MERGE 1  // workgroup jobs: per-wave sorts + merge-path levels (0: bitonic phases through LDS)
-#endif
 #ifndef MJOB_MIN_WAVES
 #define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
 #endif
 #ifndef JOB_MIN_WAVES
-#define JOB_MIN_WAVES 5  // 6 spills with the payload prefetch (wave jobs 2.24 -> 2.14 ms with prefetch at 5; 2.53 spilling at 6)
+#define JOB_MIN_WAVES 6  // 64-bit keys: 80 VGPRs without spills at 6 waves per SIMD (the 96-bit keys spilled at 6)
 #endif
 
 enum : uint32_t { MODE_STRING = 0, MODE_RANK = 1 };
@@ -216,24 +213,6 @@ __device__ __forceinline__ uint64_t pk_load64(const uint8_t* __restrict__ pk, ui
     return sh ? (hi << sh) | ((uint64_t) p[8] >> (8 - sh)) : hi;
 }
 
-// 128 bits of a packed string from bit bp: w0 = bits [bp, bp + 64), w1 = the next 64
-__device__ __forceinline__ void pk_load128(const uint8_t* __restrict__ pk, uint32_t bp, uint64_t& w0, uint64_t& w1)
-{
-    const uint8_t* p  = pk + (bp >> 3);
-    const uint4    q  = *reinterpret_cast<const uint4_u*>(p);
-    uint64_t       a  = __builtin_bswap64(((uint64_t) q.y << 32) | q.x);
-    uint64_t       c  = __builtin_bswap64(((uint64_t) q.w << 32) | q.z);
-    const uint32_t sh = bp & 7;
-    if (sh)
-    {
-        const uint64_t e = p[16];
-        a                = (a << sh) | (c >> (64 - sh));
-        c                = (c << sh) | (e >> (8 - sh));
-    }
-    w0 = a;
-    w1 = c;
-}
-
 // STRING-mode payload (64 bits): the rotation index in bits 0-23 and CARRY digits, virtual bytes
 // [kd, kd + CARRY) of the rotation, big-endian in bits 24-63.  A bucket at depth d reads digit
 // d - kd; the scatter that moves an element into a bucket at depth kd + CARRY gathers the next
@@ -271,16 +250,6 @@ __global__ void k_ctr_init(Counters* ctr, uint32_t nslots)
 __device__ __forceinline__ uint32_t dev_count(const uint32_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The call-wide job counts as they stand (the boundary between the two job phases, see run_jobs).
-__global__ void k_job_snap(const Counters* __restrict__ ctr, uint32_t* __restrict__ snap)
-{
-    if (threadIdx.x == 0)
-    {
-        snap[0] = dev_count(&ctr->n_jobs);
-        snap[1] = dev_count(&ctr->n_mjobs);
-    }
 }
 
 // Host mailbox record: a level's counts, written by k_publish into pinned host memory so the host
@@ -1547,29 +1516,31 @@ __device__ __forceinline__ JobRange job_range(const JobArgs& a, const uint32_t* 
 }
 
 template <int W>
+struct JobGeom
+{
+    static constexpr int      LOGS  = (W == 1) ? 8 : (W == 2) ? 9 : (W == 4) ? 10 : (W == 8) ? 11 : 12;  // log2(256 * W)
+    static constexpr int      GBITS = LOGS;                                // group id bits (top of the key)
+    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;                  // slot bits (bottom of the key)
+    // 64-bit keys: group id | the rotation's next packed bits | slot.  Round 1 (no group bits)
+    // carries 6-7 rotation bytes, later rounds 5-6.  A 64-bit compare-exchange is 7 VALU against
+    // the 10 / 13 of the 96 / 128-bit keys of round 2, and the keys take half the registers; the
+    // elements still tied after round 1 (about a quarter of them on text) take another round.
+    static constexpr int      KD    = 2;
+    static constexpr uint32_t KBITS = 32 * KD;
+    static constexpr uint32_t ADV   = (KBITS - GBITS - LOGS) / 8;          // whole rotation bytes per key
+    static constexpr uint32_t ADV1  = (KBITS - LOGS) / 8;                  // round 1: no group bits
+};
+
+template <int W>
 struct JobLds
 {
-    uint64_t kh[256 * W];   // cross-wave network exchange, neighbour keys, compaction scratch
-    uint64_t kl[256 * W];
+    static constexpr int KD = JobGeom<W>::KD;
+    uint64_t kh[256 * W];                // neighbour keys, merge levels, compaction scratch
+    uint64_t kl[KD == 2 ? 1 : 256 * W];  // low key words (keys wider than 64 bits only)
     uint32_t v[256 * W];    // payload of every slot of the current round (the keys carry the slot)
     uint32_t nx[256 * W];   // group-end scratch
     uint16_t pos[256 * W];  // job position of each active slot (increasing)
     uint32_t agg[W];
-};
-
-template <int W>
-struct JobGeom
-{
-    static constexpr int      LOGS  = (W == 1) ? 8 : (W == 2) ? 9 : (W == 4) ? 10 : (W == 8) ? 11 : 12;  // log2(256 * W)
-    static constexpr int      GBITS = LOGS;                                // group id bits (top of kh)
-    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;                  // slot bits (bottom of kl)
-    // key dwords: 96-bit keys for wave jobs (11 rotation bytes in round 1; the cheaper network
-    // outweighs the extra rounds), 128 bits for workgroup jobs (with 96 bits 62 % of them needed a
-    // second round, which cost what the network saved)
-    static constexpr int      KD    = (W == 1) ? 3 : 4;
-    static constexpr uint32_t KBITS = 32 * KD;
-    static constexpr uint32_t ADV   = (KBITS - GBITS - LOGS) / 8;          // whole rotation bytes per key
-    static constexpr uint32_t ADV1  = (KBITS - LOGS) / 8;                  // round 1: no group bits
 };
 
 template <int W>
@@ -1674,11 +1645,13 @@ __device__ __forceinline__ void job_excl_count(const bool (&f)[4], uint32_t (&ex
 
 // One bitonic stage whose partners sit LM lanes away (same element r): exchanged with DPP /
 // permlane swaps.  k[i][r] = dword i of element r's key.
-// Keys of KD dwords (3: 96 bits, wave jobs; 4: 128 bits, workgroup jobs).
+// Keys of KD dwords (2: 64 bits, the job sorts; 3 / 4: 96 / 128 bits).
 template <int KD>
 __device__ __forceinline__ void cxk(uint32_t (&k)[KD][4], int r, const uint32_t (&o)[KD], uint64_t keep_min)
 {
-    if constexpr (KD == 3)
+    if constexpr (KD == 2)
+        cx64(k[0][r], k[1][r], o[0], o[1], keep_min);
+    else if constexpr (KD == 3)
         cx96(k[0][r], k[1][r], k[2][r], o[0], o[1], o[2], keep_min);
     else
         cx128(k[0][r], k[1][r], k[2][r], k[3][r], o[0], o[1], o[2], o[3], keep_min);
@@ -1687,7 +1660,9 @@ __device__ __forceinline__ void cxk(uint32_t (&k)[KD][4], int r, const uint32_t 
 template <int KD>
 __device__ __forceinline__ void cxk_pair(uint32_t (&a)[KD], uint32_t (&b)[KD], uint64_t asc)
 {
-    if constexpr (KD == 3)
+    if constexpr (KD == 2)
+        cx64_pair(a[0], a[1], b[0], b[1], asc);
+    else if constexpr (KD == 3)
         cx96_pair(a[0], a[1], a[2], b[0], b[1], b[2], asc);
     else
         cx128_pair(a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], asc);
@@ -1746,44 +1721,9 @@ __device__ __forceinline__ void net_stage_swap(uint32_t (&k)[KD][4], uint64_t as
 template <int W, int KD, int SIZE, int J>
 __device__ __forceinline__ void net_stage(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0)
 {
-    if constexpr (J >= 256)
-    {
-        static_assert(W > 1, "cross-wave stage");
-        uint4* X = reinterpret_cast<uint4*>(S.kh);  // S.kh and S.kl back to back: 256*W 16-byte words
-        job_sync<W>();
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], KD == 4 ? k[KD - 1][r] : 0u);
-        job_sync<W>();
-        const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            const uint4    o4 = X[(e0 + r) ^ J];
-            const uint32_t ow[4] = {o4.x, o4.y, o4.z, o4.w};
-            uint32_t       o[KD];
-#pragma unroll
-            for (int i = 0; i < KD; ++i)
-                o[i] = ow[i];
-            cxk<KD>(k, r, o, keep_min);
-        }
-        if constexpr (J == 256)
-        {
-            // the rest of the phase stays inside the wave: a wave left with padding only skips it
-            uint32_t a = ~0u;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int i = 0; i < KD; ++i)
-                    a &= k[i][r];
-            if (__builtin_amdgcn_ballot_w64(a != ~0u) == 0)
-                return;
-        }
-    }
-#ifndef BRA_NO_SWAP_STAGES
-    else if constexpr (J == 64 || J == 128)
+    static_assert(J < 256, "cross-wave merges are merge_level's");
+    if constexpr (J == 64 || J == 128)
         net_stage_swap<J / 4, KD>(k, __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0));
-#endif
     else if constexpr (J >= 4)
     {
         const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
@@ -1823,89 +1763,48 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[KD][4], JobLds<W>& S, ui
 template <int W, int KD, int SIZE>
 __device__ __forceinline__ void net_phase(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0)
 {
-    if constexpr (SIZE <= 256 * W)
-        net_stage<W, KD, SIZE, SIZE / 2>(k, S, e0);
-}
-
-// 128-bit keys as uint4 (x lowest): a <= b
-__device__ __forceinline__ bool key_le(const uint4& a, const uint4& b)
-{
-    const uint64_t ah = ((uint64_t) a.w << 32) | a.z, bh = ((uint64_t) b.w << 32) | b.z;
-    const uint64_t al = ((uint64_t) a.y << 32) | a.x, bl = ((uint64_t) b.y << 32) | b.x;
-    return ah < bh || (ah == bh && al <= bl);
+    net_stage<W, KD, SIZE, SIZE / 2>(k, S, e0);
 }
 
 // One merge level of a workgroup job's sort: sorted runs of m slots (in LDS) merged pairwise into
 // runs of 2m.  Merge path: the lane owning output slots [e0, e0 + 4) finds how many of them come
-// from the left run with one binary search (co-rank), then merges its 4 outputs sequentially --
-// about 40 VALU per element and level instead of the ~230 of the bitonic phases it replaces
-// (log2(2m) compare-exchange stages, cross-wave ones through LDS with two barriers each).  Equal
-// keys (padding) take the left run first.
-#ifndef BRA_MERGE_ARY
-#define BRA_MERGE_ARY 2  // co-rank search arity (2: binary)
-#endif
-template <int W, int KD>
-__device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0, uint32_t m)
+// from the left run with one binary search (co-rank), then merges its 4 outputs sequentially
+// (instead of log2(2m) compare-exchange stages, the cross-wave ones through LDS with two barriers
+// each).  Equal keys (padding) take the left run first.
+template <int W>
+__device__ __forceinline__ void merge_level(uint32_t (&k)[2][4], JobLds<W>& S, uint32_t e0, uint32_t m)
 {
-    static_assert(KD == 4, "workgroup jobs sort 128-bit keys");
-    uint4* X = reinterpret_cast<uint4*>(S.kh);  // S.kh and S.kl back to back: 256*W 16-byte words
+    uint64_t* X = S.kh;
     job_sync<W>();
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-        X[e0 + r] = make_uint4(k[0][r], k[1][r], k[2][r], k[3][r]);
+        X[e0 + r] = ((uint64_t) k[1][r] << 32) | k[0][r];
     job_sync<W>();
-    const uint32_t base = e0 & ~(2 * m - 1), kk = e0 - base;
-    const uint4*   A    = X + base;
-    const uint4*   B    = X + base + m;
+    const uint32_t  base = e0 & ~(2 * m - 1), kk = e0 - base;
+    const uint64_t* A    = X + base;
+    const uint64_t* B    = X + base + m;
     // a pair whose right run is all padding (it starts with the padding key; then so is the left
     // run if it does too) is already merged: it stays as it is
-    const uint4 b0 = B[0];
-    if ((b0.x & b0.y & b0.z & b0.w) != ~0u)
+    if (B[0] != ~0ull)
     {
         uint32_t lo = kk > m ? kk - m : 0u, hi = kk < m ? kk : m;  // i = outputs [0, kk) taken from A
-#if BRA_MERGE_ARY > 2
-        // K-ary search: K - 1 independent probe pairs per step (fewer dependent LDS round trips)
-        constexpr uint32_t K = BRA_MERGE_ARY;
-        while (lo < hi)
-        {
-            const uint32_t len = hi - lo;
-            uint32_t       q[K - 1];
-            bool           pr[K - 1];
-#pragma unroll
-            for (uint32_t t = 0; t < K - 1; ++t)
-            {
-                q[t]  = lo + ((t + 1) * len) / K;
-                pr[t] = key_le(A[q[t]], B[kk - 1 - q[t]]);
-            }
-            uint32_t nlo = q[K - 2] + 1, nhi = hi;  // all probes true: past the last one
-#pragma unroll
-            for (int t = K - 2; t >= 0; --t)
-                if (!pr[t])
-                {
-                    nhi = q[t];
-                    nlo = t ? q[t - 1] + 1 : lo;
-                }
-            lo = nlo;
-            hi = nhi;
-        }
-#else
         while (lo < hi)
         {
             const uint32_t mid = (lo + hi) >> 1;
-            if (key_le(A[mid], B[kk - 1 - mid]))
+            if (A[mid] <= B[kk - 1 - mid])
                 lo = mid + 1;
             else
                 hi = mid;
         }
-#endif
         uint32_t i = lo, j = kk - lo;
-        uint4    a = A[min(i, m - 1)], b = B[min(j, m - 1)];
+        uint64_t a = A[min(i, m - 1)], b = B[min(j, m - 1)];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            const bool ta = i < m && (j >= m || key_le(a, b));
-            const uint4 o = ta ? a : b;
-            k[0][r] = o.x, k[1][r] = o.y, k[2][r] = o.z, k[3][r] = o.w;
+            const bool     ta = i < m && (j >= m || a <= b);
+            const uint64_t o  = ta ? a : b;
+            k[0][r]           = (uint32_t) o;
+            k[1][r]           = (uint32_t) (o >> 32);
             if (r < 3)
             {
                 if (ta)
@@ -1917,26 +1816,22 @@ __device__ __forceinline__ void merge_level(uint32_t (&k)[KD][4], JobLds<W>& S, 
     }
 }
 
-// Bitonic sort of the job's 256*W slots (4 consecutive per lane, slot e = wj*256 + lane*4 + r)
-// over the first P (power of two) slots.  Workgroup jobs (W > 1, P > 256) sort every wave's 256
-// slots on their own and merge the sorted runs (merge_level).  Keys are unique (the slot is in the low bits).  The
-// network runs on dwords (no 64-bit register pairs to keep together); cross-wave stages exchange
-// whole keys through LDS as 16-byte words.
+// Sort of the job's 256*W 64-bit keys (4 consecutive per lane, slot e = wj*256 + lane*4 + r) over
+// the first P (power of two) slots: each wave's 256 slots by the in-wave bitonic phases (DPP /
+// permlane partners), then (W > 1, P > 256) merge-path levels across the waves.  Keys are unique
+// (the slot is in the low bits).  The network runs on dwords (no 64-bit register pairs to keep
+// together).
 template <int W>
-__device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], int P, JobLds<W>& S, int wj)
+__device__ __forceinline__ void job_sort(uint64_t (&key)[4], int P, JobLds<W>& S, int wj)
 {
-    constexpr int  KD   = JobGeom<W>::KD;
     const int      lane = lane_id();
     const uint32_t e0   = wj * 256 + lane * 4;
-    uint32_t       k[KD][4];
+    uint32_t       k[2][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        k[0][r] = (uint32_t) kl[r];
-        if constexpr (KD == 4)
-            k[1][r] = (uint32_t) (kl[r] >> 32);
-        k[KD - 2][r] = (uint32_t) kh[r];
-        k[KD - 1][r] = (uint32_t) (kh[r] >> 32);
+        k[0][r] = (uint32_t) key[r];
+        k[1][r] = (uint32_t) (key[r] >> 32);
     }
     // A wave whose slots all hold padding keys (all ones) skips the phases that stay inside the
     // wave (SIZE <= 256: no barriers, no data from other waves); any order of equal keys is
@@ -1944,85 +1839,62 @@ __device__ __forceinline__ void job_sort(uint64_t (&kh)[4], uint64_t (&kl)[4], i
     // of two, or the waves beyond P in later rounds).
     bool dead = false;
     if (W > 1)
-    {
-        uint32_t a = ~0u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int i = 0; i < KD; ++i)
-                a &= k[i][r];
-        dead = __builtin_amdgcn_ballot_w64(a != ~0u) == 0;
-    }
+        dead = __builtin_amdgcn_ballot_w64((k[0][0] & k[1][0] & k[0][1] & k[1][1] & k[0][2] & k[1][2] & k[0][3] & k[1][3]) != ~0u) == 0;
     // the in-wave phases sort each wave's slots ascending (directions from the wave-local slot)
-    const uint32_t el = (W > 1 && P > 256 && BRA_MJ_MERGE) ? (uint32_t) lane * 4 : e0;
+    const uint32_t el = (W > 1 && P > 256) ? (uint32_t) lane * 4 : e0;
     for (int size = 2; size <= P; size <<= 1)
     {
         if (dead && size <= 256)
             continue;
-        if constexpr (W > 1 && BRA_MJ_MERGE)
+        if constexpr (W > 1)
             if (size > 256)
             {
-                merge_level<W, KD>(k, S, e0, (uint32_t) size / 2);
+                merge_level<W>(k, S, e0, (uint32_t) size / 2);
                 continue;
             }
-        const uint32_t e0w = el;
         switch (size)
         {
-        case 2: net_phase<W, KD, 2>(k, S, e0w); break;
-        case 4: net_phase<W, KD, 4>(k, S, e0w); break;
-        case 8: net_phase<W, KD, 8>(k, S, e0w); break;
-        case 16: net_phase<W, KD, 16>(k, S, e0w); break;
-        case 32: net_phase<W, KD, 32>(k, S, e0w); break;
-        case 64: net_phase<W, KD, 64>(k, S, e0w); break;
-        case 128: net_phase<W, KD, 128>(k, S, e0w); break;
-        case 256: net_phase<W, KD, 256>(k, S, e0w); break;
-        case 512: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 512>(k, S, e0); break;
-        case 1024: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 1024>(k, S, e0); break;
-        case 2048: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 2048>(k, S, e0); break;
-        default: if constexpr (!BRA_MJ_MERGE) net_phase<W, KD, 4096>(k, S, e0); break;
+        case 2: net_phase<W, 2, 2>(k, S, el); break;
+        case 4: net_phase<W, 2, 4>(k, S, el); break;
+        case 8: net_phase<W, 2, 8>(k, S, el); break;
+        case 16: net_phase<W, 2, 16>(k, S, el); break;
+        case 32: net_phase<W, 2, 32>(k, S, el); break;
+        case 64: net_phase<W, 2, 64>(k, S, el); break;
+        case 128: net_phase<W, 2, 128>(k, S, el); break;
+        default: net_phase<W, 2, 256>(k, S, el); break;
         }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-    {
-        kl[r] = (KD == 4) ? (((uint64_t) k[1][r] << 32) | k[0][r]) : (uint64_t) k[0][r];
-        kh[r] = ((uint64_t) k[KD - 1][r] << 32) | k[KD - 2][r];
-    }
+        key[r] = ((uint64_t) k[1][r] << 32) | k[0][r];
     job_sync<W>();
 }
 
-// Group heads / group ends / ties over the T active slots; kh / km are the keys without the slot
-// bits.
+// Group heads / group ends / ties over the T active slots; km = the keys without the slot bits.
 template <int W>
-__device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64_t (&km)[4], uint32_t T, JobLds<W>& S, int wj,
-                                           uint32_t (&g)[4], uint32_t (&gend)[4], bool (&tied)[4])
+__device__ __forceinline__ bool job_groups(const uint64_t (&km)[4], uint32_t T, JobLds<W>& S, int wj, uint32_t (&g)[4], uint32_t (&gend)[4],
+                                           bool (&tied)[4])
 {
     constexpr uint32_t SLOTS = 256 * W;
     const int          lane  = lane_id();
     // previous slot's key: the lane's own element r - 1, the previous lane's element 3 (ds_bpermute),
     // or (lane 0 of waves > 0) the previous wave's last element through LDS
-    uint64_t ph = (uint64_t) __shfl_up((long long) kh[3], 1, WAVE), pm = (uint64_t) __shfl_up((long long) km[3], 1, WAVE);
+    uint64_t pm = (uint64_t) __shfl_up((long long) km[3], 1, WAVE);
     if (W > 1)
     {
         if (lane == 63)
-        {
-            S.kh[wj * 256 + 255] = kh[3];
-            S.kl[wj * 256 + 255] = km[3];
-        }
+            S.kh[wj * 256 + 255] = km[3];
         job_sync<W>();
         if (lane == 0 && wj > 0)
-        {
-            ph = S.kh[wj * 256 - 1];
-            pm = S.kl[wj * 256 - 1];
-        }
+            pm = S.kh[wj * 256 - 1];
     }
     uint32_t x[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         const uint32_t c  = wj * 256 + lane * 4 + r;
-        const uint64_t qh = r ? kh[r - 1] : ph, qm = r ? km[r - 1] : pm;
-        const bool     hd = (c == 0) || c >= T || qh != kh[r] || qm != km[r];
+        const uint64_t qm = r ? km[r - 1] : pm;
+        const bool     hd = (c == 0) || c >= T || qm != km[r];
         g[r]              = hd ? c : 0;
         x[r]              = hd ? c : 0xFFFFFFFFu;
     }
@@ -2056,49 +1928,24 @@ __device__ __forceinline__ bool job_groups(const uint64_t (&kh)[4], const uint64
 }
 
 
-// round-1 key: the rotation's 12 bytes from depth d-1, low LOGS bits = slot
+// round-1 key: the rotation's packed bits from the key's first depth, low LOGS bits = slot
 template <int W>
-__device__ __forceinline__ void make_key1(uint32_t slot, uint64_t w0, uint64_t w1, uint64_t& kh, uint64_t& kl)
+__device__ __forceinline__ uint64_t make_key1(uint32_t slot, uint64_t w0)
+{
+    return (w0 & ~JobGeom<W>::SMASK) | slot;
+}
+
+// key = group | the rotation's bits (w0) shifted right by GBITS, low LOGS bits = slot
+template <int W>
+__device__ __forceinline__ uint64_t make_key(uint32_t grp, uint32_t slot, uint64_t w0)
 {
     using G = JobGeom<W>;
-    kh      = w0;
-    kl      = ((G::KD == 3 ? (w1 >> 32) : w1) & ~G::SMASK) | slot;
+    return ((((uint64_t) grp << (64 - G::GBITS)) | (w0 >> G::GBITS)) & ~G::SMASK) | slot;
 }
-
-// key = group | the rotation's bytes (w0:w1) shifted right by GBITS, low LOGS bits = slot
-template <int W>
-__device__ __forceinline__ void make_key(uint32_t grp, uint32_t slot, uint64_t w0, uint64_t w1, uint64_t& kh, uint64_t& kl)
-{
-    using G          = JobGeom<W>;
-    kh               = ((uint64_t) grp << (64 - G::GBITS)) | (w0 >> G::GBITS);
-    const uint64_t l = (w0 << (64 - G::GBITS)) | (w1 >> G::GBITS);
-    kl               = ((G::KD == 3 ? (l >> 32) : l) & ~G::SMASK) | slot;
-}
-
-#ifdef BRA_PHASES
-// Phase profile of the job kernels (make EXTRA=-DBRA_PHASES): [wave jobs, workgroup jobs] x
-// {setup, gathers, sorts, groups+outputs, compaction, rounds, sum of P, jobs}; shader cycles of
-// the job's first wave.
-__device__ unsigned long long g_phase[2][8];
-#define PH_T(v) const unsigned long long v = (wj == 0) ? clock64() : 0
-#define PH_ADD(i, x)                                                                \
-    do                                                                              \
-    {                                                                               \
-        if (wj == 0 && lane_id() == 0)                                              \
-            atomicAdd(&g_phase[W > 1][i], (unsigned long long) (x));               \
-    } while (0)
-#else
-#define PH_T(v)
-#define PH_ADD(i, x)
-#endif
 
 template <uint32_t MODE, int W>
 __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj, const uint64_t* pre = nullptr)
 {
-    PH_T(t_start);
-#ifdef BRA_PHASES
-    unsigned long long t_setup = t_start;
-#endif
     using G                 = JobGeom<W>;
     const int       lane    = lane_id();
     const BlockDesc BD      = a.blocks[J.block];
@@ -2110,7 +1957,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     const uint64_t* K       = J.buf ? a.key1 : a.key0;
     const uint32_t* V       = J.buf ? a.pay1 : a.pay0;
     const uint32_t  boff    = (uint32_t) BD.off;
-    uint64_t        kh[4], kl[4], km[4];
+    uint64_t        key[4];  // sorted keys; after a sort: without the slot bits
     uint32_t        v[4];
     uint32_t        pos[4];  // job position of slot c
     uint32_t        g[4], gend[4];
@@ -2122,7 +1969,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                     MODE, W, J.start, T, J.block, (unsigned long long) BD.off, BD.len))
         T = 0;
     // Round 1.  STRING: all elements share their first d-1 bytes (one parent bucket), so the key
-    // is the rotation's bytes from depth d-1 -- its first byte orders the packed sub-buckets, no
+    // is the rotation's bits from depth d-1 -- its first byte orders the packed sub-buckets, no
     // group id and no carried key needed.  RANK: the 32-bit rank key.
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -2130,8 +1977,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         const uint32_t c = wj * 256 + lane * 4 + r;
         pos[r]           = c;
         v[r]             = 0;
-        kh[r] = ~0ull;
-        kl[r] = (G::KD == 3) ? 0xFFFFFFFFull : ~0ull;
+        key[r]           = ~0ull;  // padding: sorts last
         if (c < T)
         {
             // STRING payloads are the 64-bit MSD payloads in the key buffers (index in the low bits)
@@ -2140,71 +1986,39 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                             J.start + c))
                 v[r] = 0;
             if (MODE == MODE_RANK)
-            {
-                kh[r] = K[J.start + c];
-                kl[r] = c;
-            }
+                key[r] = K[J.start + c] | c;  // rank key in the top 32 bits
             else
             {
                 // STRING payloads carry an MSD digit in the top byte: replace it by the rotation's
                 // previous byte (its BWT output byte), gathered together with the key
                 const uint32_t idx = v[r] & 0xFFFFFFu;
-#ifdef BRA_EXP_NOGATHER
-                const uint8_t lb = 0;  // measurement variant: no gathers (results are wrong)
-                uint64_t      w0 = 0, w1 = ((uint64_t) idx << 20) ^ depth;
-#else
-#ifdef BRA_EXP_NOLB
-                const uint8_t lb = 0;  // measurement variant: no BWT-byte gather (results are wrong)
-#else
-                const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
-#endif
-                uint64_t      w0, w1;
+                const uint8_t  lb  = blk[idx ? idx - 1 : BD.len - 1];
                 // a single sub-bucket (every workgroup job, flagged wave jobs) shares byte d-1: its
                 // key starts at d
-                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, single ? depth : depth - 1), w0, w1);
-#endif
-                make_key1<W>(c, w0, w1, kh[r], kl[r]);
-                v[r] = ((uint32_t) lb << 24) | idx;
+                key[r] = make_key1<W>(c, pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, idx, single ? depth : depth - 1)));
+                v[r]   = ((uint32_t) lb << 24) | idx;
             }
         }
         S.v[c] = v[r];
     }
-#ifdef BRA_PHASES
-    t_setup = (wj == 0) ? clock64() : 0;
-    PH_ADD(0, t_setup - t_start);
-    PH_ADD(7, 1);
-#endif
     int P = 4;
     while ((uint32_t) P < T)
         P <<= 1;
-#ifdef BRA_EXP_NOSORT
-    P = 1;  // measurement variant: no sort network (results are wrong)
-#endif
-    PH_T(t_g1);
-#ifdef BRA_PHASES
-    if (MODE == MODE_STRING)
-        PH_ADD(1, t_g1 - t_setup);
-#endif
-    job_sort<W>(kh, kl, P, S, wj);
-    PH_T(t_s1);
-    PH_ADD(2, t_s1 - t_g1);
-    PH_ADD(5, 1);
-    PH_ADD(6, P);
+    job_sort<W>(key, P, S, wj);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        v[r]  = S.v[(uint32_t) (kl[r] & G::SMASK)];
-        km[r] = kl[r] & ~G::SMASK;
+        v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
+        key[r] &= ~G::SMASK;
     }
     if (MODE == MODE_STRING)
         depth += single ? G::ADV1 : G::ADV1 - 1;
     for (;;)
     {
-        PH_T(t_r0);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             S.pos[wj * 256 + lane * 4 + r] = (uint16_t) pos[r];
-        const bool any    = job_groups<W>(kh, km, T, S, wj, g, gend, tied);
+        const bool any    = job_groups<W>(key, T, S, wj, g, gend, tied);
         bool       finish = (MODE == MODE_RANK) || !any;
         bool final_ties = false, to_fallback = false;
         if (!finish && depth >= PK.nvb)  // tied on every bit of the cyclic string: identical rotations
@@ -2220,10 +2034,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 continue;
             const uint32_t slot = J.start + pos[r];
             const uint32_t idx  = v[r] & 0xFFFFFFu;
-#ifndef BRA_EXP_NOOUT
             a.fsa[slot]         = idx;
             a.L[slot]           = (uint8_t) (v[r] >> 24);
-#endif
             const uint32_t gst  = J.start + S.pos[g[r]] - boff;  // block-local start of the group
             if (MODE == MODE_RANK)
                 a.isa[BD.off + idx] = gst;
@@ -2250,8 +2062,6 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                     atomicExch(&a.ctr->overflow, 1u);
             }
         }
-        PH_T(t_r1);
-        PH_ADD(3, t_r1 - t_r0);
         if (finish)
             break;
         // ---- compact the tied slots; next round on the next ADV bytes ----
@@ -2268,8 +2078,6 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             }
         job_sync<W>();
         T = T2;
-        PH_T(t_r2);
-        PH_ADD(4, t_r2 - t_r1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -2278,33 +2086,24 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             {
                 const uint64_t gp = S.kh[c];
                 pos[r]            = (uint32_t) (gp & 0xFFFF);
-                uint64_t w0, w1;
-                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth), w0, w1);
-                make_key<W>((uint32_t) (gp >> 16), c, w0, w1, kh[r], kl[r]);
+                key[r]            = make_key<W>((uint32_t) (gp >> 16), c, pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth)));
             }
             else
             {
                 pos[r] = c;
-                kh[r]  = ~0ull;
-                kl[r]  = (G::KD == 3) ? 0xFFFFFFFFull : ~0ull;
+                key[r] = ~0ull;
             }
         }
         job_sync<W>();
         P = 4;
         while ((uint32_t) P < T)
             P <<= 1;
-        PH_T(t_r3);
-        PH_ADD(1, t_r3 - t_r2);
-        job_sort<W>(kh, kl, P, S, wj);
-        PH_T(t_r4);
-        PH_ADD(2, t_r4 - t_r3);
-        PH_ADD(5, 1);
-        PH_ADD(6, P);
+        job_sort<W>(key, P, S, wj);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            v[r]  = S.v[(uint32_t) (kl[r] & G::SMASK)];
-            km[r] = kl[r] & ~G::SMASK;
+            v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
+            key[r] &= ~G::SMASK;
         }
         depth += G::ADV;
     }
@@ -2415,13 +2214,21 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
     }
 }
 
-// Block-major, XCD-major job order: key(b) = (b % 8) * kb + b / 8.
-// Size class first (jobs longer than split_len after the others; split_len 0 = one class).
-// With many blocks, q consecutive blocks of one XCD share a key (q = 1 up to 8192 blocks), so the
-// keys of a list fit the LDS counters of the ordering kernels.
-__device__ __forceinline__ uint32_t job_key(const Job& J, uint32_t kb, uint32_t q, uint32_t split_len)
+// Workgroup-job size classes: a job of (256, 512] elements runs on 2 waves, (512, 1024] on 4,
+// (1024, 2048] on 8, (2048, 4096] on 16 (never more waves than the job's network needs).
+constexpr uint32_t MJ_CLASSES = 4;
+__device__ __forceinline__ uint32_t mjob_class(uint32_t len, uint32_t classes)
 {
-    const uint32_t sc = (split_len && J.len > split_len) ? 1u : 0u;
+    const uint32_t lg = 32u - (uint32_t) __builtin_clz(max(len, 257u) - 1u);  // ceil(log2(len)) >= 9
+    return min(lg - 9u, classes - 1u);
+}
+
+// Block-major, XCD-major job order: key(b) = (b % 8) * kb + b / 8, size class first (classes = 1:
+// one class).  With many blocks, q consecutive blocks of one XCD share a key (q = 1 up to 4096
+// blocks), so the keys of a list fit the LDS counters of the ordering kernels.
+__device__ __forceinline__ uint32_t job_key(const Job& J, uint32_t kb, uint32_t q, uint32_t classes)
+{
+    const uint32_t sc = classes > 1 ? mjob_class(J.len, classes) : 0u;
     return sc * 8 * kb + (J.block & 7u) * kb + (J.block >> 3) / q;
 }
 
@@ -2431,7 +2238,7 @@ constexpr uint32_t JOB_CHUNK = 4096;  // jobs per workgroup of the ordering kern
 // to the global ones (one atomic per key and workgroup instead of one per job: thousands of jobs of
 // one block share a key, and same-address device atomics serialise).  nkeys <= lds capacity.
 __global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs, const uint32_t* __restrict__ pb, const uint32_t* __restrict__ pn,
-                                                   uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cnt)
+                                                   uint32_t kb, uint32_t q, uint32_t classes, uint32_t nkeys, uint32_t* __restrict__ cnt)
 {
     extern __shared__ uint32_t h[];
     const uint32_t b0 = pb ? dev_count(pb) : 0u, n = dev_count(pn);
@@ -2442,7 +2249,7 @@ __global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs,
         __syncthreads();
         const uint32_t c1 = min(n, c0 + JOB_CHUNK);
         for (uint32_t j = c0 + threadIdx.x; j < c1; j += 256)
-            atomicAdd(&h[job_key(jobs[j], kb, q, split_len)], 1u);
+            atomicAdd(&h[job_key(jobs[j], kb, q, classes)], 1u);
         __syncthreads();
         for (uint32_t k = threadIdx.x; k < nkeys; k += 256)
             if (h[k])
@@ -2454,7 +2261,7 @@ __global__ void __launch_bounds__(256) k_job_count(const Job* __restrict__ jobs,
 // Scatter into key order: per chunk, local ranks from LDS atomics, one global cursor reservation per
 // nonzero key and workgroup.  (Job order within a key only affects speed.)
 __global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in, const uint32_t* __restrict__ pb, const uint32_t* __restrict__ pn,
-                                                     uint32_t kb, uint32_t q, uint32_t split_len, uint32_t nkeys, uint32_t* __restrict__ cursor,
+                                                     uint32_t kb, uint32_t q, uint32_t classes, uint32_t nkeys, uint32_t* __restrict__ cursor,
                                                      Job* __restrict__ out)
 {
     extern __shared__ uint32_t h[];
@@ -2472,7 +2279,7 @@ __global__ void __launch_bounds__(256) k_job_scatter(const Job* __restrict__ in,
             const uint32_t j = c0 + threadIdx.x + i * 256;
             if (j < n)
             {
-                key[i]  = job_key(in[j], kb, q, split_len);
+                key[i]  = job_key(in[j], kb, q, classes);
                 rank[i] = atomicAdd(&h[key[i]], 1u);
             }
         }
@@ -2549,12 +2356,12 @@ __global__ void __launch_bounds__(256) k_tile_prefix(const uint32_t* __restrict_
         xseg[8] = carry;
 }
 
-// One workgroup: the job lists' key counts cnt[list][class][nkeys] (k_job_count) -> cursors of the same
-// layout and the per-XCD ranges of the three job launches, seg[16 * k + x] (x = 0..8): k = 0 the
-// wave jobs, k = 1 / 2 the workgroup jobs of the small / large size class.  The two classes of a
-// list are stored one after the other (class 1 after class 0).
-__global__ void __launch_bounds__(256) k_job_prefix(const uint32_t* __restrict__ cnt, uint32_t nkeys, uint32_t kb, uint32_t* __restrict__ cursor,
-                                                    uint32_t* __restrict__ seg)
+// One workgroup: the job lists' key counts cnt[list][class][nk] (k_job_count) -> cursors of the same
+// layout and the per-XCD ranges of the job launches, seg[16 * k + x] (x = 0..8): k = 0 the wave
+// jobs (list 0, one class), k = 1 + c the workgroup jobs of size class c (list 1).  The classes of
+// a list are stored one after the other.
+__global__ void __launch_bounds__(256) k_job_prefix(const uint32_t* __restrict__ cnt, uint32_t nk, uint32_t kb, uint32_t classes,
+                                                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ seg)
 {
     __shared__ uint32_t tmp[8];
     __shared__ uint32_t carry;
@@ -2563,22 +2370,22 @@ __global__ void __launch_bounds__(256) k_job_prefix(const uint32_t* __restrict__
         if (threadIdx.x == 0)
             carry = 0;
         __syncthreads();
-        for (uint32_t c = 0; c < 2; ++c)
+        const uint32_t nc = l == 0 ? 1u : classes;
+        for (uint32_t c = 0; c < nc; ++c)
         {
-            const bool      used = (l == 1 || c == 0);
-            uint32_t*       xs   = seg + 16 * (l == 0 ? 0 : 1 + c);
-            const uint32_t* hc   = cnt + ((size_t) l * 2 + c) * nkeys;
-            uint32_t*       hu   = cursor + ((size_t) l * 2 + c) * nkeys;
-            for (uint32_t k0 = 0; k0 < nkeys; k0 += 256)
+            uint32_t*       xs = seg + 16 * (l == 0 ? 0 : 1 + c);
+            const uint32_t* hc = cnt + ((size_t) l * MJ_CLASSES + c) * nk;
+            uint32_t*       hu = cursor + ((size_t) l * MJ_CLASSES + c) * nk;
+            for (uint32_t k0 = 0; k0 < nk; k0 += 256)
             {
                 const uint32_t k = k0 + threadIdx.x;
-                const uint32_t v = k < nkeys ? hc[k] : 0u;
+                const uint32_t v = k < nk ? hc[k] : 0u;
                 uint32_t       tot;
                 const uint32_t ex = block256_exclusive_sum(v, tmp, &tot) + carry;
-                if (k < nkeys)
+                if (k < nk)
                 {
                     hu[k] = ex;
-                    if (used && k % kb == 0)
+                    if (k % kb == 0)
                         xs[k / kb] = ex;
                 }
                 __syncthreads();
@@ -2586,7 +2393,7 @@ __global__ void __launch_bounds__(256) k_job_prefix(const uint32_t* __restrict__
                     carry += tot;
                 __syncthreads();
             }
-            if (used && threadIdx.x == 0)
+            if (threadIdx.x == 0)
                 xs[8] = carry;
             __syncthreads();
         }
@@ -2838,8 +2645,8 @@ struct BwtWorkspace
     Job*      mjobs          = nullptr;
     Job*      jobs_sorted    = nullptr;  // block-major, XCD-major copies (order_jobs)
     Job*      mjobs_sorted   = nullptr;
-    uint32_t* job_cnt        = nullptr;  // 2 lists x 2 size classes x 8 * ceil(blocks / 8) keys, then the cursors
-    uint32_t* jseg           = nullptr;  // per-XCD ranges of the three job launches (k_job_prefix), 3 x 16 dwords
+    uint32_t* job_cnt        = nullptr;  // 2 lists x MJ_CLASSES size classes x 8 * ceil(blocks / 8) keys, then the cursors
+    uint32_t* jseg           = nullptr;  // per-XCD ranges of the job launches (k_job_prefix), (1 + MJ_CLASSES) x 16 dwords
     uint32_t* tile_cnt       = nullptr;  // MSD tile order: key counts, cursors, xseg[9]
     TileDesc* tile_order     = nullptr;
     TileDesc* tdesc[2]       = {nullptr, nullptr};  // STRING: tile-order descriptors written by the scan (per level, ping-pong)
@@ -2857,24 +2664,17 @@ struct BwtWorkspace
     std::vector<BlockDesc> geo;          // block geometry the level-0 tiles / buckets on the device were built for
     uint32_t  nt0 = 0;
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
-    int       grid = 16384;  // workgroups of the MSD / level-0 tile kernels (env BRA_GRID; 2048: 11.9, 8192: 12.3, 16384: 12.5 GB/s)
-    uint32_t  scan_grid = 4096;         // workgroups of a level's scan (4 buckets each per pass; env BRA_SCAN_GRID)
-    uint32_t  lookahead = 2;            // MSD levels enqueued before the host has seen the bucket count they consume (env BRA_LOOKAHEAD)
-    int       mj_waves = MJ_WAVES_DEF;  // 0: no workgroup jobs
-    uint32_t  jobs_grid = 2048;         // workgroups of the wave-job launch (env BRA_JOBS_GRID): about the resident
-                                        // capacity (6 waves/SIMD = 1536 four-wave groups); with the dynamic job
-                                        // queues extra groups only cost launch overhead (8192: 2.94 ms, 2048: 2.67)
-    uint32_t* jobq      = nullptr;      // per-XCD claim counters of the three job launches (3 x 8 x 32 dwords)
-    int       jobq_on   = 1;            // dynamic job order (env BRA_JOBQ=0: static strides)
-    int       tile_order_mode = 1;      // MSD tile order: 0 scan order, 1 XCD-major on re-gather levels, 2 always (env BRA_TILE_ORDER)
-    uint32_t  jobq_chunk = 2;           // wave jobs claimed at once (env BRA_JOBQ_CH)
-    hipStream_t s2      = nullptr;      // job stream: the jobs of the first levels run beside the later MSD levels
-    hipEvent_t  ev_a = nullptr, ev_j = nullptr;
-    uint32_t*   snap      = nullptr;    // job counts at the phase boundary (k_job_snap)
-    int         overlap   = 0;          // env BRA_OVERLAP=1: two job phases (measured slower: the levels starve)
-    uint32_t    grid_div_a = 2;         // phase-1 job launches use 1/grid_div_a of the resident capacity (env BRA_JOBS_DIV_A)
-    uint32_t  nblocks   = 0;            // blocks of the current call
-    uint32_t  levels    = 0;            // MSD levels enqueued by the last STRING level loop
+    int       grid       = 16384;     // workgroups of the MSD / level-0 tile kernels (2048: 11.9, 8192: 12.3, 16384: 12.5 GB/s)
+    uint32_t  scan_grid  = 4096;      // workgroups of a level's scan (4 buckets each per pass)
+    uint32_t  lookahead  = 2;         // MSD levels enqueued before the host has seen the bucket count they consume
+    int       mj_waves   = MJ_WAVES_DEF;  // waves of the largest workgroup job (0: no workgroup jobs)
+    uint32_t  jobs_grid  = 2048;      // workgroups of the wave-job launch: about the resident capacity (with the
+                                      // dynamic job queues extra groups only cost launch overhead: 8192: 2.94 ms, 2048: 2.67)
+    uint32_t* jobq       = nullptr;   // per-XCD claim counters of the job launches ((1 + MJ_CLASSES) x 8 x 32 dwords)
+    uint32_t  jobq_chunk = 2;         // wave jobs claimed at once
+    uint32_t  nblocks    = 0;         // blocks of the current call
+    uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
+    uint32_t  mj_classes() const { return mj_waves >= 16 ? 4u : mj_waves >= 8 ? 3u : mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
@@ -2938,37 +2738,36 @@ static bool post_wait(BwtWorkspace& w, uint32_t slot, hipStream_t s, Mail& out)
 }
 
 // Reorder the wave-job and workgroup-job lists block-major per XCD (see job_range), all on the
-// device: count jobs per key, k_job_prefix (cursors + the three launches' per-XCD ranges), scatter.
-// The workgroup jobs are also split into two size classes (<= half the workgroup-job size, larger):
-// out[0] wave jobs, out[1] small workgroup jobs, out[2] large ones.  The job counts are read on the
-// device (counters slot 0), so the host never waits for them.
-static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[3], hipStream_t s,
-                       const uint32_t* beg = nullptr, const uint32_t* end = nullptr)
+// device: count jobs per key, k_job_prefix (cursors + the launches' per-XCD ranges), scatter.  The
+// workgroup jobs are also split into size classes (mjob_class): out[0] wave jobs, out[1 + c] the
+// workgroup jobs of class c.  The job counts are read on the device (counters slot 0), so the host
+// never waits for them.
+static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, const JobArgs& jm, JobArgs (&out)[1 + MJ_CLASSES], hipStream_t s)
 {
-    const uint32_t  kb0 = div_up(nblocks, 8), q = div_up(kb0, 1024u);
-    const uint32_t  kb = div_up(kb0, q), nk = 8 * kb;  // keys per size class (<= 8192)
-    const uint32_t  split[2] = {0, w.mjob_max() / 2};
-    const Job*      src[2]   = {w.jobs, w.mjobs};
-    Job*            dst[2]   = {w.jobs_sorted, w.mjobs_sorted};
-    const uint32_t* pn[2]    = {end ? end : &w.ctr[0].n_jobs, end ? end + 1 : &w.ctr[0].n_mjobs};
-    const uint32_t* pb[2]    = {beg, beg ? beg + 1 : nullptr};
-    uint32_t*       dcnt     = w.job_cnt;                    // [list][class][nk] counts
-    uint32_t*       dcur     = w.job_cnt + 4 * (size_t) nk;  // cursors, same layout
+    const uint32_t  kb0 = div_up(nblocks, 8), q = div_up(kb0, 512u);
+    const uint32_t  kb = div_up(kb0, q), nk = 8 * kb;  // keys per size class (<= 4096)
+    const uint32_t  classes[2] = {1, w.mj_classes()};
+    const Job*      src[2]     = {w.jobs, w.mjobs};
+    Job*            dst[2]     = {w.jobs_sorted, w.mjobs_sorted};
+    const uint32_t* pn[2]      = {&w.ctr[0].n_jobs, &w.ctr[0].n_mjobs};
+    uint32_t*       dcnt       = w.job_cnt;                                // [list][class][nk] counts
+    uint32_t*       dcur       = w.job_cnt + 2 * MJ_CLASSES * (size_t) nk;  // cursors, same layout
     const dim3      g(1024);
-    BRA_HIP_CHECK(hipMemsetAsync(dcnt, 0, 4 * (size_t) nk * 4, s));
+    BRA_HIP_CHECK(hipMemsetAsync(dcnt, 0, 2 * MJ_CLASSES * (size_t) nk * 4, s));
     for (int l = 0; l < 2; ++l)
     {
-        hipLaunchKernelGGL(k_job_count, g, dim3(256), 2 * nk * 4, s, src[l], pb[l], pn[l], kb, q, split[l], 2 * nk, dcnt + (size_t) l * 2 * nk);
+        hipLaunchKernelGGL(k_job_count, g, dim3(256), classes[l] * nk * 4, s, src[l], nullptr, pn[l], kb, q, classes[l], classes[l] * nk,
+                           dcnt + (size_t) l * MJ_CLASSES * nk);
         BRA_DSYNC(s);
     }
-    hipLaunchKernelGGL(k_job_prefix, dim3(1), dim3(256), 0, s, dcnt, nk, kb, dcur, w.jseg); BRA_DSYNC(s);
+    hipLaunchKernelGGL(k_job_prefix, dim3(1), dim3(256), 0, s, dcnt, nk, kb, classes[1], dcur, w.jseg); BRA_DSYNC(s);
     for (int l = 0; l < 2; ++l)
     {
-        hipLaunchKernelGGL(k_job_scatter, g, dim3(256), 2 * nk * 4, s, src[l], pb[l], pn[l], kb, q, split[l], 2 * nk, dcur + (size_t) l * 2 * nk,
-                           dst[l]);
+        hipLaunchKernelGGL(k_job_scatter, g, dim3(256), classes[l] * nk * 4, s, src[l], nullptr, pn[l], kb, q, classes[l], classes[l] * nk,
+                           dcur + (size_t) l * MJ_CLASSES * nk, dst[l]);
         BRA_DSYNC(s);
     }
-    for (int k = 0; k < 3; ++k)
+    for (uint32_t k = 0; k < 1 + MJ_CLASSES; ++k)
     {
         out[k]           = k == 0 ? ja : jm;
         out[k].jobs      = k == 0 ? dst[0] : dst[1];
@@ -2982,13 +2781,11 @@ static bool order_jobs(BwtWorkspace& w, uint32_t nblocks, const JobArgs& ja, con
 
 static uint32_t round8(uint32_t g) { return (g + 7u) & ~7u; }
 
-static uint32_t g_mjobs_grid = 0;  // workgroups of a workgroup-job launch (env BRA_MJOBS_GRID; 0 = by size class)
-
 template <uint32_t MODE>
-static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s, uint32_t div = 1)
+static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
 {
-    // about the resident capacity: 2-wave jobs fit twice as many groups per CU as 4-wave ones
-    const uint32_t cap = (g_mjobs_grid ? g_mjobs_grid : (waves <= 2 ? 3072u : 1536u)) / div;
+    // about the resident capacity: 6144 waves (24 per CU)
+    const uint32_t cap = 6144u / (uint32_t) waves;
     const dim3     g(round8(std::min<uint32_t>(n, cap)));
     if (waves == 16)
         hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>) + 16, s, a);
@@ -3024,13 +2821,6 @@ static void ws_free(BwtWorkspace& w)
         (void) hipHostFree(w.h_ctr);
     if (w.h_mail)
         (void) hipHostFree(w.h_mail);
-    (void) hipFree(w.snap);
-    if (w.ev_a)
-        (void) hipEventDestroy(w.ev_a);
-    if (w.ev_j)
-        (void) hipEventDestroy(w.ev_j);
-    if (w.s2)
-        (void) hipStreamDestroy(w.s2);
     w = BwtWorkspace{};
 }
 
@@ -3044,34 +2834,14 @@ void          bwt_workspace_destroy(BwtWorkspace* w)
     }
 }
 
-// Tuning knobs from the environment (ws_free resets the workspace, so they are applied after it).
+// Largest workgroup job from the environment (BRA_MJ_WAVES = 2, 4, 8 or 16; measurement only).
 static void ws_env(BwtWorkspace& w)
 {
-    if (const char* e = getenv("BRA_MJ_WAVES"))  // tuning knob: 0 (off), 2, 4, 8 or 16 waves per workgroup job
+    if (const char* e = getenv("BRA_MJ_WAVES"))
     {
         const int v = atoi(e);
-        w.mj_waves  = (v == 0 || v == 2 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
+        w.mj_waves  = (v == 2 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
     }
-    if (const char* e = getenv("BRA_JOBS_GRID"))
-        w.jobs_grid = std::max(8, atoi(e));
-    if (const char* e = getenv("BRA_MJOBS_GRID"))
-        g_mjobs_grid = std::max(8, atoi(e));
-    if (const char* e = getenv("BRA_JOBQ"))
-        w.jobq_on = atoi(e) != 0;
-    if (const char* e = getenv("BRA_GRID"))  // workgroups of the MSD / level-0 tile kernels
-        w.grid = std::max(8, atoi(e));
-    if (const char* e = getenv("BRA_SCAN_GRID"))
-        w.scan_grid = (uint32_t) std::max(8, atoi(e));
-    if (const char* e = getenv("BRA_LOOKAHEAD"))
-        w.lookahead = (uint32_t) std::max(1, atoi(e));
-    if (const char* e = getenv("BRA_TILE_ORDER"))
-        w.tile_order_mode = atoi(e);
-    if (const char* e = getenv("BRA_JOBQ_CH"))
-        w.jobq_chunk = (uint32_t) std::max(1, atoi(e));
-    if (const char* e = getenv("BRA_OVERLAP"))
-        w.overlap = atoi(e) != 0;
-    if (const char* e = getenv("BRA_JOBS_DIV_A"))
-        w.grid_div_a = (uint32_t) std::max(1, atoi(e));
 }
 
 static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
@@ -3103,13 +2873,11 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     ok = ok && dev_alloc(w.fsa, N) && dev_alloc(w.isa, N) && dev_alloc(w.tile_hist, (uint64_t) tmax * 256) &&
          dev_alloc(w.tile_off, (uint64_t) tmax * 256) && dev_alloc(w.nomove, std::max<uint32_t>(w.cap_big, B)) && dev_alloc(w.flag, B) &&
          dev_alloc(w.jobs, w.cap_jobs) && dev_alloc(w.mjobs, w.cap_mjobs) && dev_alloc(w.jobs_sorted, cap_sorted) &&
-         dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 8 * nkeys) && dev_alloc(w.jseg, 3 * 16) &&
+         dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 4 * MJ_CLASSES * nkeys) && dev_alloc(w.jseg, (1 + MJ_CLASSES) * 16) &&
          dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
-         dev_alloc(w.jobq, 3 * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
+         dev_alloc(w.jobq, (1 + MJ_CLASSES) * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
          dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B) &&
          dev_alloc(w.tmask, 8ull * w.cap_l0);
-    ok = ok && dev_alloc(w.snap, 16) && hipStreamCreateWithFlags(&w.s2, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&w.ev_a, hipEventDisableTiming) == hipSuccess && hipEventCreateWithFlags(&w.ev_j, hipEventDisableTiming) == hipSuccess;
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -3130,50 +2898,35 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
 
 static size_t tile_stage_bytes() { return sizeof(TileStage); }
 
-// The STRING jobs of one phase, enqueued on w.s2 behind everything enqueued on s so far: order the
-// jobs appended between the counts at `beg` and `end` (device words; null beg = 0, null end = the
-// call-wide counts) block-major per XCD, then the wave-job and the two workgroup-job launches.
-// Phase 1 takes the jobs of level 0 and level 1 while s goes on with the deeper MSD levels: the
-// job kernels are VALU bound and the levels memory bound, so they share the CUs (phase 1 launches
-// about 1/grid_div_a of the resident capacity, the levels' tiles fill the rest).  Jobs are final
-// when emitted: no later level touches their slots.  Phase 2 takes the rest after the last level.
+// The STRING jobs of a call, after the last MSD level: order the jobs block-major per XCD, then
+// the wave-job launch and one workgroup-job launch per size class.  Jobs are final when emitted:
+// no later level touches their slots.
 struct JobPhase
 {
     JobArgs  ja, jm;
     uint32_t nblocks;
 };
 
-static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s, const uint32_t* beg, const uint32_t* end, uint32_t div)
+static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
 {
-    hipStream_t s2 = w.s2;
-    BRA_HIP_CHECK(hipEventRecord(w.ev_a, s));
-    BRA_HIP_CHECK(hipStreamWaitEvent(s2, w.ev_a, 0));
-    JobArgs ord[3];
-    if (!order_jobs(w, ph.nblocks, ph.ja, ph.jm, ord, s2, beg, end))
+    JobArgs ord[1 + MJ_CLASSES];
+    if (!order_jobs(w, ph.nblocks, ph.ja, ph.jm, ord, s))
         return false;
-    if (w.jobq_on)
+    BRA_HIP_CHECK(hipMemsetAsync(w.jobq, 0, (1 + MJ_CLASSES) * 8 * 32 * 4, s));
+    for (uint32_t k = 0; k < 1 + MJ_CLASSES; ++k)
     {
-        BRA_HIP_CHECK(hipMemsetAsync(w.jobq, 0, 3 * 8 * 32 * 4, s2));
-        for (int k = 0; k < 3; ++k)
-        {
-            ord[k].jq       = w.jobq + k * 8 * 32;
-            ord[k].jq_chunk = w.jobq_chunk;
-        }
+        ord[k].jq       = w.jobq + k * 8 * 32;
+        ord[k].jq_chunk = w.jobq_chunk;
     }
     {
-        BRA_PROF(P_BWT_JOBS, s2);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(std::max<uint32_t>(w.jobs_grid / div, 8))), dim3(256), 0, s2, ord[0]);
-        BRA_DSYNC(s2);
+        BRA_PROF(P_BWT_JOBS, s);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, s, ord[0]);
+        BRA_DSYNC(s);
     }
     {
-        // workgroup jobs of at most half the size run on half the waves
-        BRA_PROF(P_BWT_MJOBS, s2);
-        const int half = w.mj_waves / 2;
-        if (w.mj_waves)
-        {
-            launch_mjobs<MODE_STRING>(half >= 2 ? half : w.mj_waves, ~0u, ord[1], s2, div);
-            launch_mjobs<MODE_STRING>(w.mj_waves, ~0u, ord[2], s2, div);
-        }
+        BRA_PROF(P_BWT_MJOBS, s);
+        for (uint32_t c = 0; c < w.mj_classes(); ++c)
+            launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     return true;
@@ -3187,7 +2940,7 @@ static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s, const u
 // Sub-buckets become jobs / fallback groups (appended to the call-wide lists, slot 0).
 template <uint32_t MODE>
 static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, int cur, Group* groups_out, hipStream_t s,
-                       uint32_t first_seq, const JobPhase* phase1 = nullptr)
+                       uint32_t first_seq)
 {
     const size_t   lds    = tile_stage_bytes();
     const int      grid   = w.grid;
@@ -3208,7 +2961,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
         {
             const uint32_t  lvl_d   = k;
             const bool      rg      = lvl_d + 1 - lvl_kd >= CARRY;
-            const bool      ordered = w.tile_order_mode == 2 || (w.tile_order_mode == 1 && rg);
+            const bool      ordered = rg;
             const Counters* lin     = w.ctr + k;
             Counters*       lout    = w.ctr + k + 1;
             TileOrder       to{nullptr, nullptr, 0};
@@ -3254,12 +3007,6 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             }
             BRA_HIP_CHECK(hipGetLastError());
             seqs[k + 1] = post(w, k + 1, s);
-            if (phase1 && k == 1)
-            {
-                hipLaunchKernelGGL(k_job_snap, dim3(1), dim3(64), 0, s, w.ctr, w.snap);
-                if (!run_jobs(w, *phase1, s, nullptr, w.snap, w.grid_div_a))
-                    return false;
-            }
             cur ^= 1;
             if (rg)
                 lvl_kd = lvl_d + 1;
@@ -3414,20 +3161,18 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     prof_bytes(P_BWT_L0HIST, (double) N + 1024.0 * nt0);
     prof_bytes(P_BWT_SCAN, 3072.0 * nt0);
     prof_bytes(P_BWT_L0SCATTER, 9.0 * N + 1024.0 * nt0);  // window in, payload out
-    // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]; the jobs of levels
-    // 0 and 1 run on w.s2 beside the deeper levels (run_jobs), the rest after the last level
+    // level-0 sub-buckets all live in KV buffer 0, their tiles in tile_bucket[0]; the jobs run after
+    // the last level
     JobPhase ph;
     ph.ja = JobArgs{w.jobs,  0,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
                     w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0, w.packed, w.pkd};
     ph.jm      = ph.ja;
     ph.jm.jobs = w.mjobs;
     ph.nblocks = nblocks;
-    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s), w.overlap ? &ph : nullptr))
+    if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s)))
         return false;
-    if (!run_jobs(w, ph, s, w.overlap ? w.snap : nullptr, nullptr, 1))
+    if (!run_jobs(w, ph, s))
         return false;
-    BRA_HIP_CHECK(hipEventRecord(w.ev_j, w.s2));
-    BRA_HIP_CHECK(hipStreamWaitEvent(s, w.ev_j, 0));
     BRA_HIP_CHECK(hipGetLastError());
     if (!account_levels<MODE_STRING>(w, s))
         return false;
@@ -3447,17 +3192,6 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     Mail mc{};
     if (!post_wait(w, 0, s, mc))
         return false;
-#ifdef BRA_PHASES
-    {
-        unsigned long long ph[2][8];
-        BRA_HIP_CHECK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof ph));
-        for (int k = 0; k < 2; ++k)
-            fprintf(stderr, "[phases %s] setup %llu gather %llu sort %llu groups+out %llu compact %llu | rounds %llu sumP %llu jobs %llu\n",
-                    k ? "mjobs" : "jobs", ph[k][0], ph[k][1], ph[k][2], ph[k][3], ph[k][4], ph[k][5], ph[k][6], ph[k][7]);
-        std::memset(ph, 0, sizeof ph);
-        BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof ph));
-    }
-#endif
     // SURVEY 8.1(d) BWT model: 11 algorithmic bytes per element (input read, SA written and
     // re-read, L gathered and written), charged to the job kernels by the elements each kind covers
     if (g_prof && (g_prof->mask >> P_BWT_JOBS & 1 || g_prof->mask >> P_BWT_MJOBS & 1))

@@ -1647,11 +1647,7 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
         BRA_PROF(P_HUF_OFFSETS, s);
         hipLaunchKernelGGL(k_huff_offsets, dim3(1), dim3(TPB), 0, s, d_meta, nblocks, d_payload_off);
     }
-    static const uint32_t grid_cap = [] {  // workgroups of the tile kernels (env BRA_HUF_GRID)
-        const char* e = getenv("BRA_HUF_GRID");
-        return e ? (uint32_t) std::max(8, atoi(e)) : 32768u;  // 8192: 0.03 ms slower per stage
-    }();
-    const uint32_t grid = std::min<uint32_t>(nt, grid_cap);
+    const uint32_t grid = std::min<uint32_t>(nt, 32768u);  // workgroups of the tile kernels (8192: 0.03 ms slower per stage)
     {
         BRA_PROF(P_HUF_TILEBITS, s);
         hipLaunchKernelGGL(k_huff_tilebits, dim3(grid), dim3(TPB), 0, s, d_rle, w.tiling.d_pieces, nt, d_meta, w.tbits);

@@ -8,8 +8,9 @@
 // initial identity table is the recency order of a virtual prefix 255, 254, ..., 0).  So
 //   k_mtf_lastocc   last occurrence of every symbol inside each segment (LDS atomicMax),
 //   k_mtf_scan      exclusive max-scan over the segments of a block -> start-of-segment times,
-//   k_mtf_encode    each thread rebuilds its segment's start table (a wave sorts 256 times per
-//                   table) and runs the sequential MTF on a private LDS table.
+//   k_mtf_encode_reg   blocks of <= MTF_REG distinct symbols: one thread per segment, the table
+//                      front in registers;
+//   k_mtf_encode_wave  larger alphabets: one wave per segment, 64 symbols per step (ballots).
 // Decode uses relabelling: a decode step moves table POSITION p to the front whatever the table
 // holds, so decoding a segment from the identity table gives labels u_i and an end permutation
 // P_k; the true start tables satisfy S_{k+1}[j] = S_k[P_k[j]] and the output is S_k[u_i].
@@ -117,17 +118,6 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
     }
 }
 
-// Encode: the table of thread t occupies TSTRIDE dwords at tbl[t * TSTRIDE] (dword w holds entries
-// 4w..4w+3, little-endian); the 4-dword pad makes 16-byte reads of 16 consecutive lanes hit
-// disjoint banks.  (Decode keeps its own interleaved layout, tbl[w * TPB + t].)
-constexpr uint32_t TSTRIDE = 68;
-__device__ __forceinline__ uint32_t start_table_dword(const int32_t* __restrict__ st);
-
-__device__ __forceinline__ void build_table_wave(const int32_t* __restrict__ st, uint32_t* tbl, uint32_t owner)
-{
-    tbl[owner * TSTRIDE + lane_id()] = start_table_dword(st);
-}
-
 // Stage (SIZE, J) of a bitonic network over 256 unique 32-bit keys, 4 per lane (slot 4 lane + r),
 // ascending, and recursively the rest of its merge phase: partners J >= 4 slots away sit J / 4
 // lanes away (DPP / permlane, xlane), closer ones in the same lane.  A compare-exchange of 32-bit
@@ -227,166 +217,6 @@ __device__ __forceinline__ uint32_t shift_upto(uint32_t cur, uint32_t below_top,
 {
     const uint32_t keep = (b == 3) ? 0u : (0xFFFFFFFFu << (8 * (b + 1)));
     return (cur & keep) | (((cur << 8) | below_top) & ~keep);
-}
-
-// One 16-entry LDS chunk d of the table during a search for c (cc = c in every byte): if c is in
-// it, shift the entries below it up by one (the entry `top` enters at 0), store, set r to c's
-// position in the chunk and return true; otherwise shift the whole chunk, store, and carry its top
-// entry out in `top`.
-__device__ __forceinline__ bool mtf_chunk(const uint4& v, uint32_t cc, uint32_t c, uint32_t& top, uint32_t* dst, uint32_t& r)
-{
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-    uint32_t       zc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        zc[k] = haszero8(d[k] ^ cc);
-    uint32_t o[4];
-    if (zc[0] | zc[1] | zc[2] | zc[3])
-    {
-        const uint32_t k  = zc[0] ? 0 : zc[1] ? 1 : zc[2] ? 2 : 3;
-        const uint32_t zz = zc[0] ? zc[0] : zc[1] ? zc[1] : zc[2] ? zc[2] : zc[3];
-        const uint32_t b  = (uint32_t) __builtin_ctz(zz) >> 3;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            const uint32_t ntop = d[q] >> 24;
-            o[q]                = ((uint32_t) q < k) ? shift1(d[q], top) : ((uint32_t) q == k) ? shift_upto(d[q], top, b) : d[q];
-            top                 = ntop;
-        }
-        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-        r                              = k * 4 + b;
-        return true;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-    {
-        const uint32_t ntop = d[q] >> 24;
-        o[q]                = shift1(d[q], top);
-        top                 = ntop;
-    }
-    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-    (void) c;
-    return false;
-}
-
-// One MTF step.  Entries 0..15 live in registers R; entries 16..255 in this thread's LDS table,
-// read, checked and written back shifted 16 entries at a time (one ds_read_b128 / ds_write_b128
-// pair per chunk) until the chunk holding the symbol.  Returns the symbol's position.
-__device__ __forceinline__ uint32_t mtf_step(uint32_t (&R)[4], uint32_t* tbl, uint32_t c)
-{
-    const uint32_t cc = c * 0x01010101u;
-    uint32_t       z[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        z[k] = haszero8(R[k] ^ cc);
-    if (z[0] | z[1] | z[2] | z[3])
-    {
-        const uint32_t k = z[0] ? 0 : z[1] ? 1 : z[2] ? 2 : 3;
-        const uint32_t zz = z[0] ? z[0] : z[1] ? z[1] : z[2] ? z[2] : z[3];
-        const uint32_t b = (uint32_t) __builtin_ctz(zz) >> 3;
-        uint32_t       top = c;  // entry entering dword 0
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            const uint32_t cur = R[q], ntop = cur >> 24;
-            if ((uint32_t) q < k)
-                R[q] = shift1(cur, top);
-            else if ((uint32_t) q == k)
-                R[q] = shift_upto(cur, top, b);
-            top = ntop;
-        }
-        return k * 4 + b;
-    }
-    // not in the register chunk: shift it fully, carry its top entry into the LDS chunks
-    uint32_t top = c;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-    {
-        const uint32_t cur = R[q], ntop = cur >> 24;
-        R[q]                = shift1(cur, top);
-        top                 = ntop;
-    }
-    // Chunks are visited two at a time: both 16-byte reads are issued together, so a deep search
-    // waits for one LDS round trip per 32 entries.  (Chunk 16 is the row's pad: it is read with
-    // chunk 15 but never examined, since the symbol is found by chunk 15 at the latest.)
-    for (uint32_t ch = 1; ch < 16; ch += 2)
-    {
-        const uint4 va = *reinterpret_cast<const uint4*>(tbl + ch * 4);
-        const uint4 vb = *reinterpret_cast<const uint4*>(tbl + ch * 4 + 4);
-        uint32_t    r;
-        if (mtf_chunk(va, cc, c, top, tbl + ch * 4, r))
-            return ch * 16 + r;
-        if (mtf_chunk(vb, cc, c, top, tbl + ch * 4 + 4, r))
-            return ch * 16 + 16 + r;
-    }
-    return 255;  // unreachable: the table is a permutation of 0..255
-}
-
-// Sequential MTF of one segment on this thread's table (tbl = its TSTRIDE dwords).  Input is read
-// and output written 16 bytes at a time (the next 16 input bytes are loaded before the current
-// ones are coded) whenever the segment is 16-byte aligned; the ragged tail goes byte by byte.
-__device__ __forceinline__ void mtf_encode_segment(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece P, uint32_t* tbl)
-{
-    const uint8_t* src = in + P.off;
-    uint8_t*       dst = out + P.off;
-    uint32_t       R[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        R[k] = tbl[k];
-    uint32_t i = 0;
-    if ((((uintptr_t) src | (uintptr_t) dst) & 15) == 0 && P.len >= 16)
-    {
-        const uint32_t nv  = P.len / 16;
-        uint4          nxt = reinterpret_cast<const uint4*>(src)[0];
-        for (uint32_t v = 0; v < nv; ++v)
-        {
-            const uint4 cur = nxt;
-            if (v + 1 < nv)
-                nxt = reinterpret_cast<const uint4*>(src)[v + 1];
-            const uint32_t iw[4] = {cur.x, cur.y, cur.z, cur.w};
-            uint32_t       ow[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                ow[j >> 2] |= mtf_step(R, tbl, (iw[j >> 2] >> (8 * (j & 3))) & 0xFF) << (8 * (j & 3));
-            reinterpret_cast<uint4*>(dst)[v] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-        }
-        i = nv * 16;
-    }
-    for (; i < P.len; ++i)
-        dst[i] = (uint8_t) mtf_step(R, tbl, src[i]);
-}
-
-// Segments of blocks with more than MTF_REG distinct symbols (the others go to k_mtf_encode_reg).
-__global__ void __launch_bounds__(TPB) k_mtf_encode(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
-                                                    uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t tbl[];  // TSTRIDE * TPB dwords
-    const uint32_t t    = threadIdx.x;
-    const int      lane = lane_id();
-    const uint32_t wave = t >> 6;
-    for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
-    {
-        // tables for the 64 segments of this wave
-        for (int q = 0; q < 64; ++q)
-        {
-            const uint32_t owner = wave * 64 + q;
-            const uint32_t s     = g0 + owner;
-            if (s >= nseg)
-                break;
-            const Piece P = segs[s];
-            if (nsym[P.block] <= MTF_REG)
-                continue;
-            if (P.start == 0)
-                tbl[owner * TSTRIDE + lane] = (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u;
-            else
-                build_table_wave(state + (size_t) s * 256, tbl, owner);
-        }
-        __syncthreads();
-        const uint32_t s = g0 + t;
-        if (s < nseg && nsym[segs[s].block] > MTF_REG)
-            mtf_encode_segment(in, out, segs[s], tbl + t * TSTRIDE);
-        __syncthreads();
-    }
 }
 
 // ---- register tables: blocks of at most MTF_REG distinct symbols ----
@@ -1110,28 +940,13 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
         hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
                            nblocks, st, w.nsym);
     }
-    const size_t lds = (size_t) TSTRIDE * TPB * 4;
-    static bool  attr = false;
-    if (!attr)
-    {
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mtf_encode, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-        attr = true;
-    }
     {
         BRA_PROF(P_MTF_ENCODE, s);
         // every segment goes to exactly one of the two kernels (by its block's distinct symbols)
         hipLaunchKernelGGL(k_mtf_encode_reg, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), 0, s, d_in, d_out,
                            w.tiling.d_pieces, nseg, st, w.nsym);
-        static const int wave_kernel = [] {
-            const char* e = getenv("BRA_MTF_WAVE");  // 0: per-thread table walks for blocks of > MTF_REG symbols
-            return e ? atoi(e) : 1;
-        }();
-        if (wave_kernel)
-            hipLaunchKernelGGL(k_mtf_encode_wave, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, d_out,
-                               w.tiling.d_pieces, nseg, st, w.nsym);
-        else
-            hipLaunchKernelGGL(k_mtf_encode, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), lds, s, d_in, d_out,
-                               w.tiling.d_pieces, nseg, st, w.nsym);
+        hipLaunchKernelGGL(k_mtf_encode_wave, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, d_out,
+                           w.tiling.d_pieces, nseg, st, w.nsym);
     }
     uint64_t N = 0;
     for (uint32_t b = 0; b < nblocks; ++b)

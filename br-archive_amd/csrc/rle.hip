@@ -485,11 +485,7 @@ bool rle_encode_device(RleWorkspace& w, const uint8_t* d_in, const BlockDesc* h_
     const uint32_t nt = w.tiling.n;
     if (!w.reserve(nt))
         return false;
-    static const uint32_t grid_cap = [] {  // workgroups of the tile kernels (env BRA_RLE_GRID)
-        const char* e = getenv("BRA_RLE_GRID");
-        return e ? (uint32_t) std::max(8, atoi(e)) : 32768u;  // 8192: 0.03 ms slower per stage
-    }();
-    const uint32_t grid = std::min<uint32_t>(nt, grid_cap);
+    const uint32_t grid = std::min<uint32_t>(nt, 32768u);  // workgroups of the tile kernels (8192: 0.03 ms slower per stage)
     BRA_HIP_CHECK(hipMemsetAsync(d_hist, 0, (size_t) nblocks * 256 * 4, s));
     TileRun*  runs = static_cast<TileRun*>(w.runs);
     TileLink* link = static_cast<TileLink*>(w.link);

@@ -6,8 +6,10 @@
  * signatures, memory ownership and error behaviour, so that lib_bra's chunk loop
  * (src/io/lib_bra_io_file_chunks.c:217-262, :362-393) and therefore bra / unbra / bra.sfx link
  * against libbra_hip.so unchanged.  Every call runs on the GPU; there is no
- * CPU code path.  A process-wide device context is created lazily on first use (the reference
- * tests call the encoders without bra_init(), test/test_bra_encoders.cpp); calls are serialised.
+ * CPU code path.  No bra_init() is needed (the reference tests call the encoders without it,
+ * test/test_bra_encoders.cpp): a call leases a device context from a per-device pool for the
+ * calling thread's current HIP device (created on first use), so concurrent callers run on
+ * separate contexts and the functions are re-entrant as the reference's are.
  *
  * Part 2 is the batch API the throughput path uses: many independent blocks, all buffers already
  * in HBM, one call.

@@ -382,6 +382,26 @@ def test_single_block_stages_past_2_24(bra, orc):
         assert bra.huffman_decode(h.lengths, h.orig_size, h.encoded_size, h.data) == r, kind
 
 
+def test_mtf_start_tables_straddling_2_24(bra, orc):
+    """The MTF start-table sort for positions at or past 2^24 (csrc/mtf.hip start_table_dword: two
+    passes over 24-bit digits when a last occurrence reaches 0xFFFFFE): a 17 MiB block whose
+    distinct symbols' last occurrences fall on 2^24 - 3 .. 2^24 + 2, so a segment's start table
+    mixes occurrences just below and just above the 24-bit limit; small and large alphabets."""
+    n = 17 << 20
+    base = (1 << 24) - 3
+    rng = np.random.default_rng(2424)
+    for alpha in (8, 200):
+        x = bytearray(rng.integers(0, alpha, n, dtype=np.uint8).tobytes())
+        syms = [alpha + k for k in range(6)] if alpha + 6 <= 256 else list(range(250, 256))
+        for k, c in enumerate(syms):  # symbol c occurs only at 2^24 - 3 + k and once early
+            x[base + k] = c
+            x[1000 + k] = c
+        x = bytes(x)
+        m = bra.mtf_encode(x)
+        assert m == orc.mtf_encode(x), alpha
+        assert bra.mtf_decode(m) == x, alpha
+
+
 def test_batch_max_block_size(bra, codec, orc):
     """The batched path at its largest block, 2^24 - 1 bytes (24-bit rotation indices at their
     maximum): uniform random bytes and text, every stage against the oracle, plus the round trip."""
