@@ -1943,6 +1943,27 @@ __device__ __forceinline__ uint64_t make_key(uint32_t grp, uint32_t slot, uint64
     return ((((uint64_t) grp << (64 - G::GBITS)) | (w0 >> G::GBITS)) & ~G::SMASK) | slot;
 }
 
+#ifdef BRA_JOB_TIMING
+// Diagnostic build only (make EXTRA=-DBRA_JOB_TIMING): shader cycles of the job phases, summed over
+// the jobs by the first wave of each job, [wave jobs, workgroup jobs] x {claim + descriptor, gathers
+// of round 1, sort of round 1, groups + outputs, compaction + gathers of later rounds, sorts of later
+// rounds, rounds, jobs}; printed to stderr after each STRING encode.
+__device__ unsigned long long g_jt[2][8];
+#define JT_NOW() (wj == 0 ? (unsigned long long) clock64() : 0ull)
+#define JT_ADD(i, x)                                           \
+    do                                                        \
+    {                                                         \
+        if (wj == 0 && lane_id() == 0)                        \
+            atomicAdd(&g_jt[W > 1][i], (unsigned long long) (x)); \
+    } while (0)
+#else
+#define JT_NOW() 0ull
+#define JT_ADD(i, x) \
+    do               \
+    {                \
+    } while (0)
+#endif
+
 template <uint32_t MODE, int W>
 __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj, const uint64_t* pre = nullptr)
 {
@@ -1968,6 +1989,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     if (!BRA_DCHECK(T <= 256u * W && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job mode %u W %d start %u len %u block %u off %llu blen %u",
                     MODE, W, J.start, T, J.block, (unsigned long long) BD.off, BD.len))
         T = 0;
+    [[maybe_unused]] unsigned long long jt = JT_NOW();
+    JT_ADD(7, 1);
     // Round 1.  STRING: all elements share their first d-1 bytes (one parent bucket), so the key
     // is the rotation's bits from depth d-1 -- its first byte orders the packed sub-buckets, no
     // group id and no carried key needed.  RANK: the 32-bit rank key.
@@ -2004,12 +2027,27 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     int P = 4;
     while ((uint32_t) P < T)
         P <<= 1;
+#ifdef BRA_JOB_TIMING
+    if (W == 1)  // the gathers' data arrive at the sort (workgroup jobs: at its first barrier)
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+    {
+        [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+        JT_ADD(1, t1 - jt);
+        jt = t1;
+    }
     job_sort<W>(key, P, S, wj);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
         key[r] &= ~G::SMASK;
+    }
+    {
+        [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+        JT_ADD(2, t1 - jt);
+        JT_ADD(6, 1);
+        jt = t1;
     }
     if (MODE == MODE_STRING)
         depth += single ? G::ADV1 : G::ADV1 - 1;
@@ -2062,6 +2100,11 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                     atomicExch(&a.ctr->overflow, 1u);
             }
         }
+        {
+            [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+            JT_ADD(3, t1 - jt);
+            jt = t1;
+        }
         if (finish)
             break;
         // ---- compact the tied slots; next round on the next ADV bytes ----
@@ -2098,12 +2141,27 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         P = 4;
         while ((uint32_t) P < T)
             P <<= 1;
+#ifdef BRA_JOB_TIMING
+        if (W == 1)
+            __builtin_amdgcn_s_waitcnt(0);
+#endif
+        {
+            [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+            JT_ADD(4, t1 - jt);
+            jt = t1;
+        }
         job_sort<W>(key, P, S, wj);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
             v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
             key[r] &= ~G::SMASK;
+        }
+        {
+            [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+            JT_ADD(5, t1 - jt);
+            JT_ADD(6, 1);
+            jt = t1;
         }
         depth += G::ADV;
     }
@@ -2206,11 +2264,364 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
         __syncthreads();
         return __builtin_amdgcn_readfirstlane(claim[(k++) & 1]);
     };
+    const int wj = threadIdx.x >> 6;
+    [[maybe_unused]] unsigned long long tc = JT_NOW();
     uint32_t j = dyn ? next(0) : (R.first < R.end ? R.first : ~0u);
     while (j != ~0u)
     {
-        job_run<MODE, W>(a, a.jobs[j], S, threadIdx.x >> 6);
+        {
+            [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+            JT_ADD(0, t1 - tc);
+        }
+        job_run<MODE, W>(a, a.jobs[j], S, wj);
+        tc = JT_NOW();
         j = next(j);
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// Single-wave jobs of up to 64 * E elements (E = 8 or 16 per lane): the workgroup-job size classes
+// (256, 512] and (512, 1024] sorted by ONE wave with E keys per lane, so a job needs no workgroup
+// barrier and no merge level (the multi-wave jobs spend most of their time waiting on those: a
+// merge level is a chain of dependent LDS reads behind two barriers).  The wave's network: in-lane
+// compare-exchanges for partners closer than E slots, DPP / permlane partners beyond.  Same
+// algorithm and outputs as job_run (rounds on 64-bit keys, compaction of the tied slots).
+// -------------------------------------------------------------------------------------------------
+template <int E>
+struct JobGeomE
+{
+    static constexpr int      SLOTS = 64 * E;
+    static constexpr int      LOGS  = (E == 8) ? 9 : 10;
+    static constexpr int      GBITS = LOGS;
+    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;
+    static constexpr uint32_t ADV   = (64 - GBITS - LOGS) / 8;
+    static constexpr uint32_t ADV1  = (64 - LOGS) / 8;
+};
+
+template <int E>
+struct JobLdsE
+{
+    uint32_t kh[64 * E];   // compaction scratch: new group head << 16 | position
+    uint32_t v[64 * E];    // payload of every slot of the current round
+    uint16_t pos[64 * E];  // job position of each active slot (increasing)
+};
+
+template <int E, int SIZE, int J>
+__device__ __forceinline__ void nete_stage(uint32_t (&k)[2][E], uint32_t e0)
+{
+    if constexpr (J >= E)
+    {
+        constexpr int LM = J / E;  // partner lane distance
+        if constexpr (LM == 16 || LM == 32)
+        {
+            // a permlane swap gathers each partner pair into one lane (see net_stage_swap)
+            const uint64_t asc = __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0);
+#pragma unroll
+            for (int q = 0; q < E; q += 2)
+            {
+                uint32_t a[2], b[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                {
+                    const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(k[i][q], k[i][q + 1], false, false)
+                                              : __builtin_amdgcn_permlane32_swap(k[i][q], k[i][q + 1], false, false);
+                    a[i] = t[0];
+                    b[i] = t[1];
+                }
+                cx64_pair(a[0], a[1], b[0], b[1], asc);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                {
+                    const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(a[i], b[i], false, false)
+                                              : __builtin_amdgcn_permlane32_swap(a[i], b[i], false, false);
+                    k[i][q]     = t[0];
+                    k[i][q + 1] = t[1];
+                }
+            }
+        }
+        else
+        {
+            const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+            {
+                const uint32_t o0 = xlane<LM>(k[0][r]), o1 = xlane<LM>(k[1][r]);
+                cx64(k[0][r], k[1][r], o0, o1, keep_min);
+            }
+        }
+    }
+    else
+    {
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if ((r & J) == 0)
+            {
+                const int      q   = r | J;
+                const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & SIZE) == 0);
+                cx64_pair(k[0][r], k[1][r], k[0][q], k[1][q], asc);
+            }
+    }
+    if constexpr (J > 1)
+        nete_stage<E, SIZE, J / 2>(k, e0);
+}
+
+template <int E, int SIZE>
+__device__ __forceinline__ void nete_phases(uint32_t (&k)[2][E], uint32_t e0, int P)
+{
+    if (SIZE > P)
+        return;
+    nete_stage<E, SIZE, SIZE / 2>(k, e0);
+    if constexpr (SIZE < 64 * E)
+        nete_phases<E, SIZE * 2>(k, e0, P);
+}
+
+// Ascending sort of the wave's 64 * E keys (slot = lane * E + r) over the first P slots (P a power
+// of two >= 2; the keys beyond hold padding, all ones).
+template <int E>
+__device__ __forceinline__ void job_sort_e(uint64_t (&key)[E], int P)
+{
+    const uint32_t e0 = (uint32_t) lane_id() * E;
+    uint32_t       k[2][E];
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+    {
+        k[0][r] = (uint32_t) key[r];
+        k[1][r] = (uint32_t) (key[r] >> 32);
+    }
+    nete_phases<E, 2>(k, e0, P);
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+        key[r] = ((uint64_t) k[1][r] << 32) | k[0][r];
+}
+
+template <int E>
+__device__ __forceinline__ void wave_sync_e()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int E>
+__device__ __forceinline__ void job_run_e(const JobArgs& a, const Job& J, JobLdsE<E>& S)
+{
+    using G                = JobGeomE<E>;
+    const uint32_t  lane   = (uint32_t) lane_id();
+    const uint32_t  e0     = lane * E;
+    const BlockDesc BD     = a.blocks[J.block];
+    const uint8_t*  blk    = a.in + BD.off;
+    const PackDesc  PK     = a.pk[J.block];
+    const uint8_t*  pkb    = a.packed + PK.poff;
+    const uint64_t* K      = J.buf ? a.key1 : a.key0;
+    const uint32_t  boff   = (uint32_t) BD.off;
+    uint64_t        key[E];
+    uint32_t        v[E], g[E];
+    uint32_t        T     = J.len;
+    uint32_t        depth = J.d;  // every workgroup job is one sub-bucket: its keys start at depth d
+    if (!BRA_DCHECK(T <= (uint32_t) G::SLOTS && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job_e start %u len %u block %u", J.start, T,
+                    J.block))
+        T = 0;
+    // round 1
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+    {
+        const uint32_t c = e0 + r;
+        key[r]           = ~0ull;
+        uint32_t vv      = 0;
+        if (c < T)
+        {
+            const uint32_t idx = (uint32_t) K[J.start + c] & 0xFFFFFFu;
+            const uint8_t  lb  = blk[idx ? idx - 1 : BD.len - 1];
+            key[r]             = (pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, idx, depth)) & ~G::SMASK) | c;
+            vv                 = ((uint32_t) lb << 24) | idx;
+        }
+        S.v[c]   = vv;
+        S.pos[c] = (uint16_t) c;
+    }
+    int P = 2;
+    while ((uint32_t) P < T)
+        P <<= 1;
+    wave_sync_e<E>();
+    job_sort_e<E>(key, P);
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+    {
+        v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
+        key[r] &= ~G::SMASK;
+    }
+    depth += G::ADV1;
+    for (;;)
+    {
+        // ---- groups: heads, group starts (max-scan), ties (an equal neighbour) ----
+        const uint64_t kprev = (uint64_t) __shfl_up((long long) key[E - 1], 1, WAVE);
+        const uint64_t knext = (uint64_t) __shfl_down((long long) key[0], 1, WAVE);
+        uint32_t       tiedm = 0;  // bit r: slot e0 + r is tied
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+        {
+            const uint32_t c  = e0 + r;
+            const uint64_t qp = r ? key[r - 1] : kprev;
+            const uint64_t qn = r + 1 < E ? key[r + 1] : knext;
+            const bool     hd = c == 0 || c >= T || qp != key[r];
+            const bool     tn = c + 1 < T && qn == key[r];
+            g[r]              = hd ? c : 0u;
+            if (c < T && (!hd || tn))
+                tiedm |= 1u << r;
+        }
+#pragma unroll
+        for (int r = 1; r < E; ++r)
+            g[r] = max(g[r], g[r - 1]);
+        {
+            uint32_t ex;
+            wave_scan<true>(g[E - 1], 0u, OpMax(), &ex);
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+                g[r] = max(g[r], ex);
+        }
+        const bool any    = __any(tiedm != 0);
+        bool       finish = !any;
+        bool final_ties = false, to_fallback = false;
+        if (!finish && depth >= PK.nvb)  // tied on every bit of the cyclic string: identical rotations
+            finish = final_ties = true;
+        else if (!finish && depth >= a.dcap)
+            finish = to_fallback = true;
+        // group ends, only to emit fallback groups (rare): min reverse scan of the next heads
+        uint32_t gend[E];
+        if (to_fallback)
+        {
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+            {
+                const uint32_t c = e0 + r;
+                gend[r]          = (g[r] == c || c >= T) ? c : 0xFFFFFFFFu;  // head positions
+            }
+            // gend[r] = the first head after slot r (or T)
+            uint32_t nx[E];
+            uint32_t run = 0xFFFFFFFFu;
+#pragma unroll
+            for (int r = E - 1; r >= 0; --r)
+            {
+                nx[r] = run;
+                run   = min(run, gend[r]);
+            }
+            uint32_t ex;
+            wave_scan<false>(run, 0xFFFFFFFFu, OpMin(), &ex);
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+                gend[r] = min(min(nx[r], ex), T);
+        }
+        // ---- outputs of the resolved slots (all slots when finishing) ----
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+        {
+            const uint32_t c    = e0 + r;
+            const bool     tied = (tiedm >> r) & 1u;
+            if (c >= T || (!finish && tied))
+                continue;
+            const uint32_t slot = J.start + S.pos[c];
+            const uint32_t idx  = v[r] & 0xFFFFFFu;
+            a.fsa[slot]         = idx;
+            a.L[slot]           = (uint8_t) (v[r] >> 24);
+            if (idx == 0)
+            {
+                if (final_ties)
+                    a.pi[J.block] = J.start + S.pos[g[r]] - boff;
+                else if (!(to_fallback && tied))
+                    a.pi[J.block] = slot - boff;
+            }
+            if (to_fallback && tied && g[r] == c)
+            {
+                const uint32_t gl    = gend[r] - c;
+                const uint32_t slot2 = atomicAdd(&a.ctr->n_groups, 1u);
+                if (slot2 < a.cap_groups)
+                {
+                    a.groups[slot2] = Group{slot, gl, depth, J.block | (1u << 30)};  // bit 30: members already in fsa
+                    atomicAdd(&a.ctr->g_members, gl);
+                    atomicMin(&a.ctr->hmin, depth);
+                }
+                else
+                    atomicExch(&a.ctr->overflow, 1u);
+            }
+        }
+        if (finish)
+            break;
+        // ---- compact the tied slots; next round on the next ADV bytes ----
+        uint32_t cnt = 0, cx[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+        {
+            cx[r] = cnt;
+            cnt += (tiedm >> r) & 1u;
+        }
+        uint32_t       pre;
+        const uint32_t inc = wave_scan<true>(cnt, 0u, OpAdd(), &pre);
+        const uint32_t T2  = __builtin_amdgcn_readlane(inc, 63);
+        uint16_t       pc[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            pc[r] = S.pos[e0 + r];
+        wave_sync_e<E>();
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if ((tiedm >> r) & 1u)
+            {
+                const uint32_t c = e0 + r, d = pre + cx[r];
+                S.v[d]           = v[r];
+                S.kh[d]          = ((d - (c - g[r])) << 16) | pc[r];  // new group head | position
+            }
+        wave_sync_e<E>();
+        T = T2;
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+        {
+            const uint32_t c = e0 + r;
+            key[r]           = ~0ull;
+            if (c < T)
+            {
+                const uint32_t gp = S.kh[c];
+                S.pos[c]          = (uint16_t) (gp & 0xFFFF);
+                const uint64_t w0 = pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth));
+                key[r] = ((((uint64_t) (gp >> 16) << (64 - G::GBITS)) | (w0 >> G::GBITS)) & ~G::SMASK) | c;
+            }
+        }
+        P = 2;
+        while ((uint32_t) P < T)
+            P <<= 1;
+        wave_sync_e<E>();
+        job_sort_e<E>(key, P);
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+        {
+            v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
+            key[r] &= ~G::SMASK;
+        }
+        depth += G::ADV;
+    }
+    wave_sync_e<E>();  // the LDS of this job is reused by the wave's next job
+}
+
+// One wave per job (4 independent waves per workgroup), jobs claimed from the per-XCD queues.
+template <int E>
+__global__ void __launch_bounds__(256) k_jobs_e(JobArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ uint32_t xs[9];
+    load_xseg(a, xs);
+    const int      wl = threadIdx.x >> 6;
+    JobLdsE<E>&    S  = reinterpret_cast<JobLdsE<E>*>(smem)[wl];
+    JobClaim       c{xcc_id(), 0};
+    uint32_t       end = 0, j = ~0u;
+    const auto next = [&]() -> uint32_t {
+        if (j != ~0u && j + 1 < end)
+            return j + 1;
+        uint32_t first = 0;
+        return job_claim(a, xs, c, 1, first, end) ? first : ~0u;
+    };
+    j = next();
+    while (j != ~0u)
+    {
+        job_run_e<E>(a, a.jobs[j], S);
+        j = next();
     }
 }
 
@@ -2674,6 +3085,7 @@ struct BwtWorkspace
     uint32_t  jobq_chunk = 2;         // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
+    int       jobs_e     = 0;         // single-wave jobs (k_jobs_e) for the two smallest workgroup-job classes
     uint32_t  mj_classes() const { return mj_waves >= 16 ? 4u : mj_waves >= 8 ? 3u : mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -2837,6 +3249,8 @@ void          bwt_workspace_destroy(BwtWorkspace* w)
 // Largest workgroup job from the environment (BRA_MJ_WAVES = 2, 4, 8 or 16; measurement only).
 static void ws_env(BwtWorkspace& w)
 {
+    if (const char* e = getenv("BRA_JOBS_E"))
+        w.jobs_e = atoi(e);
     if (const char* e = getenv("BRA_MJ_WAVES"))
     {
         const int v = atoi(e);
@@ -2926,7 +3340,15 @@ static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
     {
         BRA_PROF(P_BWT_MJOBS, s);
         for (uint32_t c = 0; c < w.mj_classes(); ++c)
-            launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], s);
+        {
+            if ((w.jobs_e & 1) && c == 0)
+                hipLaunchKernelGGL(k_jobs_e<8>, dim3(1536), dim3(256), 4 * sizeof(JobLdsE<8>), s, ord[1]);
+            else if ((w.jobs_e & 2) && c == 1)
+                hipLaunchKernelGGL(k_jobs_e<16>, dim3(1536), dim3(256), 4 * sizeof(JobLdsE<16>), s, ord[2]);
+            else
+                launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], s);
+            BRA_DSYNC(s);
+        }
     }
     BRA_HIP_CHECK(hipGetLastError());
     return true;
@@ -3192,6 +3614,17 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     Mail mc{};
     if (!post_wait(w, 0, s, mc))
         return false;
+#ifdef BRA_JOB_TIMING
+    {
+        unsigned long long jt[2][8];
+        BRA_HIP_CHECK(hipMemcpyFromSymbol(jt, HIP_SYMBOL(g_jt), sizeof jt));
+        for (int k = 0; k < 2; ++k)
+            fprintf(stderr, "[job timing %s] claim %llu gather1 %llu sort1 %llu groups+out %llu regather %llu sortN %llu | sorts %llu jobs %llu\n",
+                    k ? "wg" : "wave", jt[k][0], jt[k][1], jt[k][2], jt[k][3], jt[k][4], jt[k][5], jt[k][6], jt[k][7]);
+        std::memset(jt, 0, sizeof jt);
+        BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_jt), jt, sizeof jt));
+    }
+#endif
     // SURVEY 8.1(d) BWT model: 11 algorithmic bytes per element (input read, SA written and
     // re-read, L gathered and written), charged to the job kernels by the elements each kind covers
     if (g_prof && (g_prof->mask >> P_BWT_JOBS & 1 || g_prof->mask >> P_BWT_MJOBS & 1))

@@ -93,6 +93,8 @@ struct MtfWorkspace
     void*     state     = nullptr;
     size_t    cap_state = 0;
     uint32_t* nsym      = nullptr;  // distinct symbols per block (k_mtf_scan)
+    uint8_t*  amap      = nullptr;  // per block: alphabet index of every byte value (k_mtf_scan)
+    uint32_t* amode     = nullptr;  // per block: position-table dwords of the register encoder (0: byte tables)
     uint32_t  cap_nsym  = 0;
 
     bool reserve(size_t bytes)
@@ -111,7 +113,7 @@ struct MtfWorkspace
         if (nblocks <= cap_nsym)
             return true;
         cap_nsym = 0;
-        if (!dev_alloc(nsym, (uint64_t) nblocks + 64))
+        if (!dev_alloc(nsym, (uint64_t) nblocks + 64) || !dev_alloc(amap, 256ull * (nblocks + 64)) || !dev_alloc(amode, (uint64_t) nblocks + 64))
             return false;
         cap_nsym = nblocks + 64;
         return true;
@@ -121,8 +123,12 @@ struct MtfWorkspace
         tiling.release();
         (void) hipFree(state);
         (void) hipFree(nsym);
+        (void) hipFree(amap);
+        (void) hipFree(amode);
         state     = nullptr;
         nsym      = nullptr;
+        amap      = nullptr;
+        amode     = nullptr;
         cap_state = 0;
         cap_nsym  = 0;
     }

@@ -81,9 +81,14 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
 }
 
 // One workgroup per block; thread c scans symbol c over the block's segments (exclusive max).
+// Also the block's alphabet for the position-table encoder: amap[b][c] = rank of value c among the
+// values present in the block (0xFF: absent), amode[b] = 4 / 8 table dwords when the block has at
+// most 16 / 32 distinct values, all below 127 (every MTF position then stays below 127), else 0.
 __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
-                                                  uint32_t nblocks, int32_t* __restrict__ state, uint32_t* __restrict__ nsym)
+                                                  uint32_t nblocks, int32_t* __restrict__ state, uint32_t* __restrict__ nsym,
+                                                  uint8_t* __restrict__ amap, uint32_t* __restrict__ amode)
 {
+    __shared__ uint32_t tmp[8];
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint32_t s0  = first_seg[b];
@@ -112,9 +117,16 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
             state[(size_t) (s0 + k) * 256 + c] = run;
             run                                   = max(run, v);
         }
-        const int n = __syncthreads_count(run >= 0);  // distinct symbols of the block
+        const int      n    = __syncthreads_count(run >= 0);  // distinct symbols of the block
+        const bool     high = __syncthreads_or(run >= 0 && c >= 127) != 0;
+        const uint32_t rk   = block256_exclusive_sum(run >= 0 ? 1u : 0u, tmp);
+        amap[(size_t) b * 256 + c] = run >= 0 ? (uint8_t) rk : (uint8_t) 0xFF;
         if (threadIdx.x == 0)
-            nsym[b] = (uint32_t) n;
+        {
+            nsym[b]  = (uint32_t) n;
+            amode[b] = high ? 0u : (n <= 16 ? 4u : (n <= 32 ? 8u : 0u));
+        }
+        __syncthreads();
     }
 }
 
@@ -405,6 +417,110 @@ __device__ __forceinline__ uint32_t start_front_small(const int32_t* __restrict_
     return d;
 }
 
+// ---- position tables: blocks of <= 16 / 32 distinct values, all below 127 ----
+// The table is kept inverted: byte a of NP registers holds 0x80 | position of the block's a-th
+// alphabet value (input bytes are mapped to alphabet indices through an LDS copy of amap).  A
+// step reads the symbol's position r, adds one to every position below r and sets the symbol's
+// to 0 -- the move to front -- with byte-parallel arithmetic: bit 7 of byte (0x80 | p) - r is set
+// iff p >= r (the guard bit keeps the bytes from borrowing into each other; positions stay below
+// 127, so p + 1 never reaches the guard).  About 4 VALU per table dword plus a select tree, 45 / 75
+// VALU per symbol for 4 / 8 dwords against ~120 for the byte table's search and shift.  Unused
+// bytes hold 0xFF (never below any r, never selected).
+template <int NP>
+__device__ __forceinline__ uint32_t mtf_step_pos(uint32_t (&R)[NP], uint32_t a)
+{
+    const uint32_t q = a >> 2;
+    uint32_t       x;
+    if constexpr (NP == 8)
+    {
+        const uint32_t x0 = (q & 1) ? R[1] : R[0], x1 = (q & 1) ? R[3] : R[2], x2 = (q & 1) ? R[5] : R[4], x3 = (q & 1) ? R[7] : R[6];
+        const uint32_t y0 = (q & 2) ? x1 : x0, y1 = (q & 2) ? x3 : x2;
+        x = (q & 4) ? y1 : y0;
+    }
+    else
+    {
+        static_assert(NP == 4, "4 or 8 table dwords");
+        const uint32_t x0 = (q & 1) ? R[1] : R[0], x1 = (q & 1) ? R[3] : R[2];
+        x = (q & 2) ? x1 : x0;
+    }
+    const uint32_t sh = (a & 3u) << 3;
+    const uint32_t r  = (x >> sh) & 0x7Fu;
+    const uint32_t rr = r * 0x01010101u;
+    const uint32_t dl = r << sh;
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+    {
+        const uint32_t lt = ~(R[k] - rr) & 0x80808080u;  // bytes whose position is below r
+        const uint32_t nv = R[k] + (lt >> 7);
+        R[k]              = ((uint32_t) k == q) ? nv - dl : nv;
+    }
+    return r;
+}
+
+// Position bytes of a segment's start table, one wave: value c at position #(seen values with a
+// later last occurrence) if seen, else #seen + #(unseen values below c) (the identity order of the
+// unseen ones).  Writes byte amap[c] of the segment's front row (front[k][owner], bytes 4k..4k+3).
+__device__ __forceinline__ void start_pos_small(const int32_t* __restrict__ st, const uint8_t* __restrict__ map_s, uint32_t* sc_t,
+                                                uint32_t* sc_c, uint32_t (*front)[TPB], uint32_t owner)
+{
+    const int      lane  = lane_id();
+    const int4     tv    = reinterpret_cast<const int4*>(st)[lane];
+    const int32_t  tt[4] = {tv.x, tv.y, tv.z, tv.w};
+    uint32_t       nseen = 0, seen_before = 0;
+    uint64_t       bal[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        bal[r] = __builtin_amdgcn_ballot_w64(tt[r] >= 0);
+        nseen += (uint32_t) __popcll(bal[r]);
+    }
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        seen_before += (uint32_t) __popcll(bal[r] & below);
+    if (lane < 8)
+        front[lane][owner] = 0xFFFFFFFFu;
+    uint32_t own_seen = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = (uint32_t) lane * 4 + r;
+        if (tt[r] >= 0)
+        {
+            sc_t[seen_before + own_seen] = (uint32_t) tt[r];
+            sc_c[seen_before + own_seen] = c;
+            ++own_seen;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint8_t* fb = reinterpret_cast<uint8_t*>(front);  // byte a of the row: dword (a >> 2) * TPB + owner, byte a & 3
+    if ((uint32_t) lane < nseen)
+    {
+        const uint32_t my = sc_t[lane];
+        uint32_t       p  = 0;
+        for (uint32_t j = 0; j < nseen; ++j)
+            p += sc_t[j] > my ? 1u : 0u;
+        const uint32_t a = map_s[sc_c[lane]];
+        fb[((a >> 2) * TPB + owner) * 4 + (a & 3)] = (uint8_t) (0x80u | p);
+    }
+    uint32_t sb = seen_before;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = (uint32_t) lane * 4 + r;
+        const uint32_t a = map_s[c];
+        if (tt[r] < 0 && a != 0xFFu)
+            fb[((a >> 2) * TPB + owner) * 4 + (a & 3)] = (uint8_t) (0x80u | (nseen + c - sb));
+        if (tt[r] >= 0)
+            ++sb;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Symbols and ranks move through LDS in rounds of 64 bytes per segment, chunk-major (io[c][t]:
 // the 16-byte accesses of consecutive threads are conflict-free): the workgroup loads the next 64
 // bytes of all its segments with line-contiguous 16-byte loads (4 lanes per 64-byte run), every
@@ -414,8 +530,101 @@ __device__ __forceinline__ uint32_t start_front_small(const int32_t* __restrict_
 constexpr uint32_t MR_RB = 64;           // bytes per segment per round
 constexpr uint32_t MR_NC = MR_RB / 16;   // 16-byte chunks per segment per round
 
+// The coding loop of one workgroup iteration (STEP: one MTF step on the thread's table R).
+template <int NR, bool MAP, typename Step>
+__device__ __forceinline__ void mtf_code_rounds(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint32_t (&R)[NR], uint4 (*io)[TPB],
+                                                const uint64_t* s_off, const uint32_t* s_len, const uint8_t* map_s, Step step)
+{
+    const uint32_t t    = threadIdx.x;
+    const uint32_t len  = s_len[t];
+    const uint64_t off  = s_off[t];
+    const uint32_t full = len & ~15u;  // whole 16-byte chunks go through LDS, the tail byte by byte
+    uint32_t       rmax = 0;           // rounds the workgroup needs
+    for (uint32_t u = 0; u < TPB; ++u)
+        rmax = max(rmax, (s_len[u] & ~15u));
+    for (uint32_t r0 = 0; r0 < rmax; r0 += MR_RB)
+    {
+        // load: piece p = (segment p / MR_NC, chunk p % MR_NC)
+#pragma unroll
+        for (uint32_t i = 0; i < MR_NC; ++i)
+        {
+            const uint32_t p = t + i * TPB, sl = p / MR_NC, c = p % MR_NC;
+            const uint32_t at = r0 + c * 16;
+            if (at + 16 <= (s_len[sl] & ~15u))
+            {
+                const uint8_t* q = in + s_off[sl] + at;
+                if ((((uintptr_t) q) & 15) == 0)
+                    io[c][sl] = *reinterpret_cast<const uint4*>(q);
+                else
+                {
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (int k = 0; k < 16; ++k)
+                        w[k >> 2] |= (uint32_t) q[k] << (8 * (k & 3));
+                    io[c][sl] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (uint32_t c = 0; c < MR_NC && r0 + c * 16 < full; ++c)
+        {
+            uint4 cur = io[c][t];
+            if (MAP)
+            {
+                // input bytes -> alphabet indices (16 independent LDS lookups)
+                uint32_t w[4] = {cur.x, cur.y, cur.z, cur.w}, m[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    m[k >> 2] |= (uint32_t) map_s[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu] << (8 * (k & 3));
+                cur = make_uint4(m[0], m[1], m[2], m[3]);
+            }
+            // 16 symbols shifted out of a 128-bit register pair, ranks shifted in (a rolled
+            // loop: 16 inlined steps cost 2x the registers for nothing, the steps are serial)
+            uint64_t ilo = ((uint64_t) cur.y << 32) | cur.x, ihi = ((uint64_t) cur.w << 32) | cur.z;
+            uint64_t olo = 0, ohi = 0;
+#pragma unroll 1
+            for (int j = 0; j < 16; ++j)
+            {
+                const uint32_t rk = step(R, (uint32_t) ilo & 0xFFu);
+                ilo               = (ilo >> 8) | (ihi << 56);
+                ihi >>= 8;
+                olo = (olo >> 8) | (ohi << 56);
+                ohi = (ohi >> 8) | ((uint64_t) rk << 56);
+            }
+            io[c][t] = make_uint4((uint32_t) olo, (uint32_t) (olo >> 32), (uint32_t) ohi, (uint32_t) (ohi >> 32));
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < MR_NC; ++i)
+        {
+            const uint32_t p = t + i * TPB, sl = p / MR_NC, c = p % MR_NC;
+            const uint32_t at = r0 + c * 16;
+            if (at + 16 <= (s_len[sl] & ~15u))
+            {
+                uint8_t*    q = out + s_off[sl] + at;
+                const uint4 v = io[c][sl];
+                if ((((uintptr_t) q) & 15) == 0)
+                    *reinterpret_cast<uint4*>(q) = v;
+                else
+                {
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                    for (int k = 0; k < 16; ++k)
+                        q[k] = (uint8_t) (w[k >> 2] >> (8 * (k & 3)));
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = full; i < len; ++i)
+        out[off + i] = (uint8_t) step(R, MAP ? (uint32_t) map_s[in[off + i]] : (uint32_t) in[off + i]);
+}
+
+// Blocks of at most MTF_REG distinct symbols.  A workgroup iteration whose 256 segments all lie in
+// one block with a position-table alphabet (amode 4 / 8) codes them with mtf_step_pos; any other
+// iteration with the byte tables (mtf_step_reg).
 __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
-                                                        uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym)
+                                                        uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym,
+                                                        const uint8_t* __restrict__ amap, const uint32_t* __restrict__ amode)
 {
     __shared__ uint32_t front[NRD][TPB];  // start-table fronts of the workgroup's segments (thread-major: conflict-free)
     __shared__ uint32_t sc_t[TPB / 64][MTF_REG], sc_c[TPB / 64][MTF_REG];
@@ -423,11 +632,23 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restric
     __shared__ uint4    io[MR_NC][TPB];
     __shared__ uint64_t s_off[TPB];
     __shared__ uint32_t s_len[TPB];  // 0: not coded by this kernel (or past the batch)
+    __shared__ uint8_t  map_s[256];
+    __shared__ uint32_t mode_s;
     const uint32_t t    = threadIdx.x;
     const int      lane = lane_id();
     const uint32_t wave = t >> 6;
     for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
     {
+        if (t == 0)
+        {
+            const uint32_t b0 = segs[g0].block, b1 = segs[min(nseg, g0 + TPB) - 1].block;
+            mode_s            = (b0 == b1) ? (amode[b0] | (b0 << 4)) : 0u;
+        }
+        __syncthreads();
+        const uint32_t mode = mode_s & 15u;
+        if (mode)
+            map_s[t] = amap[(size_t) (mode_s >> 4) * 256 + t];
+        __syncthreads();
         for (int q = 0; q < 64; ++q)
         {
             const uint32_t owner = wave * 64 + q;
@@ -437,10 +658,15 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restric
             const Piece P = segs[s];
             if (nsym[P.block] > MTF_REG)
                 continue;
-            const uint32_t d = (P.start == 0) ? (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u
-                                              : start_front_small(state + (size_t) s * 256, sc_t[wave], sc_c[wave], sc_out[wave]);
-            if (lane < NRD)
-                front[lane][owner] = d;
+            if (mode)
+                start_pos_small(state + (size_t) s * 256, map_s, sc_t[wave], sc_c[wave], front, owner);
+            else
+            {
+                const uint32_t d = (P.start == 0) ? (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u
+                                                  : start_front_small(state + (size_t) s * 256, sc_t[wave], sc_c[wave], sc_out[wave]);
+                if (lane < NRD)
+                    front[lane][owner] = d;
+            }
         }
         {
             const uint32_t s = g0 + t;
@@ -454,82 +680,31 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restric
             s_len[t] = l;
         }
         __syncthreads();
-        const uint32_t len = s_len[t];
-        const uint64_t off = s_off[t];
-        uint32_t       R[NRD];
-#pragma unroll
-        for (int k = 0; k < NRD; ++k)
-            R[k] = len ? front[k][t] : 0u;
-        const uint32_t full = len & ~15u;  // whole 16-byte chunks go through LDS, the tail byte by byte
-        uint32_t       rmax = 0;           // rounds the workgroup needs
-        for (uint32_t u = 0; u < TPB; ++u)
-            rmax = max(rmax, (s_len[u] & ~15u));
-        for (uint32_t r0 = 0; r0 < rmax; r0 += MR_RB)
+        const bool act = s_len[t] != 0;
+        if (mode == 4)
         {
-            // load: piece p = (segment p / MR_NC, chunk p % MR_NC)
+            uint32_t R[4];
 #pragma unroll
-            for (uint32_t i = 0; i < MR_NC; ++i)
-            {
-                const uint32_t p = t + i * TPB, sl = p / MR_NC, c = p % MR_NC;
-                const uint32_t at = r0 + c * 16;
-                if (at + 16 <= (s_len[sl] & ~15u))
-                {
-                    const uint8_t* q = in + s_off[sl] + at;
-                    if ((((uintptr_t) q) & 15) == 0)
-                        io[c][sl] = *reinterpret_cast<const uint4*>(q);
-                    else
-                    {
-                        uint32_t w[4] = {0, 0, 0, 0};
-                        for (int k = 0; k < 16; ++k)
-                            w[k >> 2] |= (uint32_t) q[k] << (8 * (k & 3));
-                        io[c][sl] = make_uint4(w[0], w[1], w[2], w[3]);
-                    }
-                }
-            }
-            __syncthreads();
-#pragma unroll 1
-            for (uint32_t c = 0; c < MR_NC && r0 + c * 16 < full; ++c)
-            {
-                const uint4 cur = io[c][t];
-                // 16 symbols shifted out of a 128-bit register pair, ranks shifted in (a rolled
-                // loop: 16 inlined steps cost 2x the registers for nothing, the steps are serial)
-                uint64_t ilo = ((uint64_t) cur.y << 32) | cur.x, ihi = ((uint64_t) cur.w << 32) | cur.z;
-                uint64_t olo = 0, ohi = 0;
-#pragma unroll 1
-                for (int j = 0; j < 16; ++j)
-                {
-                    const uint32_t rk = mtf_step_reg(R, (uint32_t) ilo & 0xFFu);
-                    ilo               = (ilo >> 8) | (ihi << 56);
-                    ihi >>= 8;
-                    olo = (olo >> 8) | (ohi << 56);
-                    ohi = (ohi >> 8) | ((uint64_t) rk << 56);
-                }
-                io[c][t] = make_uint4((uint32_t) olo, (uint32_t) (olo >> 32), (uint32_t) ohi, (uint32_t) (ohi >> 32));
-            }
-            __syncthreads();
-#pragma unroll
-            for (uint32_t i = 0; i < MR_NC; ++i)
-            {
-                const uint32_t p = t + i * TPB, sl = p / MR_NC, c = p % MR_NC;
-                const uint32_t at = r0 + c * 16;
-                if (at + 16 <= (s_len[sl] & ~15u))
-                {
-                    uint8_t*    q = out + s_off[sl] + at;
-                    const uint4 v = io[c][sl];
-                    if ((((uintptr_t) q) & 15) == 0)
-                        *reinterpret_cast<uint4*>(q) = v;
-                    else
-                    {
-                        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-                        for (int k = 0; k < 16; ++k)
-                            q[k] = (uint8_t) (w[k >> 2] >> (8 * (k & 3)));
-                    }
-                }
-            }
-            __syncthreads();
+            for (int k = 0; k < 4; ++k)
+                R[k] = act ? front[k][t] : 0xFFFFFFFFu;
+            mtf_code_rounds<4, true>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[4], uint32_t a) { return mtf_step_pos<4>(T, a); });
         }
-        for (uint32_t i = full; i < len; ++i)
-            out[off + i] = (uint8_t) mtf_step_reg(R, in[off + i]);
+        else if (mode == 8)
+        {
+            uint32_t R[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                R[k] = act ? front[k][t] : 0xFFFFFFFFu;
+            mtf_code_rounds<8, true>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[8], uint32_t a) { return mtf_step_pos<8>(T, a); });
+        }
+        else
+        {
+            uint32_t R[NRD];
+#pragma unroll
+            for (int k = 0; k < NRD; ++k)
+                R[k] = act ? front[k][t] : 0u;
+            mtf_code_rounds<NRD, false>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[NRD], uint32_t c) { return mtf_step_reg(T, c); });
+        }
         __syncthreads();
     }
 }
@@ -938,13 +1113,13 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     {
         BRA_PROF(P_MTF_SCAN, s);
         hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
-                           nblocks, st, w.nsym);
+                           nblocks, st, w.nsym, w.amap, w.amode);
     }
     {
         BRA_PROF(P_MTF_ENCODE, s);
         // every segment goes to exactly one of the two kernels (by its block's distinct symbols)
         hipLaunchKernelGGL(k_mtf_encode_reg, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), 0, s, d_in, d_out,
-                           w.tiling.d_pieces, nseg, st, w.nsym);
+                           w.tiling.d_pieces, nseg, st, w.nsym, w.amap, w.amode);
         hipLaunchKernelGGL(k_mtf_encode_wave, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, d_out,
                            w.tiling.d_pieces, nseg, st, w.nsym);
     }
