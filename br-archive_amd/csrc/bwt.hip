@@ -60,7 +60,7 @@ constexpr int      TILE         = BRA_TILE;  // elements per MSD tile (256 threa
 constexpr int      TPB          = 256;
 constexpr int      PER_THREAD   = TILE / TPB;
 constexpr uint32_t JOB_MAX      = 256;  // elements one wave sorts in registers
-constexpr int      MJ_WAVES_DEF = 4;    // waves of a workgroup job (2, 4, 8 or 16; env BRA_MJ_WAVES)
+constexpr int      MJ_WAVES_DEF = 4;    // waves of a workgroup job (2, 4, 8 or 16)
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
@@ -85,7 +85,7 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
 #endif
 #ifndef JOB_MIN_WAVES
-#define JOB_MIN_WAVES 6  // 64-bit keys: 80 VGPRs without spills at 6 waves per SIMD (the 96-bit keys spilled at 6)
+#define JOB_MIN_WAVES 5  // min waves per SIMD of the wave-job kernel (6 spills)
 #endif
 
 enum : uint32_t { MODE_STRING = 0, MODE_RANK = 1 };
@@ -202,6 +202,25 @@ __device__ __forceinline__ uint32_t pk_bitpos(uint32_t b, uint32_t nbits, uint32
     if (bp >= nbits)
         bp %= nbits;
     return bp;
+}
+
+// 128 bits of a packed string from bit bp: w0 = bits [bp, bp + 64), w1 = the next 64 (one 16-byte
+// load and one byte: the same latency as 64 bits)
+__device__ __forceinline__ void pk_load128(const uint8_t* __restrict__ pk, uint32_t bp, uint64_t& w0, uint64_t& w1)
+{
+    const uint8_t* p  = pk + (bp >> 3);
+    const uint4    q  = *reinterpret_cast<const uint4_u*>(p);
+    uint64_t       a  = __builtin_bswap64(((uint64_t) q.y << 32) | q.x);
+    uint64_t       c  = __builtin_bswap64(((uint64_t) q.w << 32) | q.z);
+    const uint32_t sh = bp & 7;
+    if (sh)
+    {
+        const uint64_t e = p[16];
+        a                = (a << sh) | (c >> (64 - sh));
+        c                = (c << sh) | (e >> (8 - sh));
+    }
+    w0 = a;
+    w1 = c;
 }
 
 // 64 bits of a packed string from bit bp (bit bp in the MSB)
@@ -1535,10 +1554,10 @@ template <int W>
 struct JobLds
 {
     static constexpr int KD = JobGeom<W>::KD;
-    uint64_t kh[256 * W];                // neighbour keys, merge levels, compaction scratch
-    uint64_t kl[KD == 2 ? 1 : 256 * W];  // low key words (keys wider than 64 bits only)
+    uint64_t kh[256 * W];   // neighbour keys, merge levels, compaction scratch
+    uint64_t wx[256 * W];   // STRING: the 64 rotation bits after each element's round-1 key (the round-2 key bits)
     uint32_t v[256 * W];    // payload of every slot of the current round (the keys carry the slot)
-    uint32_t nx[256 * W];   // group-end scratch
+    uint32_t nx[W];         // group-end scratch (the first head of each wave)
     uint16_t pos[256 * W];  // job position of each active slot (increasing)
     uint32_t agg[W];
 };
@@ -1870,63 +1889,78 @@ __device__ __forceinline__ void job_sort(uint64_t (&key)[4], int P, JobLds<W>& S
     job_sync<W>();
 }
 
-// Group heads / group ends / ties over the T active slots; km = the keys without the slot bits.
+// Group heads, group starts (g: max-scan of the head positions) and ties over the T active slots
+// (a slot is tied when a neighbour holds the same key); km = the keys without the slot bits.
+// Returns whether any slot is tied (job-wide).
 template <int W>
-__device__ __forceinline__ bool job_groups(const uint64_t (&km)[4], uint32_t T, JobLds<W>& S, int wj, uint32_t (&g)[4], uint32_t (&gend)[4],
-                                           bool (&tied)[4])
+__device__ __forceinline__ bool job_groups(const uint64_t (&km)[4], uint32_t T, JobLds<W>& S, int wj, uint32_t (&g)[4], bool (&tied)[4],
+                                           bool (&hd)[4])
 {
-    constexpr uint32_t SLOTS = 256 * W;
-    const int          lane  = lane_id();
-    // previous slot's key: the lane's own element r - 1, the previous lane's element 3 (ds_bpermute),
-    // or (lane 0 of waves > 0) the previous wave's last element through LDS
+    const int lane = lane_id();
+    // neighbour keys: the lane's own elements, the previous / next lane's (ds_bpermute), or (the
+    // first / last lane of a wave of a workgroup job) the neighbouring wave's through LDS
     uint64_t pm = (uint64_t) __shfl_up((long long) km[3], 1, WAVE);
+    uint64_t nm = (uint64_t) __shfl_down((long long) km[0], 1, WAVE);
     if (W > 1)
     {
         if (lane == 63)
             S.kh[wj * 256 + 255] = km[3];
+        if (lane == 0)
+            S.kh[wj * 256] = km[0];
         job_sync<W>();
         if (lane == 0 && wj > 0)
             pm = S.kh[wj * 256 - 1];
+        if (lane == 63 && wj + 1 < W)
+            nm = S.kh[(wj + 1) * 256];
     }
-    uint32_t x[4];
+    bool any = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
         const uint32_t c  = wj * 256 + lane * 4 + r;
-        const uint64_t qm = r ? km[r - 1] : pm;
-        const bool     hd = (c == 0) || c >= T || qm != km[r];
-        g[r]              = hd ? c : 0;
-        x[r]              = hd ? c : 0xFFFFFFFFu;
+        const uint64_t qp = r ? km[r - 1] : pm;
+        const uint64_t qn = r < 3 ? km[r + 1] : nm;
+        hd[r]             = (c == 0) || c >= T || qp != km[r];
+        g[r]              = hd[r] ? c : 0;
+        tied[r]           = c < T && (!hd[r] || (c + 1 < T && qn == km[r]));
+        any |= tied[r];
     }
-    job_max_scan<W>(g, S, wj);
+    job_max_scan<W>(g, S, wj);  // (its barriers also order the S.kh reads above before later writes)
+    return job_any<W>(any);
+}
+
+// Group ends (the next head after each slot, or T): only where groups are emitted (RANK mode, or
+// STRING groups sent to the fallback).
+template <int W>
+__device__ __forceinline__ void job_group_ends(const bool (&hd)[4], uint32_t T, JobLds<W>& S, int wj, uint32_t (&gend)[4])
+{
+    constexpr uint32_t SLOTS = 256 * W;
+    const int          lane  = lane_id();
+    uint32_t           x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        x[r] = hd[r] ? wj * 256 + lane * 4 + r : 0xFFFFFFFFu;
     job_min_rscan<W>(x, S, wj);
-    // next slot's x: own element r + 1, the next lane's element 0, or the next wave's first
     uint32_t nx3 = (uint32_t) __shfl_down((int) x[0], 1, WAVE);
     if (lane == 63)
         nx3 = 0xFFFFFFFFu;
     if (W > 1)
     {
         if (lane == 0)
-            S.nx[wj * 256] = x[0];
+            S.nx[wj] = x[0];
         job_sync<W>();
         if (lane == 63 && wj + 1 < W)
-            nx3 = S.nx[(wj + 1) * 256];
+            nx3 = S.nx[wj + 1];
+        job_sync<W>();
     }
-    bool any = false;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
-        const uint32_t c   = wj * 256 + lane * 4 + r;
-        const uint32_t nh  = (c + 1 < SLOTS) ? (r < 3 ? x[r + 1] : nx3) : 0xFFFFFFFFu;
-        const uint32_t end = min(nh == 0xFFFFFFFFu ? SLOTS : nh, T);
-        gend[r]            = end;
-        tied[r]            = c < T && (end - g[r]) >= 2;
-        any |= tied[r];
+        const uint32_t c  = wj * 256 + lane * 4 + r;
+        const uint32_t nh = (c + 1 < SLOTS) ? (r < 3 ? x[r + 1] : nx3) : 0xFFFFFFFFu;
+        gend[r]           = min(nh == 0xFFFFFFFFu ? SLOTS : nh, T);
     }
-    job_sync<W>();
-    return job_any<W>(any);
 }
-
 
 // round-1 key: the rotation's packed bits from the key's first depth, low LOGS bits = slot
 template <int W>
@@ -1982,7 +2016,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     uint32_t        v[4];
     uint32_t        pos[4];  // job position of slot c
     uint32_t        g[4], gend[4];
-    bool            tied[4];
+    bool            tied[4], hd[4];
     uint32_t        T     = J.len;
     uint32_t        depth = (MODE == MODE_STRING) ? J.d : J.gdepth;
     const bool      single = MODE == MODE_STRING && (W > 1 || J.kd == 1u);
@@ -1993,7 +2027,9 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     JT_ADD(7, 1);
     // Round 1.  STRING: all elements share their first d-1 bytes (one parent bucket), so the key
     // is the rotation's bits from depth d-1 -- its first byte orders the packed sub-buckets, no
-    // group id and no carried key needed.  RANK: the 32-bit rank key.
+    // group id and no carried key needed.  The same 16-byte gather brings the next 64 bits, the
+    // key bits of round 2 (S.wx): most tied elements need no second gather.  RANK: the 32-bit
+    // rank key.
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -2001,6 +2037,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         pos[r]           = c;
         v[r]             = 0;
         key[r]           = ~0ull;  // padding: sorts last
+        uint64_t wx      = 0;
         if (c < T)
         {
             // STRING payloads are the 64-bit MSD payloads in the key buffers (index in the low bits)
@@ -2018,11 +2055,16 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
                 const uint8_t  lb  = blk[idx ? idx - 1 : BD.len - 1];
                 // a single sub-bucket (every workgroup job, flagged wave jobs) shares byte d-1: its
                 // key starts at d
-                key[r] = make_key1<W>(c, pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, idx, single ? depth : depth - 1)));
+                uint64_t w0, w1;
+                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, single ? depth : depth - 1), w0, w1);
+                key[r] = make_key1<W>(c, w0);
+                wx     = (w0 << (8 * G::ADV1)) | (w1 >> (64 - 8 * G::ADV1));
                 v[r]   = ((uint32_t) lb << 24) | idx;
             }
         }
         S.v[c] = v[r];
+        if (MODE == MODE_STRING)
+            S.wx[c] = wx;
     }
     int P = 4;
     while ((uint32_t) P < T)
@@ -2037,11 +2079,24 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         jt = t1;
     }
     job_sort<W>(key, P, S, wj);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
     {
-        v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
-        key[r] &= ~G::SMASK;
+        // payloads and round-2 key bits into sorted order
+        uint64_t t[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t sl = (uint32_t) (key[r] & G::SMASK);
+            v[r]              = S.v[sl];
+            t[r]              = MODE == MODE_STRING ? S.wx[sl] : 0ull;
+            key[r] &= ~G::SMASK;
+        }
+        if (MODE == MODE_STRING)
+        {
+            job_sync<W>();
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                S.wx[wj * 256 + lane * 4 + r] = t[r];
+        }
     }
     {
         [[maybe_unused]] const unsigned long long t1 = JT_NOW();
@@ -2051,18 +2106,56 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     }
     if (MODE == MODE_STRING)
         depth += single ? G::ADV1 : G::ADV1 - 1;
-    for (;;)
+    for (uint32_t round = 1;; ++round)
     {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             S.pos[wj * 256 + lane * 4 + r] = (uint16_t) pos[r];
-        const bool any    = job_groups<W>(key, T, S, wj, g, gend, tied);
+        const bool any    = job_groups<W>(key, T, S, wj, g, tied, hd);
         bool       finish = (MODE == MODE_RANK) || !any;
         bool final_ties = false, to_fallback = false;
         if (!finish && depth >= PK.nvb)  // tied on every bit of the cyclic string: identical rotations
             finish = final_ties = true;
         else if (!finish && depth >= a.dcap)
             finish = to_fallback = true;
+        if (MODE == MODE_RANK || to_fallback)  // job-uniform
+            job_group_ends<W>(hd, T, S, wj, gend);
+        // ---- not finished: compact the tied slots and start the next round's key loads BEFORE
+        // this round's output stores (vector-memory counts complete in issue order: a load issued
+        // after a store waits for the store too) ----
+        // (the keys are not needed past job_groups: key[] receives the next round's rotation bits)
+        uint32_t T2 = 0;
+        if (!finish)
+        {
+            uint32_t cx[4];
+            job_excl_count<W>(tied, cx, T2, S, wj);
+            if (round == 1)
+            {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    key[r] = tied[r] ? S.wx[wj * 256 + lane * 4 + r] : 0ull;
+            }
+            job_sync<W>();
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (tied[r])
+                {
+                    const uint32_t c = wj * 256 + lane * 4 + r;
+                    S.v[cx[r]]       = v[r];
+                    S.kh[cx[r]]      = ((uint64_t) (cx[r] - (c - g[r])) << 16) | pos[r];  // new group head | position
+                    if (round == 1)
+                        S.wx[cx[r]] = key[r];
+                }
+            job_sync<W>();
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const uint32_t c = wj * 256 + lane * 4 + r;
+                key[r]           = 0;
+                if (c < T2)
+                    key[r] = round == 1 ? S.wx[c] : pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth));
+            }
+        }
         // ---- outputs of the resolved slots (all slots when finishing) ----
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -2074,13 +2167,12 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
             const uint32_t idx  = v[r] & 0xFFFFFFu;
             a.fsa[slot]         = idx;
             a.L[slot]           = (uint8_t) (v[r] >> 24);
-            const uint32_t gst  = J.start + S.pos[g[r]] - boff;  // block-local start of the group
             if (MODE == MODE_RANK)
-                a.isa[BD.off + idx] = gst;
+                a.isa[BD.off + idx] = J.start + S.pos[g[r]] - boff;  // block-local start of the group
             if (idx == 0)
             {
                 if (MODE == MODE_RANK || final_ties)
-                    a.pi[J.block] = gst;
+                    a.pi[J.block] = J.start + S.pos[g[r]] - boff;
                 else if (!(to_fallback && tied[r]))
                     a.pi[J.block] = slot - boff;
             }
@@ -2107,35 +2199,21 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         }
         if (finish)
             break;
-        // ---- compact the tied slots; next round on the next ADV bytes ----
-        uint32_t cx[4], T2;
-        job_excl_count<W>(tied, cx, T2, S, wj);
-        job_sync<W>();
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (tied[r])
-            {
-                const uint32_t c = wj * 256 + lane * 4 + r;
-                S.v[cx[r]]       = v[r];
-                S.kh[cx[r]]      = ((uint64_t) (cx[r] - (c - g[r])) << 16) | pos[r];  // new group head | position
-            }
-        job_sync<W>();
+        // ---- next round on the next ADV bytes ----
         T = T2;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
             const uint32_t c = wj * 256 + lane * 4 + r;
+            pos[r]           = c;
             if (c < T)
             {
                 const uint64_t gp = S.kh[c];
                 pos[r]            = (uint32_t) (gp & 0xFFFF);
-                key[r]            = make_key<W>((uint32_t) (gp >> 16), c, pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth)));
+                key[r]            = make_key<W>((uint32_t) (gp >> 16), c, key[r]);
             }
             else
-            {
-                pos[r] = c;
                 key[r] = ~0ull;
-            }
         }
         job_sync<W>();
         P = 4;
@@ -2276,352 +2354,6 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
         job_run<MODE, W>(a, a.jobs[j], S, wj);
         tc = JT_NOW();
         j = next(j);
-    }
-}
-
-// -------------------------------------------------------------------------------------------------
-// Single-wave jobs of up to 64 * E elements (E = 8 or 16 per lane): the workgroup-job size classes
-// (256, 512] and (512, 1024] sorted by ONE wave with E keys per lane, so a job needs no workgroup
-// barrier and no merge level (the multi-wave jobs spend most of their time waiting on those: a
-// merge level is a chain of dependent LDS reads behind two barriers).  The wave's network: in-lane
-// compare-exchanges for partners closer than E slots, DPP / permlane partners beyond.  Same
-// algorithm and outputs as job_run (rounds on 64-bit keys, compaction of the tied slots).
-// -------------------------------------------------------------------------------------------------
-template <int E>
-struct JobGeomE
-{
-    static constexpr int      SLOTS = 64 * E;
-    static constexpr int      LOGS  = (E == 8) ? 9 : 10;
-    static constexpr int      GBITS = LOGS;
-    static constexpr uint64_t SMASK = (1ull << LOGS) - 1;
-    static constexpr uint32_t ADV   = (64 - GBITS - LOGS) / 8;
-    static constexpr uint32_t ADV1  = (64 - LOGS) / 8;
-};
-
-template <int E>
-struct JobLdsE
-{
-    uint32_t kh[64 * E];   // compaction scratch: new group head << 16 | position
-    uint32_t v[64 * E];    // payload of every slot of the current round
-    uint16_t pos[64 * E];  // job position of each active slot (increasing)
-};
-
-template <int E, int SIZE, int J>
-__device__ __forceinline__ void nete_stage(uint32_t (&k)[2][E], uint32_t e0)
-{
-    if constexpr (J >= E)
-    {
-        constexpr int LM = J / E;  // partner lane distance
-        if constexpr (LM == 16 || LM == 32)
-        {
-            // a permlane swap gathers each partner pair into one lane (see net_stage_swap)
-            const uint64_t asc = __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0);
-#pragma unroll
-            for (int q = 0; q < E; q += 2)
-            {
-                uint32_t a[2], b[2];
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-                {
-                    const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(k[i][q], k[i][q + 1], false, false)
-                                              : __builtin_amdgcn_permlane32_swap(k[i][q], k[i][q + 1], false, false);
-                    a[i] = t[0];
-                    b[i] = t[1];
-                }
-                cx64_pair(a[0], a[1], b[0], b[1], asc);
-#pragma unroll
-                for (int i = 0; i < 2; ++i)
-                {
-                    const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(a[i], b[i], false, false)
-                                              : __builtin_amdgcn_permlane32_swap(a[i], b[i], false, false);
-                    k[i][q]     = t[0];
-                    k[i][q + 1] = t[1];
-                }
-            }
-        }
-        else
-        {
-            const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
-#pragma unroll
-            for (int r = 0; r < E; ++r)
-            {
-                const uint32_t o0 = xlane<LM>(k[0][r]), o1 = xlane<LM>(k[1][r]);
-                cx64(k[0][r], k[1][r], o0, o1, keep_min);
-            }
-        }
-    }
-    else
-    {
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-            if ((r & J) == 0)
-            {
-                const int      q   = r | J;
-                const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & SIZE) == 0);
-                cx64_pair(k[0][r], k[1][r], k[0][q], k[1][q], asc);
-            }
-    }
-    if constexpr (J > 1)
-        nete_stage<E, SIZE, J / 2>(k, e0);
-}
-
-template <int E, int SIZE>
-__device__ __forceinline__ void nete_phases(uint32_t (&k)[2][E], uint32_t e0, int P)
-{
-    if (SIZE > P)
-        return;
-    nete_stage<E, SIZE, SIZE / 2>(k, e0);
-    if constexpr (SIZE < 64 * E)
-        nete_phases<E, SIZE * 2>(k, e0, P);
-}
-
-// Ascending sort of the wave's 64 * E keys (slot = lane * E + r) over the first P slots (P a power
-// of two >= 2; the keys beyond hold padding, all ones).
-template <int E>
-__device__ __forceinline__ void job_sort_e(uint64_t (&key)[E], int P)
-{
-    const uint32_t e0 = (uint32_t) lane_id() * E;
-    uint32_t       k[2][E];
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-    {
-        k[0][r] = (uint32_t) key[r];
-        k[1][r] = (uint32_t) (key[r] >> 32);
-    }
-    nete_phases<E, 2>(k, e0, P);
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-        key[r] = ((uint64_t) k[1][r] << 32) | k[0][r];
-}
-
-template <int E>
-__device__ __forceinline__ void wave_sync_e()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int E>
-__device__ __forceinline__ void job_run_e(const JobArgs& a, const Job& J, JobLdsE<E>& S)
-{
-    using G                = JobGeomE<E>;
-    const uint32_t  lane   = (uint32_t) lane_id();
-    const uint32_t  e0     = lane * E;
-    const BlockDesc BD     = a.blocks[J.block];
-    const uint8_t*  blk    = a.in + BD.off;
-    const PackDesc  PK     = a.pk[J.block];
-    const uint8_t*  pkb    = a.packed + PK.poff;
-    const uint64_t* K      = J.buf ? a.key1 : a.key0;
-    const uint32_t  boff   = (uint32_t) BD.off;
-    uint64_t        key[E];
-    uint32_t        v[E], g[E];
-    uint32_t        T     = J.len;
-    uint32_t        depth = J.d;  // every workgroup job is one sub-bucket: its keys start at depth d
-    if (!BRA_DCHECK(T <= (uint32_t) G::SLOTS && J.start >= BD.off && J.start + T <= BD.off + BD.len, "job_e start %u len %u block %u", J.start, T,
-                    J.block))
-        T = 0;
-    // round 1
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-    {
-        const uint32_t c = e0 + r;
-        key[r]           = ~0ull;
-        uint32_t vv      = 0;
-        if (c < T)
-        {
-            const uint32_t idx = (uint32_t) K[J.start + c] & 0xFFFFFFu;
-            const uint8_t  lb  = blk[idx ? idx - 1 : BD.len - 1];
-            key[r]             = (pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, idx, depth)) & ~G::SMASK) | c;
-            vv                 = ((uint32_t) lb << 24) | idx;
-        }
-        S.v[c]   = vv;
-        S.pos[c] = (uint16_t) c;
-    }
-    int P = 2;
-    while ((uint32_t) P < T)
-        P <<= 1;
-    wave_sync_e<E>();
-    job_sort_e<E>(key, P);
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-    {
-        v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
-        key[r] &= ~G::SMASK;
-    }
-    depth += G::ADV1;
-    for (;;)
-    {
-        // ---- groups: heads, group starts (max-scan), ties (an equal neighbour) ----
-        const uint64_t kprev = (uint64_t) __shfl_up((long long) key[E - 1], 1, WAVE);
-        const uint64_t knext = (uint64_t) __shfl_down((long long) key[0], 1, WAVE);
-        uint32_t       tiedm = 0;  // bit r: slot e0 + r is tied
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-        {
-            const uint32_t c  = e0 + r;
-            const uint64_t qp = r ? key[r - 1] : kprev;
-            const uint64_t qn = r + 1 < E ? key[r + 1] : knext;
-            const bool     hd = c == 0 || c >= T || qp != key[r];
-            const bool     tn = c + 1 < T && qn == key[r];
-            g[r]              = hd ? c : 0u;
-            if (c < T && (!hd || tn))
-                tiedm |= 1u << r;
-        }
-#pragma unroll
-        for (int r = 1; r < E; ++r)
-            g[r] = max(g[r], g[r - 1]);
-        {
-            uint32_t ex;
-            wave_scan<true>(g[E - 1], 0u, OpMax(), &ex);
-#pragma unroll
-            for (int r = 0; r < E; ++r)
-                g[r] = max(g[r], ex);
-        }
-        const bool any    = __any(tiedm != 0);
-        bool       finish = !any;
-        bool final_ties = false, to_fallback = false;
-        if (!finish && depth >= PK.nvb)  // tied on every bit of the cyclic string: identical rotations
-            finish = final_ties = true;
-        else if (!finish && depth >= a.dcap)
-            finish = to_fallback = true;
-        // group ends, only to emit fallback groups (rare): min reverse scan of the next heads
-        uint32_t gend[E];
-        if (to_fallback)
-        {
-#pragma unroll
-            for (int r = 0; r < E; ++r)
-            {
-                const uint32_t c = e0 + r;
-                gend[r]          = (g[r] == c || c >= T) ? c : 0xFFFFFFFFu;  // head positions
-            }
-            // gend[r] = the first head after slot r (or T)
-            uint32_t nx[E];
-            uint32_t run = 0xFFFFFFFFu;
-#pragma unroll
-            for (int r = E - 1; r >= 0; --r)
-            {
-                nx[r] = run;
-                run   = min(run, gend[r]);
-            }
-            uint32_t ex;
-            wave_scan<false>(run, 0xFFFFFFFFu, OpMin(), &ex);
-#pragma unroll
-            for (int r = 0; r < E; ++r)
-                gend[r] = min(min(nx[r], ex), T);
-        }
-        // ---- outputs of the resolved slots (all slots when finishing) ----
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-        {
-            const uint32_t c    = e0 + r;
-            const bool     tied = (tiedm >> r) & 1u;
-            if (c >= T || (!finish && tied))
-                continue;
-            const uint32_t slot = J.start + S.pos[c];
-            const uint32_t idx  = v[r] & 0xFFFFFFu;
-            a.fsa[slot]         = idx;
-            a.L[slot]           = (uint8_t) (v[r] >> 24);
-            if (idx == 0)
-            {
-                if (final_ties)
-                    a.pi[J.block] = J.start + S.pos[g[r]] - boff;
-                else if (!(to_fallback && tied))
-                    a.pi[J.block] = slot - boff;
-            }
-            if (to_fallback && tied && g[r] == c)
-            {
-                const uint32_t gl    = gend[r] - c;
-                const uint32_t slot2 = atomicAdd(&a.ctr->n_groups, 1u);
-                if (slot2 < a.cap_groups)
-                {
-                    a.groups[slot2] = Group{slot, gl, depth, J.block | (1u << 30)};  // bit 30: members already in fsa
-                    atomicAdd(&a.ctr->g_members, gl);
-                    atomicMin(&a.ctr->hmin, depth);
-                }
-                else
-                    atomicExch(&a.ctr->overflow, 1u);
-            }
-        }
-        if (finish)
-            break;
-        // ---- compact the tied slots; next round on the next ADV bytes ----
-        uint32_t cnt = 0, cx[E];
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-        {
-            cx[r] = cnt;
-            cnt += (tiedm >> r) & 1u;
-        }
-        uint32_t       pre;
-        const uint32_t inc = wave_scan<true>(cnt, 0u, OpAdd(), &pre);
-        const uint32_t T2  = __builtin_amdgcn_readlane(inc, 63);
-        uint16_t       pc[E];
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-            pc[r] = S.pos[e0 + r];
-        wave_sync_e<E>();
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-            if ((tiedm >> r) & 1u)
-            {
-                const uint32_t c = e0 + r, d = pre + cx[r];
-                S.v[d]           = v[r];
-                S.kh[d]          = ((d - (c - g[r])) << 16) | pc[r];  // new group head | position
-            }
-        wave_sync_e<E>();
-        T = T2;
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-        {
-            const uint32_t c = e0 + r;
-            key[r]           = ~0ull;
-            if (c < T)
-            {
-                const uint32_t gp = S.kh[c];
-                S.pos[c]          = (uint16_t) (gp & 0xFFFF);
-                const uint64_t w0 = pk_load64(pkb, pk_bitpos(PK.b, PK.nbits, S.v[c] & 0xFFFFFFu, depth));
-                key[r] = ((((uint64_t) (gp >> 16) << (64 - G::GBITS)) | (w0 >> G::GBITS)) & ~G::SMASK) | c;
-            }
-        }
-        P = 2;
-        while ((uint32_t) P < T)
-            P <<= 1;
-        wave_sync_e<E>();
-        job_sort_e<E>(key, P);
-#pragma unroll
-        for (int r = 0; r < E; ++r)
-        {
-            v[r] = S.v[(uint32_t) (key[r] & G::SMASK)];
-            key[r] &= ~G::SMASK;
-        }
-        depth += G::ADV;
-    }
-    wave_sync_e<E>();  // the LDS of this job is reused by the wave's next job
-}
-
-// One wave per job (4 independent waves per workgroup), jobs claimed from the per-XCD queues.
-template <int E>
-__global__ void __launch_bounds__(256) k_jobs_e(JobArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    __shared__ uint32_t xs[9];
-    load_xseg(a, xs);
-    const int      wl = threadIdx.x >> 6;
-    JobLdsE<E>&    S  = reinterpret_cast<JobLdsE<E>*>(smem)[wl];
-    JobClaim       c{xcc_id(), 0};
-    uint32_t       end = 0, j = ~0u;
-    const auto next = [&]() -> uint32_t {
-        if (j != ~0u && j + 1 < end)
-            return j + 1;
-        uint32_t first = 0;
-        return job_claim(a, xs, c, 1, first, end) ? first : ~0u;
-    };
-    j = next();
-    while (j != ~0u)
-    {
-        job_run_e<E>(a, a.jobs[j], S);
-        j = next();
     }
 }
 
@@ -3085,7 +2817,6 @@ struct BwtWorkspace
     uint32_t  jobq_chunk = 2;         // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
-    int       jobs_e     = 0;         // single-wave jobs (k_jobs_e) for the two smallest workgroup-job classes
     uint32_t  mj_classes() const { return mj_waves >= 16 ? 4u : mj_waves >= 8 ? 3u : mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -3246,24 +2977,11 @@ void          bwt_workspace_destroy(BwtWorkspace* w)
     }
 }
 
-// Largest workgroup job from the environment (BRA_MJ_WAVES = 2, 4, 8 or 16; measurement only).
-static void ws_env(BwtWorkspace& w)
-{
-    if (const char* e = getenv("BRA_JOBS_E"))
-        w.jobs_e = atoi(e);
-    if (const char* e = getenv("BRA_MJ_WAVES"))
-    {
-        const int v = atoi(e);
-        w.mj_waves  = (v == 2 || v == 4 || v == 8 || v == 16) ? v : MJ_WAVES_DEF;
-    }
-}
-
 static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
 {
     if (n <= w.cap_n && nblocks <= w.cap_blocks)
         return true;
     ws_free(w);
-    ws_env(w);
     const uint64_t N = std::max<uint64_t>(n, 1 << 16);
     const uint32_t B = std::max<uint32_t>(nblocks, 64);
     w.cap_l0     = (uint32_t) (N / TILE + B + 1);
@@ -3301,8 +3019,7 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
         (void) hipGetLastError();
         bra_hip_report("bwt: workspace allocation for %llu elements failed", (unsigned long long) N);
         ws_free(w);  // capacities back to zero: the next call retries the allocation
-        ws_env(w);
-        return false;
+            return false;
     }
     std::memset(w.h_mail, 0, MAX_LEVELS * sizeof(Mail));
     w.cap_n      = N;
@@ -3341,12 +3058,7 @@ static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
         BRA_PROF(P_BWT_MJOBS, s);
         for (uint32_t c = 0; c < w.mj_classes(); ++c)
         {
-            if ((w.jobs_e & 1) && c == 0)
-                hipLaunchKernelGGL(k_jobs_e<8>, dim3(1536), dim3(256), 4 * sizeof(JobLdsE<8>), s, ord[1]);
-            else if ((w.jobs_e & 2) && c == 1)
-                hipLaunchKernelGGL(k_jobs_e<16>, dim3(1536), dim3(256), 4 * sizeof(JobLdsE<16>), s, ord[2]);
-            else
-                launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], s);
+            launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], s);
             BRA_DSYNC(s);
         }
     }
