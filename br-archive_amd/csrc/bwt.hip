@@ -75,11 +75,8 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
-// min waves per SIMD the job kernels are compiled for (wave jobs: 6, i.e. <= 80 VGPRs, 8 bytes of
-// spill, faster than the compiler's 84 VGPRs at 5; workgroup jobs: compiler choice, 5 -- forcing 6
-// spilled and measured no faster)
-#ifndef BRA_JOB_PREFETCH
-#define BRA_JOB_PREFETCH 1  // wave jobs: next job's descriptor and payloads loaded ahead
+#ifndef BRA_JQ_CHUNK
+#define BRA_JQ_CHUNK 2  // wave jobs a wave claims with one atomic
 #endif
 #ifndef MJOB_MIN_WAVES
 #define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
@@ -1690,6 +1687,13 @@ __device__ __forceinline__ void cxk_pair(uint32_t (&a)[KD], uint32_t (&b)[KD], u
 template <int LM, int KD>
 __device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[KD][4], uint64_t keep_min)
 {
+    if constexpr (KD == 2 && LM != 4)
+    {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            cx64_dpp<LM>(k[0][r], k[1][r], keep_min);
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -1737,17 +1741,52 @@ __device__ __forceinline__ void net_stage_swap(uint32_t (&k)[KD][4], uint64_t as
 // stage parameters are compile-time, so a phase is straight-line code with the keys in fixed
 // registers (a runtime stage loop made the compiler copy every key between register sets at each
 // stage join).
+// Lane masks of the network as compile-time constants (a ballot of a lane predicate reached the
+// inline-asm compare-exchanges only after a copy through a VGPR: 2 VALU per stage).  Slot e of lane
+// l is 4 l + r (+ a wave-uniform multiple of 256, eb): bit l of lanes_where<X, Y>() is set iff
+// ((4 l) & X) == 0 equals ((4 l) & Y) == 0 (Y = 0: iff ((4 l) & X) == 0).
+template <uint32_t X, uint32_t Y>
+constexpr uint64_t lanes_where()
+{
+    uint64_t m = 0;
+    for (uint32_t l = 0; l < 64; ++l)
+    {
+        const bool a = ((4 * l) & X) == 0, b = Y ? ((4 * l) & Y) == 0 : true;
+        if (a == b)
+            m |= 1ull << l;
+    }
+    return m;
+}
+
+// Lanes that keep the minimum at stage (SIZE, J >= 4) / sort ascending in phase SIZE.
+template <int SIZE, int J>
+__device__ __forceinline__ uint64_t net_keep_min(uint32_t eb)
+{
+    if constexpr (SIZE < 256)
+        return lanes_where<SIZE, J>();
+    else
+        return (eb & SIZE) == 0 ? lanes_where<J, 0>() : ~lanes_where<J, 0>();
+}
+template <int SIZE>
+__device__ __forceinline__ uint64_t net_asc(uint32_t eb)
+{
+    if constexpr (SIZE < 4)
+        return ~0ull;  // in-lane phase 2: direction from r (see net_stage)
+    else if constexpr (SIZE < 256)
+        return lanes_where<SIZE, 0>();
+    else
+        return (eb & SIZE) == 0 ? ~0ull : 0ull;
+}
+
 template <int W, int KD, int SIZE, int J>
 __device__ __forceinline__ void net_stage(uint32_t (&k)[KD][4], JobLds<W>& S, uint32_t e0)
 {
     static_assert(J < 256, "cross-wave merges are merge_level's");
+    const uint32_t eb = __builtin_amdgcn_readfirstlane(e0) & ~255u;  // the wave's slot base (lane 0: 4 * 0)
     if constexpr (J == 64 || J == 128)
-        net_stage_swap<J / 4, KD>(k, __builtin_amdgcn_ballot_w64((e0 & SIZE) == 0));
+        net_stage_swap<J / 4, KD>(k, net_asc<SIZE>(eb));
     else if constexpr (J >= 4)
-    {
-        const uint64_t keep_min = __builtin_amdgcn_ballot_w64(((e0 & SIZE) == 0) == ((e0 & J) == 0));
-        net_stage_lanes<J / 4, KD>(k, keep_min);
-    }
+        net_stage_lanes<J / 4, KD>(k, net_keep_min<SIZE, J>(eb));
     else
     {
         // partners in the same lane: r and r ^ J; ascending where (slot & SIZE) == 0
@@ -1757,7 +1796,7 @@ __device__ __forceinline__ void net_stage(uint32_t (&k)[KD][4], JobLds<W>& S, ui
             const int q = r ^ J;
             if (q > r)
             {
-                const uint64_t asc = __builtin_amdgcn_ballot_w64(((e0 + r) & SIZE) == 0);
+                const uint64_t asc = SIZE == 2 ? ((r & 2) == 0 ? ~0ull : 0ull) : net_asc<SIZE>(eb);
                 uint32_t a[KD], b[KD];
 #pragma unroll
                 for (int i = 0; i < KD; ++i)
@@ -1982,13 +2021,32 @@ __device__ __forceinline__ uint64_t make_key(uint32_t grp, uint32_t slot, uint64
 // the jobs by the first wave of each job, [wave jobs, workgroup jobs] x {claim + descriptor, gathers
 // of round 1, sort of round 1, groups + outputs, compaction + gathers of later rounds, sorts of later
 // rounds, rounds, jobs}; printed to stderr after each STRING encode.
-__device__ unsigned long long g_jt[2][8];
+// Accumulated per wave in LDS and added to the device totals once, when the wave leaves the kernel
+// (per-phase device atomics queued behind each other and slowed the job kernels 20x).
+__device__ unsigned long long g_jt[2][10];
+__device__ __forceinline__ unsigned long long* jt_slots()
+{
+    __shared__ unsigned long long jt_s[16][10];
+    return jt_s[threadIdx.x >> 6];
+}
 #define JT_NOW() (wj == 0 ? (unsigned long long) clock64() : 0ull)
-#define JT_ADD(i, x)                                           \
-    do                                                        \
-    {                                                         \
-        if (wj == 0 && lane_id() == 0)                        \
-            atomicAdd(&g_jt[W > 1][i], (unsigned long long) (x)); \
+#define JT_ADD(i, x)                               \
+    do                                             \
+    {                                              \
+        if (wj == 0 && lane_id() == 0)             \
+            jt_slots()[i] += (unsigned long long) (x); \
+    } while (0)
+#define JT_INIT()                                  \
+    do                                             \
+    {                                              \
+        if (lane_id() < 10)                        \
+            jt_slots()[lane_id()] = 0;             \
+    } while (0)
+#define JT_FLUSH(w2)                               \
+    do                                             \
+    {                                              \
+        if (lane_id() < 10)                        \
+            atomicAdd(&g_jt[w2][lane_id()], jt_slots()[lane_id()]); \
     } while (0)
 #else
 #define JT_NOW() 0ull
@@ -1996,18 +2054,65 @@ __device__ unsigned long long g_jt[2][8];
     do               \
     {                \
     } while (0)
+#define JT_INIT() \
+    do            \
+    {             \
+    } while (0)
+#define JT_FLUSH(w2) \
+    do               \
+    {                \
+    } while (0)
 #endif
 
+// Round-1 data of a STRING job's slots: v = BWT output byte << 24 | rotation, w0 / w1 = the 128
+// packed bits from the job's first key byte.  (Gathering them one job ahead, with the payloads two
+// jobs ahead, removed the wait before the first sort but needed 128 VGPRs, 4 waves per SIMD, and
+// moved the wait to the next job's start -- behind the previous job's output stores, since the
+// vector memory counter retires in issue order: no faster.)
+struct JobPre
+{
+    uint32_t v[4];
+    uint64_t w0[4], w1[4];
+};
+
+__device__ __forceinline__ PackDesc job_pack(const JobArgs& a, uint32_t MODE, uint32_t block)
+{
+    return MODE == MODE_STRING ? a.pk[block] : PackDesc{0, 8, 8, 1};
+}
+
+// Issue the round-1 gathers of a STRING job from its payload words (rotation in the low 24 bits).
+template <int W>
+__device__ __forceinline__ void job_gather1(const JobArgs& a, const Job& J, const BlockDesc& BD, const PackDesc& PK, const uint32_t (&pay)[4],
+                                            int wj, JobPre& p)
+{
+    const uint8_t* blk    = a.in + BD.off;
+    const uint8_t* pkb    = a.packed + PK.poff;
+    const bool     single = W > 1 || J.kd == 1u;  // one shared sub-bucket: the key starts at byte d
+    const uint32_t vd     = single ? J.d : J.d - 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t c = wj * 256 + lane_id() * 4 + r;
+        p.v[r]           = 0;
+        p.w0[r] = p.w1[r] = 0;
+        if (c < J.len)
+        {
+            uint32_t idx = pay[r] & 0xFFFFFFu;
+            if (!BRA_DCHECK(idx < BD.len, "job payload idx %u >= n %u (buf %u slot %u)", idx, BD.len, J.buf, J.start + c))
+                idx = 0;
+            const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
+            pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, vd), p.w0[r], p.w1[r]);
+            p.v[r] = ((uint32_t) lb << 24) | idx;
+        }
+    }
+}
+
 template <uint32_t MODE, int W>
-__device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W>& S, int wj, const uint64_t* pre = nullptr)
+__device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const BlockDesc& BD, const PackDesc& PK, JobLds<W>& S, int wj)
 {
     using G                 = JobGeom<W>;
     const int       lane    = lane_id();
-    const BlockDesc BD      = a.blocks[J.block];
     const uint8_t*  blk     = a.in + BD.off;  // raw bytes: the BWT output byte of a rotation
-    PackDesc        PK{0, 8, 8, 1};
-    if (MODE == MODE_STRING)
-        PK = a.pk[J.block];
     const uint8_t*  pkb     = a.packed + PK.poff;
     const uint64_t* K       = J.buf ? a.key1 : a.key0;
     const uint32_t* V       = J.buf ? a.pay1 : a.pay0;
@@ -2028,8 +2133,21 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
     // Round 1.  STRING: all elements share their first d-1 bytes (one parent bucket), so the key
     // is the rotation's bits from depth d-1 -- its first byte orders the packed sub-buckets, no
     // group id and no carried key needed.  The same 16-byte gather brings the next 64 bits, the
-    // key bits of round 2 (S.wx): most tied elements need no second gather.  RANK: the 32-bit
-    // rank key.
+    // key bits of round 2 (S.wx): most tied elements need no second gather.  STRING payloads are
+    // the 64-bit MSD payloads in the key buffers (rotation in the low bits; the top byte, an MSD
+    // digit, is replaced by the rotation's BWT output byte).  RANK: the 32-bit rank key.
+    JobPre gl;
+    if (MODE == MODE_STRING)
+    {
+        uint32_t pay[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            pay[r]           = c < T ? (uint32_t) K[J.start + c] : 0u;
+        }
+        job_gather1<W>(a, J, BD, PK, pay, wj, gl);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -2040,26 +2158,18 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, JobLds<W
         uint64_t wx      = 0;
         if (c < T)
         {
-            // STRING payloads are the 64-bit MSD payloads in the key buffers (index in the low bits)
-            v[r] = (MODE == MODE_RANK) ? V[J.start + c] : (uint32_t) (pre ? pre[r] : K[J.start + c]) & 0xFFFFFFu;
-            if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (mode %u buf %u slot %u)", v[r] & 0xFFFFFFu, BD.len, MODE, J.buf,
-                            J.start + c))
-                v[r] = 0;
             if (MODE == MODE_RANK)
+            {
+                v[r] = V[J.start + c];  // BWT output byte << 24 | rotation
+                if (!BRA_DCHECK((v[r] & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (rank slot %u)", v[r] & 0xFFFFFFu, BD.len, J.start + c))
+                    v[r] = 0;
                 key[r] = K[J.start + c] | c;  // rank key in the top 32 bits
+            }
             else
             {
-                // STRING payloads carry an MSD digit in the top byte: replace it by the rotation's
-                // previous byte (its BWT output byte), gathered together with the key
-                const uint32_t idx = v[r] & 0xFFFFFFu;
-                const uint8_t  lb  = blk[idx ? idx - 1 : BD.len - 1];
-                // a single sub-bucket (every workgroup job, flagged wave jobs) shares byte d-1: its
-                // key starts at d
-                uint64_t w0, w1;
-                pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, single ? depth : depth - 1), w0, w1);
-                key[r] = make_key1<W>(c, w0);
-                wx     = (w0 << (8 * G::ADV1)) | (w1 >> (64 - 8 * G::ADV1));
-                v[r]   = ((uint32_t) lb << 24) | idx;
+                key[r] = make_key1<W>(c, gl.w0[r]);
+                wx     = (gl.w0[r] << (8 * G::ADV1)) | (gl.w1[r] >> (64 - 8 * G::ADV1));
+                v[r]   = gl.v[r];
             }
         }
         S.v[c] = v[r];
@@ -2267,48 +2377,23 @@ __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
         return job_claim(a, xs, c, a.jq_chunk, first, end) ? first : ~0u;
     };
     uint32_t j = dyn ? next(~0u) : (R.first < R.end ? R.first : ~0u);
-#if BRA_JOB_PREFETCH
-    // STRING mode: the next job's descriptor and payloads are loaded before the current job runs
-    // (their latency overlaps the current job's key gathers)
-    const auto load_pay = [&](const Job& J, uint64_t (&p)[4]) {
-        const uint64_t* K = J.buf ? a.key1 : a.key0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            const uint32_t c = lane_id() * 4 + r;
-            p[r]             = c < J.len ? K[J.start + c] : 0ull;
-        }
-    };
-    if (MODE == MODE_STRING)
     {
-        Job      J = j != ~0u ? a.jobs[j] : Job{};
-        uint64_t pc[4];
-        if (j != ~0u)
-            load_pay(J, pc);
+        [[maybe_unused]] constexpr int W = 1, wj = 0;
+        JT_INIT();
+        [[maybe_unused]] unsigned long long tp = JT_NOW();
         while (j != ~0u)
         {
-            const uint32_t jn = next(j);
-            Job            Jn{};
-            uint64_t       pn[4] = {0, 0, 0, 0};
-            if (jn != ~0u)
+            const Job J = a.jobs[j];
             {
-                Jn = a.jobs[jn];
-                load_pay(Jn, pn);
+                [[maybe_unused]] const unsigned long long t1 = JT_NOW();
+                JT_ADD(8, t1 - tp);
             }
-            job_run<MODE, 1>(a, J, lds[wl], 0, pc);
-            J = Jn;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                pc[r] = pn[r];
-            j = jn;
+            job_run<MODE, 1>(a, J, a.blocks[J.block], job_pack(a, MODE, J.block), lds[wl], 0);
+            tp = JT_NOW();
+            j  = next(j);
         }
-        return;
-    }
-#endif
-    while (j != ~0u)
-    {
-        job_run<MODE, 1>(a, a.jobs[j], lds[wl], 0);
-        j = next(j);
+        if (MODE == MODE_STRING)
+            JT_FLUSH(0);
     }
 }
 
@@ -2343,6 +2428,7 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
         return __builtin_amdgcn_readfirstlane(claim[(k++) & 1]);
     };
     const int wj = threadIdx.x >> 6;
+    JT_INIT();
     [[maybe_unused]] unsigned long long tc = JT_NOW();
     uint32_t j = dyn ? next(0) : (R.first < R.end ? R.first : ~0u);
     while (j != ~0u)
@@ -2351,10 +2437,13 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
             [[maybe_unused]] const unsigned long long t1 = JT_NOW();
             JT_ADD(0, t1 - tc);
         }
-        job_run<MODE, W>(a, a.jobs[j], S, wj);
+        const Job J = a.jobs[j];
+        job_run<MODE, W>(a, J, a.blocks[J.block], job_pack(a, MODE, J.block), S, wj);
         tc = JT_NOW();
         j = next(j);
     }
+    if (wj == 0)
+        JT_FLUSH(1);
 }
 
 // Workgroup-job size classes: a job of (256, 512] elements runs on 2 waves, (512, 1024] on 4,
@@ -2814,7 +2903,7 @@ struct BwtWorkspace
     uint32_t  jobs_grid  = 2048;      // workgroups of the wave-job launch: about the resident capacity (with the
                                       // dynamic job queues extra groups only cost launch overhead: 8192: 2.94 ms, 2048: 2.67)
     uint32_t* jobq       = nullptr;   // per-XCD claim counters of the job launches ((1 + MJ_CLASSES) x 8 x 32 dwords)
-    uint32_t  jobq_chunk = 2;         // wave jobs claimed at once
+    uint32_t  jobq_chunk = BRA_JQ_CHUNK;  // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
     uint32_t  mj_classes() const { return mj_waves >= 16 ? 4u : mj_waves >= 8 ? 3u : mj_waves >= 4 ? 2u : 1u; }
@@ -3328,11 +3417,11 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return false;
 #ifdef BRA_JOB_TIMING
     {
-        unsigned long long jt[2][8];
+        unsigned long long jt[2][10];
         BRA_HIP_CHECK(hipMemcpyFromSymbol(jt, HIP_SYMBOL(g_jt), sizeof jt));
         for (int k = 0; k < 2; ++k)
-            fprintf(stderr, "[job timing %s] claim %llu gather1 %llu sort1 %llu groups+out %llu regather %llu sortN %llu | sorts %llu jobs %llu\n",
-                    k ? "wg" : "wave", jt[k][0], jt[k][1], jt[k][2], jt[k][3], jt[k][4], jt[k][5], jt[k][6], jt[k][7]);
+            fprintf(stderr, "[job timing %s] claim %llu gather1 %llu sort1 %llu groups+out %llu regather %llu sortN %llu | sorts %llu jobs %llu | between jobs %llu\n",
+                    k ? "wg" : "wave", jt[k][0], jt[k][1], jt[k][2], jt[k][3], jt[k][4], jt[k][5], jt[k][6], jt[k][7], jt[k][8]);
         std::memset(jt, 0, sizeof jt);
         BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_jt), jt, sizeof jt));
     }

@@ -74,6 +74,63 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t seed, u
     return op(pre, ex);
 }
 
+// Two independent exclusive workgroup scans (orders F1 / F2, seeds, identities as block_scan_excl)
+// sharing one LDS exchange and ONE barrier: tmp = 8 dwords that no thread touches again before the
+// caller's next barrier (callers rotate three regions, so a tile costs one barrier per dependent
+// scan round instead of two per scan).  all1 / all2 receive the totals including the seeds.
+template <bool F1, bool F2, typename O1, typename O2>
+__device__ __forceinline__ void block_scan_pair(uint32_t v1, uint32_t seed1, uint32_t id1, O1 op1, uint32_t& ex1, uint32_t& all1, uint32_t v2,
+                                                uint32_t seed2, uint32_t id2, O2 op2, uint32_t& ex2, uint32_t& all2, uint32_t* tmp)
+{
+    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    uint32_t       e1, e2;
+    const uint32_t i1 = wave_scan<F1>(v1, id1, op1, &e1);
+    const uint32_t i2 = wave_scan<F2>(v2, id2, op2, &e2);
+    if (lane == (F1 ? 63 : 0))
+        tmp[w] = i1;
+    if (lane == (F2 ? 63 : 0))
+        tmp[4 + w] = i2;
+    __syncthreads();
+    uint32_t p1 = seed1, a1 = seed1, p2 = seed2, a2 = seed2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+    {
+        const int      k1 = F1 ? i : 3 - i, k2 = F2 ? i : 3 - i;
+        const uint32_t t1 = tmp[k1], t2 = tmp[4 + k2];
+        if (F1 ? (k1 < w) : (k1 > w))
+            p1 = op1(p1, t1);
+        if (F2 ? (k2 < w) : (k2 > w))
+            p2 = op2(p2, t2);
+        a1 = op1(a1, t1);
+        a2 = op2(a2, t2);
+    }
+    ex1  = op1(p1, e1);
+    ex2  = op2(p2, e2);
+    all1 = a1;
+    all2 = a2;
+}
+
+// Exclusive sum over the workgroup with one barrier (tmp as in block_scan_pair: 4 dwords).
+__device__ __forceinline__ uint32_t block_sum_excl1(uint32_t v, uint32_t* tmp, uint32_t& total)
+{
+    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t x    = wave_scan<true>(v, 0u, OpAdd());
+    if (lane == 63)
+        tmp[w] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+    {
+        const uint32_t t = tmp[i];
+        if (i < w)
+            pre += t;
+        tot += t;
+    }
+    total = tot;
+    return pre + x - v;
+}
+
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[4], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
 
 // Bit i set iff byte i differs from byte i-1 (bit 0: from `prev`), for the PT bytes of w.
@@ -141,8 +198,8 @@ __device__ __forceinline__ void tile_runs(const TileThread& T, uint32_t left, ui
 {
     const uint32_t lastB  = T.bm ? T.base + hi_bit(T.bm) : 0u;
     const uint32_t firstB = T.bm ? T.base + lo_bit(T.bm) : T.n;
-    const uint32_t Sprev  = block_scan_excl<true>(lastB, 0u, 0u, OpMax(), tmp);
-    const uint32_t Enext  = block_scan_excl<false>(firstB, T.n, T.n, OpMin(), tmp);
+    uint32_t       Sprev, Enext, u0, u1;
+    block_scan_pair<true, false>(lastB, 0u, 0u, OpMax(), Sprev, u0, firstB, T.n, T.n, OpMin(), Enext, u1, tmp);
     nl = rs = 0;
 #pragma unroll
     for (int i = 0; i < PT; ++i)
@@ -234,11 +291,12 @@ __global__ void __launch_bounds__(TPB) k_rle_runs(const uint8_t* __restrict__ in
             edge[1] = byte_at(T.w, (int) T.nt - 1);
         if (threadIdx.x == 0)
             edge[0] = byte_at(T.w, 0);
-        // first boundary after position 0 and the last boundary
+        // first boundary after position 0 and the last boundary (one scan pair: edge[] is read
+        // after its barrier)
         const uint32_t b1 = T.bm & ~(T.base == 0 ? 1u : 0u);
-        uint32_t       lo, hi;
-        block_scan_excl<true>(T.bm ? T.base + hi_bit(T.bm) : 0u, 0u, 0u, OpMax(), tmp, &hi);
-        block_scan_excl<true>(b1 ? T.base + lo_bit(b1) : T.n, T.n, T.n, OpMin(), tmp, &lo);
+        uint32_t       lo, hi, u0, u1;
+        block_scan_pair<true, true>(T.bm ? T.base + hi_bit(T.bm) : 0u, 0u, 0u, OpMax(), u0, hi, b1 ? T.base + lo_bit(b1) : T.n, T.n, T.n, OpMin(),
+                                    u1, lo, tmp);
         if (threadIdx.x == 0)
         {
             const uint32_t all = lo >= T.n ? 1u : 0u;
@@ -343,7 +401,7 @@ __global__ void __launch_bounds__(64) k_rle_link(const uint32_t* __restrict__ fi
 __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ in, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                    const TileLink* __restrict__ link, TileGap* __restrict__ tg)
 {
-    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t tmp[3][8];  // one region per dependent scan round (block_scan_pair)
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const Piece    P = tiles[t];
@@ -351,13 +409,13 @@ __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ i
         TileThread     T;
         tile_load(in, P, T);
         uint32_t nl, rs, clen[PT];
-        tile_runs(T, K.left, K.right, tmp, nl, rs, clen);
-        uint32_t       maxNL, minNL;
-        const uint32_t GSprev = block_scan_excl<true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), tmp, &maxNL);
-        block_scan_excl<true>(nl ? T.base + lo_bit(nl) : T.n, T.n, T.n, OpMin(), tmp, &minNL);
+        tile_runs(T, K.left, K.right, tmp[0], nl, rs, clen);
+        uint32_t maxNL, minNL, GSprev, u0;
+        block_scan_pair<true, true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), GSprev, maxNL, nl ? T.base + lo_bit(nl) : T.n, T.n, T.n,
+                                    OpMin(), u0, minNL, tmp[1]);
         const uint32_t bytes = tile_emit<false>(T, nl, rs, clen, GSprev, 0, 0, 0, nullptr, 0);
         uint32_t       total;
-        block256_exclusive_sum(bytes, tmp, &total);
+        block_sum_excl1(bytes, tmp[2], total);
         if (threadIdx.x == 0)
         {
             const uint32_t has  = maxNL > 0 ? 1u : 0u;
@@ -365,7 +423,6 @@ __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ i
             // the leading stretch's control bytes were counted with gap offset 0: ceil(lead/128)
             tg[t] = TileGap{lead, has ? T.n - maxNL : T.n, has, total - (lead + 127) / 128};
         }
-        __syncthreads();
     }
 }
 
@@ -432,7 +489,7 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ rle_base, uint8_t* __restrict__ out,
                                                    uint32_t* __restrict__ hist)
 {
-    __shared__ uint32_t tmp[8];
+    __shared__ uint32_t tmp[2][8];  // tile_runs' scan pair, then the two-barrier scans
     __shared__ uint8_t  stage[RLE_TILE + RLE_TILE / 64 + 64];
     constexpr int       HC = 4, HS = 256 + 16;  // histogram copies (lane & 3), 16 banks apart: output bytes are skewed
     __shared__ uint32_t h[HC * HS];
@@ -448,12 +505,12 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
         TileThread T;
         tile_load(in, P, T);
         uint32_t nl, rs, clen[PT];
-        tile_runs(T, K.left, K.right, tmp, nl, rs, clen);
-        const uint32_t GSprev = block_scan_excl<true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), tmp);
-        const uint32_t GEnext = block_scan_excl<false>(nl ? T.base + lo_bit(nl) : T.n, T.n, T.n, OpMin(), tmp);
+        tile_runs(T, K.left, K.right, tmp[0], nl, rs, clen);
+        const uint32_t GSprev = block_scan_excl<true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), tmp[1]);
+        const uint32_t GEnext = block_scan_excl<false>(nl ? T.base + lo_bit(nl) : T.n, T.n, T.n, OpMin(), tmp[1]);
         const uint32_t by     = tile_emit<false>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, nullptr, 0);
         uint32_t       total;
-        const uint32_t pos = block256_exclusive_sum(by, tmp, &total);
+        const uint32_t pos = block256_exclusive_sum(by, tmp[1], &total);
         tile_emit<true>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, stage, pos);
         __syncthreads();
         uint8_t*       dst = out + rle_base[P.block] + O.out_off;
