@@ -9,6 +9,10 @@ struct BwtWorkspace;
 BwtWorkspace* bwt_workspace_create();
 void          bwt_workspace_destroy(BwtWorkspace* w);
 
+// Per block (after bwt_encode_device): 256-bit presence mask of its byte values, 8 dwords each (the
+// BWT output has the same bytes, so the MTF stage takes its alphabets from here).
+const uint32_t* bwt_alpha_masks(const BwtWorkspace* w);
+
 // BWT of every block: d_L[off..off+len) = last column, d_pi[b] = primary index (block-local).
 bool bwt_encode_device(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s);

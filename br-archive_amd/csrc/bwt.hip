@@ -3057,6 +3057,7 @@ static void ws_free(BwtWorkspace& w)
 }
 
 BwtWorkspace* bwt_workspace_create() { return new BwtWorkspace(); }
+const uint32_t* bwt_alpha_masks(const BwtWorkspace* w) { return w ? w->amask : nullptr; }
 void          bwt_workspace_destroy(BwtWorkspace* w)
 {
     if (w)

@@ -304,7 +304,8 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     }
     {
         BRA_PROF(P_STAGE_MTF, s);
-        if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s))
+        // the BWT's per-block presence masks are the alphabets of its output too
+        if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s, bwt_alpha_masks(c->bwt)))
             return -1;
     }
     {

@@ -92,10 +92,19 @@ struct MtfWorkspace
     Tiling    tiling;
     void*     state     = nullptr;
     size_t    cap_state = 0;
-    uint32_t* nsym      = nullptr;  // distinct symbols per block (k_mtf_scan)
-    uint8_t*  amap      = nullptr;  // per block: alphabet index of every byte value (k_mtf_scan)
-    uint32_t* amode     = nullptr;  // per block: position-table dwords of the register encoder (0: byte tables)
+    uint32_t* nsym      = nullptr;  // distinct symbols per block (k_mtf_alpha)
+    uint8_t*  amap      = nullptr;  // per block: alphabet index of every byte value (0xFF: absent)
+    uint8_t*  ainv      = nullptr;  // per block: byte value of alphabet index a < 32 (position-table blocks)
+    uint32_t* amode     = nullptr;  // per block: position-table dwords (4 / 8) of k_mtf_encode_pos, 0: other encoders
+    uint32_t* amask     = nullptr;  // per block: presence mask (when the caller has none)
     uint32_t  cap_nsym  = 0;
+    // chunks of half segments of the position-table passes (built with the tiling's geometry)
+    uint32_t*             pt_chunk0 = nullptr;  // per block: first chunk
+    uint32_t*             pt_chunk_blk = nullptr;  // per chunk: block
+    int32_t*              pt_cmax = nullptr;   // per chunk: 32 maxima, then exclusive prefixes
+    uint32_t              pt_nchunks = 0;
+    size_t                pt_cap_c = 0, pt_cap_b = 0;
+    std::vector<uint32_t> pt_key;              // per block segment counts the chunk arrays were built for
 
     bool reserve(size_t bytes)
     {
@@ -113,7 +122,8 @@ struct MtfWorkspace
         if (nblocks <= cap_nsym)
             return true;
         cap_nsym = 0;
-        if (!dev_alloc(nsym, (uint64_t) nblocks + 64) || !dev_alloc(amap, 256ull * (nblocks + 64)) || !dev_alloc(amode, (uint64_t) nblocks + 64))
+        if (!dev_alloc(nsym, (uint64_t) nblocks + 64) || !dev_alloc(amap, 256ull * (nblocks + 64)) || !dev_alloc(amode, (uint64_t) nblocks + 64) ||
+            !dev_alloc(ainv, 32ull * (nblocks + 64)) || !dev_alloc(amask, 8ull * (nblocks + 64)))
             return false;
         cap_nsym = nblocks + 64;
         return true;
@@ -125,16 +135,30 @@ struct MtfWorkspace
         (void) hipFree(nsym);
         (void) hipFree(amap);
         (void) hipFree(amode);
+        (void) hipFree(ainv);
+        (void) hipFree(amask);
+        (void) hipFree(pt_chunk0);
+        (void) hipFree(pt_chunk_blk);
+        (void) hipFree(pt_cmax);
+        pt_chunk0 = pt_chunk_blk = nullptr;
+        pt_cmax                  = nullptr;
+        pt_nchunks               = 0;
+        pt_cap_c = pt_cap_b = 0;
+        pt_key.clear();
         state     = nullptr;
         nsym      = nullptr;
         amap      = nullptr;
         amode     = nullptr;
+        ainv      = nullptr;
+        amask     = nullptr;
         cap_state = 0;
         cap_nsym  = 0;
     }
 };
 
-bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s);
+// d_amask: per block presence masks of d_in's blocks (8 dwords each, e.g. bwt_alpha_masks), or null.
+bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s,
+                       const uint32_t* d_amask = nullptr);
 // d_tmp: scratch of the batch size (labels)
 bool mtf_decode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, uint8_t* d_tmp, const BlockDesc* h_blocks, uint32_t nblocks,
                        hipStream_t s);

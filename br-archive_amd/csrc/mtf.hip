@@ -6,10 +6,17 @@
 // Encode is made segment-parallel with the recency formulation: the MTF table at any point lists
 // symbols by decreasing last-occurrence time, never-seen symbols last in ascending order (the
 // initial identity table is the recency order of a virtual prefix 255, 254, ..., 0).  So
-//   k_mtf_lastocc   last occurrence of every symbol inside each segment (LDS atomicMax),
-//   k_mtf_scan      exclusive max-scan over the segments of a block -> start-of-segment times,
-//   k_mtf_encode_reg   blocks of <= MTF_REG distinct symbols: one thread per segment, the table
-//                      front in registers;
+//   k_mtf_presence / k_mtf_alpha   each block's alphabet (from the BWT's presence masks when the
+//                      caller has them): distinct symbols, alphabet index of every value, and the
+//                      block's encoder: position tables (<= 32 values, all below 127: text, small
+//                      alphabets), register byte tables (other <= 32-symbol blocks) or waves;
+//   k_mtf_lastocc   last occurrence of every symbol inside each segment (LDS atomicMax); for a
+//                   position-table block, of its <= 32 alphabet values inside each HALF segment;
+//   k_mtf_scan      exclusive max-scan over the (half) segments of a block -> start-of-segment
+//                   times; position-table blocks: the start position table of every half segment;
+//   k_mtf_encode_pos   position-table blocks: one thread per 512-byte half segment;
+//   k_mtf_encode_reg   other blocks of <= MTF_REG distinct symbols: one thread per segment, the
+//                      table front in registers;
 //   k_mtf_encode_wave  larger alphabets: one wave per segment, 64 symbols per step (ballots).
 // Decode uses relabelling: a decode step moves table POSITION p to the front whatever the table
 // holds, so decoding a segment from the identity table gives labels u_i and an end permutation
@@ -35,21 +42,82 @@ __device__ __forceinline__ void wave_barrier_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Presence masks when the caller has none: one wave per segment ORs its bytes into 8 mask dwords
+// and adds them to its block's mask (amask zeroed by the caller).
+__global__ void __launch_bounds__(TPB) k_mtf_presence(const uint8_t* __restrict__ in, const Piece* __restrict__ segs, uint32_t nseg,
+                                                      uint32_t* __restrict__ amask)
+{
+    const int      lane = lane_id();
+    const uint32_t wave = threadIdx.x >> 6;
+    for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
+    {
+        const Piece P = segs[s];
+        uint32_t    m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t i = lane; i < P.len; i += 64)
+        {
+            const uint32_t v = in[P.off + i];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                m[k] |= ((v >> 5) == (uint32_t) k) ? (1u << (v & 31)) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+        {
+            const uint32_t x = wave_scan<true>(m[k], 0u, OpOr());
+            if (lane == 63 && x)
+                atomicOr(&amask[8 * (size_t) P.block + k], x);
+        }
+    }
+}
+
+// One workgroup per block, thread c = byte value c: the block's alphabet from its presence mask.
+// amap[b][c] = rank of c among the present values (0xFF: absent), ainv[b][a] = the a-th present
+// value (a < 32), amode[b] = 4 / 8 position-table dwords when the block has at most 16 / 32
+// distinct values, all below 127 (every MTF position then stays below 127), else 0.
+__global__ void __launch_bounds__(TPB) k_mtf_alpha(const uint32_t* __restrict__ amask, uint32_t nblocks, uint32_t* __restrict__ nsym,
+                                                   uint8_t* __restrict__ amap, uint8_t* __restrict__ ainv, uint32_t* __restrict__ amode)
+{
+    __shared__ uint32_t tmp[8];
+    const uint32_t      c = threadIdx.x;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const bool     pres = (amask[8 * (size_t) b + (c >> 5)] >> (c & 31)) & 1u;
+        const int      n    = __syncthreads_count(pres);
+        const bool     high = __syncthreads_or(pres && c >= 127) != 0;
+        const uint32_t rk   = block256_exclusive_sum(pres ? 1u : 0u, tmp);
+        amap[(size_t) b * 256 + c] = pres ? (uint8_t) rk : (uint8_t) 0xFF;
+        if (pres && rk < 32)
+            ainv[(size_t) b * 32 + rk] = (uint8_t) c;
+        if (c == 0)
+        {
+            nsym[b]  = (uint32_t) n;
+            amode[b] = high ? 0u : (n <= 16 ? 4u : (n <= 32 ? 8u : 0u));
+        }
+        __syncthreads();
+    }
+}
+
 // One wave per segment (1024 symbols = 16 per lane, one 16-byte load): each lane keeps only the
 // last byte of every run of equal bytes inside its 16 and max-updates the segment's 256 LDS
 // entries; the state row goes out as one 16-byte store per lane.  (A workgroup per segment with a
 // 4-byte load per thread was bound by its load -> atomics -> barrier -> store latency chain.)
+// Position-table blocks: the lanes of each half segment (lanes 0-31: bytes 0-511) update their own
+// row, and the segment's state is two compact rows, [256 s + 32 h + a] = last occurrence of the
+// block's a-th value in half h (-1: none; a >= the block's alphabet: -1).
 __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__ in, const Piece* __restrict__ segs, uint32_t nseg,
-                                                     int32_t* __restrict__ state)
+                                                     int32_t* __restrict__ state, const uint32_t* __restrict__ amode,
+                                                     const uint32_t* __restrict__ nsym, const uint8_t* __restrict__ ainv)
 {
-    __shared__ int32_t lo_s[TPB / 64][256];
+    __shared__ int32_t lo_s[TPB / 64][2][256];
     const int      lane = lane_id();
     const uint32_t wave = threadIdx.x >> 6;
-    int32_t*       lo   = lo_s[wave];
     for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
     {
-        const Piece P = segs[s];
-        reinterpret_cast<int4*>(lo)[lane] = make_int4(-1, -1, -1, -1);
+        const Piece    P    = segs[s];
+        const bool     half = amode[P.block] != 0;
+        int32_t*       lo   = lo_s[wave][half ? (lane >> 5) : 0];
+        reinterpret_cast<int4*>(lo_s[wave][0])[lane] = make_int4(-1, -1, -1, -1);
+        reinterpret_cast<int4*>(lo_s[wave][1])[lane] = make_int4(-1, -1, -1, -1);
         const uint8_t* p    = in + P.off;
         const uint32_t i0   = (uint32_t) lane * 16;
         uint32_t       w[4] = {0, 0, 0, 0};
@@ -72,27 +140,150 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
                 atomicMax(&lo[c], (int32_t) (i0 + j));
         }
         wave_barrier_lds();
-        const int4 v = reinterpret_cast<const int4*>(lo)[lane];
         const int32_t st = (int32_t) P.start;
-        reinterpret_cast<int4*>(state + (size_t) s * 256)[lane] =
-            make_int4(v.x >= 0 ? st + v.x : -1, v.y >= 0 ? st + v.y : -1, v.z >= 0 ? st + v.z : -1, v.w >= 0 ? st + v.w : -1);
+        if (half)
+        {
+            const uint32_t a = (uint32_t) lane & 31u;
+            const int32_t  v = a < nsym[P.block] ? lo_s[wave][lane >> 5][ainv[(size_t) P.block * 32 + a]] : -1;
+            state[(size_t) s * 256 + lane] = v >= 0 ? st + v : -1;
+        }
+        else
+        {
+            const int4 v = reinterpret_cast<const int4*>(lo)[lane];
+            reinterpret_cast<int4*>(state + (size_t) s * 256)[lane] =
+                make_int4(v.x >= 0 ? st + v.x : -1, v.y >= 0 ? st + v.y : -1, v.z >= 0 ? st + v.z : -1, v.w >= 0 ? st + v.w : -1);
+        }
         wave_barrier_lds();
     }
 }
 
-// One workgroup per block; thread c scans symbol c over the block's segments (exclusive max).
-// Also the block's alphabet for the position-table encoder: amap[b][c] = rank of value c among the
-// values present in the block (0xFF: absent), amode[b] = 4 / 8 table dwords when the block has at
-// most 16 / 32 distinct values, all below 127 (every MTF position then stays below 127), else 0.
-__global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
-                                                  uint32_t nblocks, int32_t* __restrict__ state, uint32_t* __restrict__ nsym,
-                                                  uint8_t* __restrict__ amap, uint32_t* __restrict__ amode)
+// ---- position-table blocks: start tables of the half segments, in three parallel passes ----
+// Half segment h of segment s: state ints [256 s + 32 (h & 1), +32) hold its last occurrences (one
+// per alphabet index a); chunks of PT_CHUNK consecutive half segments of a block, one half wave
+// (lane a) per chunk.
+constexpr uint32_t PT_CHUNK = 32;
+
+struct PtGeo
 {
-    __shared__ uint32_t tmp[8];
+    const uint32_t* first_seg;   // per block: first segment
+    const uint32_t* nseg_blk;    // per block: segments
+    const uint32_t* chunk0;      // per block: first chunk (exclusive prefix of ceil(2 ns / PT_CHUNK))
+    const uint32_t* chunk_blk;   // per chunk: block
+    uint32_t        nchunks;
+};
+
+__device__ __forceinline__ int32_t* pt_row(int32_t* state, uint32_t s0, uint32_t h, uint32_t a)
+{
+    return state + (size_t) (s0 + (h >> 1)) * 256 + (h & 1) * 32 + a;
+}
+
+// Pass 1: the maximum of every chunk (cmax[32 c + a]).
+__global__ void __launch_bounds__(TPB) k_mtf_pt_max(int32_t* __restrict__ state, PtGeo g, const uint32_t* __restrict__ amode, int32_t* __restrict__ cmax)
+{
+    const uint32_t a = threadIdx.x & 31u;
+    for (uint32_t c = blockIdx.x * (TPB / 32) + (threadIdx.x >> 5); c < g.nchunks; c += gridDim.x * (TPB / 32))
+    {
+        const uint32_t b = g.chunk_blk[c];
+        if (!amode[b])
+            continue;
+        const uint32_t s0 = g.first_seg[b], H = 2 * g.nseg_blk[b], h0 = (c - g.chunk0[b]) * PT_CHUNK, h1 = min(H, h0 + PT_CHUNK);
+        int32_t        v[PT_CHUNK];
+#pragma unroll
+        for (uint32_t u = 0; u < PT_CHUNK; ++u)
+            v[u] = h0 + u < h1 ? *pt_row(state, s0, h0 + u, a) : -1;
+        int32_t m = -1;
+#pragma unroll
+        for (uint32_t u = 0; u < PT_CHUNK; ++u)
+            m = max(m, v[u]);
+        cmax[32 * (size_t) c + a] = m;
+    }
+}
+
+// Pass 2, one workgroup per block: exclusive max-scan of its chunk maxima, in place (8 groups of 32
+// threads over consecutive eighths, group maxima through LDS).
+__global__ void __launch_bounds__(TPB) k_mtf_pt_scan(PtGeo g, uint32_t nblocks, const uint32_t* __restrict__ amode, int32_t* __restrict__ cmax)
+{
+    __shared__ int32_t agg[8][32];
+    const uint32_t     a = threadIdx.x & 31u, gr = threadIdx.x >> 5;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        if (!amode[b])
+            continue;
+        const uint32_t c0 = g.chunk0[b], nc = div_up(2ull * g.nseg_blk[b], PT_CHUNK), C = div_up(nc, 8u);
+        const uint32_t k0 = min(nc, gr * C), k1 = min(nc, k0 + C);
+        int32_t        m = -1;
+        for (uint32_t k = k0; k < k1; ++k)
+            m = max(m, cmax[32 * (size_t) (c0 + k) + a]);
+        agg[gr][a] = m;
+        __syncthreads();
+        int32_t run = -1;
+        for (uint32_t q = 0; q < gr; ++q)
+            run = max(run, agg[q][a]);
+        for (uint32_t k = k0; k < k1; ++k)
+        {
+            int32_t* p = cmax + 32 * (size_t) (c0 + k) + a;
+            const int32_t v = *p;
+            *p              = run;
+            run             = max(run, v);
+        }
+        __syncthreads();  // agg is rewritten by the next block
+    }
+}
+
+// Pass 3: every half segment's start position table from its chunk's prefix: byte a of the 32 bytes
+// at state byte 1024 s + 512 + 32 (h & 1) = 0x80 | the position of the block's a-th value (seen
+// values: the number of values seen later; unseen ones follow the seen ones by value), 0xFF beyond
+// the alphabet -- the table k_mtf_encode_pos starts from.
+__global__ void __launch_bounds__(TPB) k_mtf_pt_tables(int32_t* __restrict__ state, PtGeo g, const uint32_t* __restrict__ amode,
+                                                       const uint32_t* __restrict__ nsym, const uint8_t* __restrict__ ainv,
+                                                       const int32_t* __restrict__ cpre)
+{
+    const uint32_t a = threadIdx.x & 31u, hb = (uint32_t) lane_id() & 32u;
+    uint8_t*       pt = reinterpret_cast<uint8_t*>(state);
+    for (uint32_t c = blockIdx.x * (TPB / 32) + (threadIdx.x >> 5); c < g.nchunks; c += gridDim.x * (TPB / 32))
+    {
+        const uint32_t b = g.chunk_blk[c];  // uniform per half wave
+        if (!amode[b])
+            continue;
+        const uint32_t s0 = g.first_seg[b], H = 2 * g.nseg_blk[b], h0 = (c - g.chunk0[b]) * PT_CHUNK, h1 = min(H, h0 + PT_CHUNK);
+        const uint32_t na = nsym[b], val = a < na ? ainv[(size_t) b * 32 + a] : 0u;
+        int32_t        run = cpre[32 * (size_t) c + a];
+        int32_t        v[PT_CHUNK];
+#pragma unroll
+        for (uint32_t u = 0; u < PT_CHUNK; ++u)
+            v[u] = h0 + u < h1 ? *pt_row(state, s0, h0 + u, a) : -1;
+        for (uint32_t h = h0; h < h1; ++h)
+        {
+            int32_t nv = v[0];
+#pragma unroll
+            for (uint32_t u = 0; u + 1 < PT_CHUNK; ++u)  // shift the chunk's rows down by one (constant indices)
+                v[u] = v[u + 1];
+            const int32_t  tt   = run;  // last occurrence before half segment h
+            run                 = max(run, nv);
+            const bool     seen = a < na && tt >= 0;
+            const uint32_t mk   = (uint32_t) (__builtin_amdgcn_ballot_w64(seen) >> hb);
+            uint32_t       later = 0;
+#pragma unroll 8
+            for (uint32_t j = 0; j < 32; ++j)
+                later += __shfl(tt, (int) (hb + j), 64) > tt ? 1u : 0u;
+            const uint32_t pos = seen ? later : (uint32_t) __popc(mk) + val - (uint32_t) __popc(mk & ((1u << a) - 1u));
+            pt[(size_t) (s0 + (h >> 1)) * 1024 + 512 + (h & 1) * 32 + a] = a < na ? (uint8_t) (0x80u | pos) : (uint8_t) 0xFF;
+        }
+    }
+}
+
+// One workgroup per block; thread c scans symbol c over the block's segments (exclusive max);
+// position-table blocks are the k_mtf_pt_* passes'.
+__global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
+                                                  uint32_t nblocks, int32_t* __restrict__ state, const uint32_t* __restrict__ nsym,
+                                                  const uint8_t* __restrict__ ainv, const uint32_t* __restrict__ amode)
+{
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint32_t s0  = first_seg[b];
         const uint32_t ns  = nseg_blk[b];
+        if (amode[b])
+            continue;  // k_mtf_pt_*
         int32_t        run = -1;
         const uint32_t c   = threadIdx.x;
         uint32_t       k   = 0;
@@ -117,16 +308,6 @@ __global__ void __launch_bounds__(TPB) k_mtf_scan(const uint32_t* __restrict__ f
             state[(size_t) (s0 + k) * 256 + c] = run;
             run                                   = max(run, v);
         }
-        const int      n    = __syncthreads_count(run >= 0);  // distinct symbols of the block
-        const bool     high = __syncthreads_or(run >= 0 && c >= 127) != 0;
-        const uint32_t rk   = block256_exclusive_sum(run >= 0 ? 1u : 0u, tmp);
-        amap[(size_t) b * 256 + c] = run >= 0 ? (uint8_t) rk : (uint8_t) 0xFF;
-        if (threadIdx.x == 0)
-        {
-            nsym[b]  = (uint32_t) n;
-            amode[b] = high ? 0u : (n <= 16 ? 4u : (n <= 32 ? 8u : 0u));
-        }
-        __syncthreads();
     }
 }
 
@@ -430,17 +611,25 @@ template <int NP>
 __device__ __forceinline__ uint32_t mtf_step_pos(uint32_t (&R)[NP], uint32_t a)
 {
     const uint32_t q = a >> 2;
-    uint32_t       x;
+    // the table dwords as opaque scalar values: a select tree over loads of one array became a
+    // dynamically indexed array (the table in scratch memory)
+    const auto op = [](uint32_t v) {
+        asm("" : "+v"(v));
+        return v;
+    };
+    uint32_t x;
     if constexpr (NP == 8)
     {
-        const uint32_t x0 = (q & 1) ? R[1] : R[0], x1 = (q & 1) ? R[3] : R[2], x2 = (q & 1) ? R[5] : R[4], x3 = (q & 1) ? R[7] : R[6];
+        const uint32_t r0 = op(R[0]), r1 = op(R[1]), r2 = op(R[2]), r3 = op(R[3]), r4 = op(R[4]), r5 = op(R[5]), r6 = op(R[6]), r7 = op(R[7]);
+        const uint32_t x0 = (q & 1) ? r1 : r0, x1 = (q & 1) ? r3 : r2, x2 = (q & 1) ? r5 : r4, x3 = (q & 1) ? r7 : r6;
         const uint32_t y0 = (q & 2) ? x1 : x0, y1 = (q & 2) ? x3 : x2;
         x = (q & 4) ? y1 : y0;
     }
     else
     {
         static_assert(NP == 4, "4 or 8 table dwords");
-        const uint32_t x0 = (q & 1) ? R[1] : R[0], x1 = (q & 1) ? R[3] : R[2];
+        const uint32_t r0 = op(R[0]), r1 = op(R[1]), r2 = op(R[2]), r3 = op(R[3]);
+        const uint32_t x0 = (q & 1) ? r1 : r0, x1 = (q & 1) ? r3 : r2;
         x = (q & 2) ? x1 : x0;
     }
     const uint32_t sh = (a & 3u) << 3;
@@ -455,70 +644,6 @@ __device__ __forceinline__ uint32_t mtf_step_pos(uint32_t (&R)[NP], uint32_t a)
         R[k]              = ((uint32_t) k == q) ? nv - dl : nv;
     }
     return r;
-}
-
-// Position bytes of a segment's start table, one wave: value c at position #(seen values with a
-// later last occurrence) if seen, else #seen + #(unseen values below c) (the identity order of the
-// unseen ones).  Writes byte amap[c] of the segment's front row (front[k][owner], bytes 4k..4k+3).
-__device__ __forceinline__ void start_pos_small(const int32_t* __restrict__ st, const uint8_t* __restrict__ map_s, uint32_t* sc_t,
-                                                uint32_t* sc_c, uint32_t (*front)[TPB], uint32_t owner)
-{
-    const int      lane  = lane_id();
-    const int4     tv    = reinterpret_cast<const int4*>(st)[lane];
-    const int32_t  tt[4] = {tv.x, tv.y, tv.z, tv.w};
-    uint32_t       nseen = 0, seen_before = 0;
-    uint64_t       bal[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        bal[r] = __builtin_amdgcn_ballot_w64(tt[r] >= 0);
-        nseen += (uint32_t) __popcll(bal[r]);
-    }
-    const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        seen_before += (uint32_t) __popcll(bal[r] & below);
-    if (lane < 8)
-        front[lane][owner] = 0xFFFFFFFFu;
-    uint32_t own_seen = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        const uint32_t c = (uint32_t) lane * 4 + r;
-        if (tt[r] >= 0)
-        {
-            sc_t[seen_before + own_seen] = (uint32_t) tt[r];
-            sc_c[seen_before + own_seen] = c;
-            ++own_seen;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint8_t* fb = reinterpret_cast<uint8_t*>(front);  // byte a of the row: dword (a >> 2) * TPB + owner, byte a & 3
-    if ((uint32_t) lane < nseen)
-    {
-        const uint32_t my = sc_t[lane];
-        uint32_t       p  = 0;
-        for (uint32_t j = 0; j < nseen; ++j)
-            p += sc_t[j] > my ? 1u : 0u;
-        const uint32_t a = map_s[sc_c[lane]];
-        fb[((a >> 2) * TPB + owner) * 4 + (a & 3)] = (uint8_t) (0x80u | p);
-    }
-    uint32_t sb = seen_before;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        const uint32_t c = (uint32_t) lane * 4 + r;
-        const uint32_t a = map_s[c];
-        if (tt[r] < 0 && a != 0xFFu)
-            fb[((a >> 2) * TPB + owner) * 4 + (a & 3)] = (uint8_t) (0x80u | (nseen + c - sb));
-        if (tt[r] >= 0)
-            ++sb;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Symbols and ranks move through LDS in rounds of 64 bytes per segment, chunk-major (io[c][t]:
@@ -558,6 +683,7 @@ __device__ __forceinline__ void mtf_code_rounds(const uint8_t* __restrict__ in, 
                 else
                 {
                     uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
                     for (int k = 0; k < 16; ++k)
                         w[k >> 2] |= (uint32_t) q[k] << (8 * (k & 3));
                     io[c][sl] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -608,6 +734,7 @@ __device__ __forceinline__ void mtf_code_rounds(const uint8_t* __restrict__ in, 
                 else
                 {
                     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
                     for (int k = 0; k < 16; ++k)
                         q[k] = (uint8_t) (w[k >> 2] >> (8 * (k & 3)));
                 }
@@ -619,12 +746,79 @@ __device__ __forceinline__ void mtf_code_rounds(const uint8_t* __restrict__ in, 
         out[off + i] = (uint8_t) step(R, MAP ? (uint32_t) map_s[in[off + i]] : (uint32_t) in[off + i]);
 }
 
-// Blocks of at most MTF_REG distinct symbols.  A workgroup iteration whose 256 segments all lie in
-// one block with a position-table alphabet (amode 4 / 8) codes them with mtf_step_pos; any other
-// iteration with the byte tables (mtf_step_reg).
+// Position-table blocks (amode 4 / 8), one thread per 512-byte half segment (twice the chains of
+// one thread per segment: the coding loop is a dependent chain per symbol, and at one segment per
+// thread a 256 MiB batch had only 4 waves per SIMD to overlap them).  Workgroup (x, y) codes half
+// segments [256 x, 256 x + 256) of block y, so the block's alphabet map sits in LDS and its table
+// width (4 dwords for <= 16 values, else 8) is uniform; each thread starts from its half segment's
+// position table (k_mtf_scan).
+template <int NP>
+__device__ __forceinline__ void encode_pos_wg(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const int32_t* __restrict__ state,
+                                              uint32_t s, uint32_t half, uint32_t len, uint4 (*io)[TPB], const uint64_t* s_off,
+                                              const uint32_t* s_len, const uint8_t* map_s)
+{
+    uint32_t R[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        R[k] = 0xFFFFFFFFu;
+    if (len)
+    {
+        const uint4* pt = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(state) + (size_t) s * 1024 + 512 + half * 32);
+#pragma unroll
+        for (int q = 0; q < NP / 4; ++q)
+        {
+            const uint4 v = pt[q];
+            R[4 * q] = v.x, R[4 * q + 1] = v.y, R[4 * q + 2] = v.z, R[4 * q + 3] = v.w;
+        }
+    }
+    mtf_code_rounds<NP, true>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[NP], uint32_t a) { return mtf_step_pos<NP>(T, a); });
+}
+
+__global__ void __launch_bounds__(TPB, 8) k_mtf_encode_pos(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
+                                                        const uint32_t* __restrict__ first_seg, const uint32_t* __restrict__ nseg_blk,
+                                                        uint32_t nblocks, const int32_t* __restrict__ state, const uint8_t* __restrict__ amap,
+                                                        const uint32_t* __restrict__ amode)
+{
+    __shared__ uint4    io[MR_NC][TPB];
+    __shared__ uint64_t s_off[TPB];
+    __shared__ uint32_t s_len[TPB];  // 0: past the block
+    __shared__ uint8_t  map_s[256];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t b = blockIdx.y; b < nblocks; b += gridDim.y)
+    {
+        const uint32_t mode = amode[b], nh = 2 * nseg_blk[b], h = blockIdx.x * TPB + t;
+        if (mode == 0 || blockIdx.x * TPB >= nh)
+            continue;  // uniform per workgroup
+        const uint32_t s   = first_seg[b] + (h >> 1), half = h & 1u;
+        uint32_t       len = 0;
+        uint64_t       off = 0;
+        if (h < nh)
+        {
+            const Piece    P  = segs[s];
+            const uint32_t lo = half * (MTF_SEG_ENC / 2);
+            if (P.len > lo)
+            {
+                len = min(MTF_SEG_ENC / 2, P.len - lo);
+                off = P.off + lo;
+            }
+        }
+        s_off[t] = off;
+        s_len[t] = len;
+        map_s[t] = amap[(size_t) b * 256 + t];
+        __syncthreads();
+        if (mode == 4)
+            encode_pos_wg<4>(in, out, state, s, half, len, io, s_off, s_len, map_s);
+        else
+            encode_pos_wg<8>(in, out, state, s, half, len, io, s_off, s_len, map_s);
+        __syncthreads();
+    }
+}
+
+// Other blocks of at most MTF_REG distinct symbols: one thread per segment with the byte tables
+// (mtf_step_reg).
 __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
                                                         uint32_t nseg, const int32_t* __restrict__ state, const uint32_t* __restrict__ nsym,
-                                                        const uint8_t* __restrict__ amap, const uint32_t* __restrict__ amode)
+                                                        const uint32_t* __restrict__ amode)
 {
     __shared__ uint32_t front[NRD][TPB];  // start-table fronts of the workgroup's segments (thread-major: conflict-free)
     __shared__ uint32_t sc_t[TPB / 64][MTF_REG], sc_c[TPB / 64][MTF_REG];
@@ -632,42 +826,12 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restric
     __shared__ uint4    io[MR_NC][TPB];
     __shared__ uint64_t s_off[TPB];
     __shared__ uint32_t s_len[TPB];  // 0: not coded by this kernel (or past the batch)
-    __shared__ uint8_t  map_s[256];
-    __shared__ uint32_t mode_s;
     const uint32_t t    = threadIdx.x;
     const int      lane = lane_id();
     const uint32_t wave = t >> 6;
     for (uint32_t g0 = blockIdx.x * TPB; g0 < nseg; g0 += gridDim.x * TPB)
     {
-        if (t == 0)
-        {
-            const uint32_t b0 = segs[g0].block, b1 = segs[min(nseg, g0 + TPB) - 1].block;
-            mode_s            = (b0 == b1) ? (amode[b0] | (b0 << 4)) : 0u;
-        }
-        __syncthreads();
-        const uint32_t mode = mode_s & 15u;
-        if (mode)
-            map_s[t] = amap[(size_t) (mode_s >> 4) * 256 + t];
-        __syncthreads();
-        for (int q = 0; q < 64; ++q)
-        {
-            const uint32_t owner = wave * 64 + q;
-            const uint32_t s     = g0 + owner;
-            if (s >= nseg)
-                break;
-            const Piece P = segs[s];
-            if (nsym[P.block] > MTF_REG)
-                continue;
-            if (mode)
-                start_pos_small(state + (size_t) s * 256, map_s, sc_t[wave], sc_c[wave], front, owner);
-            else
-            {
-                const uint32_t d = (P.start == 0) ? (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u
-                                                  : start_front_small(state + (size_t) s * 256, sc_t[wave], sc_c[wave], sc_out[wave]);
-                if (lane < NRD)
-                    front[lane][owner] = d;
-            }
-        }
+        const auto mine = [&](const Piece& P) { return nsym[P.block] <= MTF_REG && amode[P.block] == 0; };
         {
             const uint32_t s = g0 + t;
             uint32_t       l = 0;
@@ -675,36 +839,33 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_reg(const uint8_t* __restric
             {
                 const Piece P = segs[s];
                 s_off[t]      = P.off;
-                l             = nsym[P.block] <= MTF_REG ? P.len : 0u;
+                l             = mine(P) ? P.len : 0u;
             }
             s_len[t] = l;
         }
+        if (!__syncthreads_or(s_len[t] != 0))
+            continue;
+        for (int q = 0; q < 64; ++q)
+        {
+            const uint32_t owner = wave * 64 + q;
+            const uint32_t s     = g0 + owner;
+            if (s >= nseg)
+                break;
+            const Piece P = segs[s];
+            if (!mine(P))
+                continue;
+            const uint32_t d = (P.start == 0) ? (uint32_t) (lane * 4) * 0x01010101u + 0x03020100u
+                                              : start_front_small(state + (size_t) s * 256, sc_t[wave], sc_c[wave], sc_out[wave]);
+            if (lane < NRD)
+                front[lane][owner] = d;
+        }
         __syncthreads();
         const bool act = s_len[t] != 0;
-        if (mode == 4)
-        {
-            uint32_t R[4];
+        uint32_t   R[NRD];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                R[k] = act ? front[k][t] : 0xFFFFFFFFu;
-            mtf_code_rounds<4, true>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[4], uint32_t a) { return mtf_step_pos<4>(T, a); });
-        }
-        else if (mode == 8)
-        {
-            uint32_t R[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                R[k] = act ? front[k][t] : 0xFFFFFFFFu;
-            mtf_code_rounds<8, true>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[8], uint32_t a) { return mtf_step_pos<8>(T, a); });
-        }
-        else
-        {
-            uint32_t R[NRD];
-#pragma unroll
-            for (int k = 0; k < NRD; ++k)
-                R[k] = act ? front[k][t] : 0u;
-            mtf_code_rounds<NRD, false>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[NRD], uint32_t c) { return mtf_step_reg(T, c); });
-        }
+        for (int k = 0; k < NRD; ++k)
+            R[k] = act ? front[k][t] : 0u;
+        mtf_code_rounds<NRD, false>(in, out, R, io, s_off, s_len, nullptr, [](uint32_t (&T)[NRD], uint32_t c) { return mtf_step_reg(T, c); });
         __syncthreads();
     }
 }
@@ -1098,7 +1259,8 @@ __global__ void __launch_bounds__(TPB) k_mtf_dec_relabel(const uint8_t* __restri
 
 }  // namespace
 
-bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s)
+bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, const BlockDesc* h_blocks, uint32_t nblocks, hipStream_t s,
+                       const uint32_t* d_amask)
 {
     if (!w.tiling.build(h_blocks, nblocks, MTF_SEG_ENC, s))
         return false;
@@ -1108,18 +1270,69 @@ bool mtf_encode_device(MtfWorkspace& w, const uint8_t* d_in, uint8_t* d_out, con
     int32_t* st = reinterpret_cast<int32_t*>(w.state);
     {
         BRA_PROF(P_MTF_LASTOCC, s);
-        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st);
+        if (!d_amask)
+        {
+            BRA_HIP_CHECK(hipMemsetAsync(w.amask, 0, (size_t) nblocks * 32, s));
+            hipLaunchKernelGGL(k_mtf_presence, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg,
+                               w.amask);
+            d_amask = w.amask;
+        }
+        hipLaunchKernelGGL(k_mtf_alpha, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, d_amask, nblocks, w.nsym, w.amap, w.ainv, w.amode);
+        hipLaunchKernelGGL(k_mtf_lastocc, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, w.tiling.d_pieces, nseg, st,
+                           w.amode, w.nsym, w.ainv);
+    }
+    if (w.pt_key != w.tiling.h_count)
+    {
+        // chunk geometry of the position-table passes (host-built once per geometry)
+        std::vector<uint32_t> c0(nblocks), cb;
+        for (uint32_t b = 0; b < nblocks; ++b)
+        {
+            c0[b] = (uint32_t) cb.size();
+            cb.insert(cb.end(), div_up(2ull * w.tiling.h_count[b], PT_CHUNK), b);
+        }
+        const uint32_t nc = (uint32_t) cb.size();
+        w.pt_key.clear();
+        if (nblocks > w.pt_cap_b)
+        {
+            w.pt_cap_b = 0;
+            if (!dev_alloc(w.pt_chunk0, (uint64_t) nblocks + 64))
+                return false;
+            w.pt_cap_b = nblocks + 64;
+        }
+        if (nc + 1 > w.pt_cap_c)
+        {
+            w.pt_cap_c = 0;
+            if (!dev_alloc(w.pt_chunk_blk, (uint64_t) nc + 64) || !dev_alloc(w.pt_cmax, 32ull * (nc + 64)))
+                return false;
+            w.pt_cap_c = nc + 64;
+        }
+        BRA_HIP_CHECK(hipMemcpyAsync(w.pt_chunk0, c0.data(), (size_t) nblocks * 4, hipMemcpyHostToDevice, s));
+        if (nc)
+            BRA_HIP_CHECK(hipMemcpyAsync(w.pt_chunk_blk, cb.data(), (size_t) nc * 4, hipMemcpyHostToDevice, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));  // host vectors are the copies' sources
+        w.pt_nchunks = nc;
+        w.pt_key     = w.tiling.h_count;
     }
     {
         BRA_PROF(P_MTF_SCAN, s);
         hipLaunchKernelGGL(k_mtf_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count,
-                           nblocks, st, w.nsym, w.amap, w.amode);
+                           nblocks, st, w.nsym, w.ainv, w.amode);
+        const PtGeo    g{w.tiling.d_first, w.tiling.d_count, w.pt_chunk0, w.pt_chunk_blk, w.pt_nchunks};
+        const uint32_t gc = std::max<uint32_t>(1, std::min<uint32_t>(div_up(w.pt_nchunks, TPB / 32), 16384));
+        hipLaunchKernelGGL(k_mtf_pt_max, dim3(gc), dim3(TPB), 0, s, st, g, w.amode, w.pt_cmax);
+        hipLaunchKernelGGL(k_mtf_pt_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, g, nblocks, w.amode, w.pt_cmax);
+        hipLaunchKernelGGL(k_mtf_pt_tables, dim3(gc), dim3(TPB), 0, s, st, g, w.amode, w.nsym, w.ainv, w.pt_cmax);
     }
     {
         BRA_PROF(P_MTF_ENCODE, s);
-        // every segment goes to exactly one of the two kernels (by its block's distinct symbols)
+        // every segment goes to exactly one of the three kernels (by its block's alphabet)
+        uint32_t maxc = 0;
+        for (uint32_t c : w.tiling.h_count)
+            maxc = std::max(maxc, c);
+        hipLaunchKernelGGL(k_mtf_encode_pos, dim3(div_up(2ull * maxc, TPB), std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, d_in, d_out,
+                           w.tiling.d_pieces, w.tiling.d_first, w.tiling.d_count, nblocks, st, w.amap, w.amode);
         hipLaunchKernelGGL(k_mtf_encode_reg, dim3(std::min<uint32_t>(div_up(nseg, TPB), 4096)), dim3(TPB), 0, s, d_in, d_out,
-                           w.tiling.d_pieces, nseg, st, w.nsym, w.amap, w.amode);
+                           w.tiling.d_pieces, nseg, st, w.nsym, w.amode);
         hipLaunchKernelGGL(k_mtf_encode_wave, dim3(std::min<uint32_t>(div_up(nseg, TPB / 64), 16384)), dim3(TPB), 0, s, d_in, d_out,
                            w.tiling.d_pieces, nseg, st, w.nsym);
     }
