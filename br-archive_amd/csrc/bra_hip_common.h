@@ -407,15 +407,17 @@ __device__ __forceinline__ void cx64_pair(uint32_t& a0, uint32_t& a1, uint32_t& 
 // VALU operations as DPP source modifiers: 2 subtractions and 2 selects read the partner's dwords
 // directly (4 VALU against 6 with separate DPP moves).  A select with a DPP operand takes it as
 // src0, so VCC is inverted (set = keep the own key): the lanes whose (k > o) equals their bit of
-// `keep_min` take o, as in cx64.  The leading s_nop covers the VALU-write -> DPP-read hazard of the
-// previous stage (the hazard recognizer does not look into inline assembly).
+// `keep_min` take o, as in cx64.  The s_nops cover the VALU-write -> DPP-read hazards on both sides
+// (the previous stage's writes; a compiler DPP reading k0 / k1 right after the block -- the hazard
+// recognizer does not look into inline assembly).
 #define BRA_DPP_CX64(CTL)                                                                                \
     asm volatile("s_nop 1\n\t"                                                                            \
                  "v_sub_co_u32_dpp %[t], vcc, %[k0], %[k0] " CTL "\n\t"                                  \
                  "v_subb_co_u32_dpp %[t], vcc, %[k1], %[k1], vcc " CTL "\n\t"                            \
                  "s_xor_b64 vcc, vcc, %[km]\n\t"                                                         \
                  "v_cndmask_b32_dpp %[k0], %[k0], %[k0], vcc " CTL "\n\t"                                \
-                 "v_cndmask_b32_dpp %[k1], %[k1], %[k1], vcc " CTL                                        \
+                 "v_cndmask_b32_dpp %[k1], %[k1], %[k1], vcc " CTL "\n\t"                                \
+                 "s_nop 1"                                                                               \
                  : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1)                                           \
                  : [km] "s"(keep_min)                                                                   \
                  : "vcc")

@@ -611,37 +611,43 @@ template <int NP>
 __device__ __forceinline__ uint32_t mtf_step_pos(uint32_t (&R)[NP], uint32_t a)
 {
     const uint32_t q = a >> 2;
-    // the table dwords as opaque scalar values: a select tree over loads of one array became a
-    // dynamically indexed array (the table in scratch memory)
+    // The table dwords as opaque scalar values, used for the select AND the update (so the barrier
+    // costs no copies): a select tree over loads of one array became a dynamically indexed array
+    // (the table in scratch memory).
     const auto op = [](uint32_t v) {
         asm("" : "+v"(v));
         return v;
     };
+    uint32_t v[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+        v[k] = op(R[k]);
     uint32_t x;
     if constexpr (NP == 8)
     {
-        const uint32_t r0 = op(R[0]), r1 = op(R[1]), r2 = op(R[2]), r3 = op(R[3]), r4 = op(R[4]), r5 = op(R[5]), r6 = op(R[6]), r7 = op(R[7]);
-        const uint32_t x0 = (q & 1) ? r1 : r0, x1 = (q & 1) ? r3 : r2, x2 = (q & 1) ? r5 : r4, x3 = (q & 1) ? r7 : r6;
+        const uint32_t x0 = (q & 1) ? v[1] : v[0], x1 = (q & 1) ? v[3] : v[2], x2 = (q & 1) ? v[5] : v[4], x3 = (q & 1) ? v[7] : v[6];
         const uint32_t y0 = (q & 2) ? x1 : x0, y1 = (q & 2) ? x3 : x2;
         x = (q & 4) ? y1 : y0;
     }
     else
     {
         static_assert(NP == 4, "4 or 8 table dwords");
-        const uint32_t r0 = op(R[0]), r1 = op(R[1]), r2 = op(R[2]), r3 = op(R[3]);
-        const uint32_t x0 = (q & 1) ? r1 : r0, x1 = (q & 1) ? r3 : r2;
+        const uint32_t x0 = (q & 1) ? v[1] : v[0], x1 = (q & 1) ? v[3] : v[2];
         x = (q & 2) ? x1 : x0;
     }
     const uint32_t sh = (a & 3u) << 3;
     const uint32_t r  = (x >> sh) & 0x7Fu;
-    const uint32_t rr = r * 0x01010101u;
+    const uint32_t rr = __builtin_amdgcn_perm(0u, r, 0x00000000u);  // r in every byte
     const uint32_t dl = r << sh;
 #pragma unroll
     for (int k = 0; k < NP; ++k)
     {
-        const uint32_t lt = ~(R[k] - rr) & 0x80808080u;  // bytes whose position is below r
-        const uint32_t nv = R[k] + (lt >> 7);
-        R[k]              = ((uint32_t) k == q) ? nv - dl : nv;
+        // bit 7 of byte (0x80 | p) - r is clear iff p < r: those positions move up by one
+        const uint32_t ge = (v[k] - rr) >> 7;
+        uint32_t       inc;  // ~ge & 0x01010101 in one v_bfi (the compiler emits a not and an and)
+        asm("v_bfi_b32 %0, %1, 0, %2" : "=v"(inc) : "v"(ge), "s"(0x01010101u));
+        const uint32_t nv  = v[k] + inc;
+        R[k]               = ((uint32_t) k == q) ? nv - dl : nv;
     }
     return r;
 }
@@ -704,20 +710,23 @@ __device__ __forceinline__ void mtf_code_rounds(const uint8_t* __restrict__ in, 
                     m[k >> 2] |= (uint32_t) map_s[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu] << (8 * (k & 3));
                 cur = make_uint4(m[0], m[1], m[2], m[3]);
             }
-            // 16 symbols shifted out of a 128-bit register pair, ranks shifted in (a rolled
-            // loop: 16 inlined steps cost 2x the registers for nothing, the steps are serial)
-            uint64_t ilo = ((uint64_t) cur.y << 32) | cur.x, ihi = ((uint64_t) cur.w << 32) | cur.z;
-            uint64_t olo = 0, ohi = 0;
+            // 16 symbols, a dword (4 steps, constant byte positions) per iteration of a rolled loop
+            // over a 4-dword queue (16 inlined steps cost 2x the registers for nothing, the steps
+            // are serial; a 128-bit shift register cost 8 VALU of shifts per symbol)
+            uint32_t q0 = cur.x, q1 = cur.y, q2 = cur.z, q3 = cur.w, o0 = 0, o1 = 0, o2 = 0, o3 = 0;
 #pragma unroll 1
-            for (int j = 0; j < 16; ++j)
+            for (int j = 0; j < 4; ++j)
             {
-                const uint32_t rk = step(R, (uint32_t) ilo & 0xFFu);
-                ilo               = (ilo >> 8) | (ihi << 56);
-                ihi >>= 8;
-                olo = (olo >> 8) | (ohi << 56);
-                ohi = (ohi >> 8) | ((uint64_t) rk << 56);
+                const uint32_t w  = q0;
+                const uint32_t k0 = step(R, w & 0xFFu);
+                const uint32_t k1 = step(R, (w >> 8) & 0xFFu);
+                const uint32_t k2 = step(R, (w >> 16) & 0xFFu);
+                const uint32_t k3 = step(R, w >> 24);
+                q0 = q1, q1 = q2, q2 = q3;
+                o0 = o1, o1 = o2, o2 = o3;
+                o3 = k0 | (k1 << 8) | (k2 << 16) | (k3 << 24);
             }
-            io[c][t] = make_uint4((uint32_t) olo, (uint32_t) (olo >> 32), (uint32_t) ohi, (uint32_t) (ohi >> 32));
+            io[c][t] = make_uint4(o0, o1, o2, o3);
         }
         __syncthreads();
 #pragma unroll

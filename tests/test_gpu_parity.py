@@ -120,6 +120,22 @@ def test_golden_stages(bra, golden):
 
 
 # ---- batched device path vs the oracle ----------------------------------------------------------
+def _stage_diagnosis(codec, orc, blk: bytes, lo: int, hi: int, total: int) -> str:
+    """Which stage of the last batch encode first differs from the oracle for one block (the BWT
+    output, then the MTF output computed from the GPU's own BWT output), with the first offsets."""
+    L = codec.stage_copy(0, total)[lo:hi]
+    ref_L = np.frombuffer(orc.bwt_encode(blk)[0], np.uint8)
+    bad = np.flatnonzero(L != ref_L)
+    if bad.size:
+        return f"BWT output differs at {bad.size} bytes (first {bad[:4].tolist()})"
+    M = codec.stage_copy(1, total)[lo:hi]
+    ref_M = np.frombuffer(orc.mtf_encode(L.tobytes()), np.uint8)
+    bad = np.flatnonzero(M != ref_M)
+    if bad.size:
+        return f"BWT ok; MTF output differs at {bad.size} bytes (first {bad[:4].tolist()})"
+    return "BWT and MTF outputs ok (RLE or Huffman differs)"
+
+
 def _encode_check(bra, codec, orc, data: np.ndarray, block_size: int, check_blocks=None, roundtrip=True):
     import torch
 
@@ -137,15 +153,11 @@ def _encode_check(bra, codec, orc, data: np.ndarray, block_size: int, check_bloc
         blk = data[lo:hi].tobytes()
         ch = orc.encode_block(blk)
         pi, lens, osz, esz = bra.parse_header(hdr_h[b].tobytes())
-        if pi != ch.primary_index:
-            L = codec.stage_copy(0, total)[lo:hi]
-            ref_L = np.frombuffer(orc.bwt_encode(blk)[0], np.uint8)
-            nbad = int((L != ref_L).sum())
-            raise AssertionError(f"pi block {b}: gpu {pi} ref {ch.primary_index}; L mismatches {nbad}")
-        assert lens == ch.lengths, ("lengths", b)
-        assert (osz, esz) == (ch.orig_size, ch.encoded_size), ("sizes", b)
-        assert int(off_h[b + 1] - off_h[b]) == esz, ("offset", b)
-        assert pay_h[off_h[b]: off_h[b] + esz].tobytes() == ch.payload, ("payload", b)
+        ok = (pi == ch.primary_index and lens == ch.lengths and (osz, esz) == (ch.orig_size, ch.encoded_size)
+              and int(off_h[b + 1] - off_h[b]) == esz and pay_h[off_h[b]: off_h[b] + esz].tobytes() == ch.payload)
+        if not ok:
+            raise AssertionError(f"block {b}: {_stage_diagnosis(codec, orc, blk, lo, hi, total)}; "
+                                 f"gpu pi {pi} sizes {(osz, esz)}, reference pi {ch.primary_index} sizes {(ch.orig_size, ch.encoded_size)}")
     if roundtrip:
         out = codec.decode(hdr, off, pay, total, block_size)
         torch.cuda.synchronize()
@@ -231,6 +243,29 @@ def test_batch_duplicated_regions(bra, codec, orc, bs, x):
     rng = np.random.default_rng(bs + x)
     text = bra.synth_fill(0, bs, bs, first_block=5)
     _encode_check(bra, codec, orc, _dup_blocks(rng, bs, x, text), bs)
+
+
+def test_batch_encode_is_deterministic(bra, codec):
+    """The same batch (text, random, duplicated regions, small alphabets) encoded 4 times gives the
+    same bytes every time: no result may depend on the order in which waves or workgroups ran."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    bs = 1 << 18
+    text = bra.synth_fill(0, 4 * bs, bs, first_block=9)
+    vals = np.arange(40, 60, dtype=np.uint8)
+    data = np.concatenate([text, _dup_blocks(rng, bs, 32 << 10, text), rng.integers(0, 256, 2 * bs, dtype=np.uint8).astype(np.uint8),
+                           vals[rng.integers(0, vals.size, 2 * bs)]])
+    d = torch.from_numpy(data).cuda()
+    first = None
+    for _ in range(4):
+        hdr, off, pay = codec.encode(d, bs)
+        torch.cuda.synchronize()
+        n = int(off[-1].item())
+        got = (hdr.cpu().numpy().tobytes(), off.cpu().numpy().tobytes(), pay[:n].cpu().numpy().tobytes())
+        if first is None:
+            first = got
+        assert got == first, "encode output changed between runs of the same batch"
 
 
 def _alphabet_block(rng, bs: int, vals: np.ndarray) -> np.ndarray:
