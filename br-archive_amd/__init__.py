@@ -310,7 +310,7 @@ class BlockCodec:
             offsets = torch.empty((nb + 1,), dtype=torch.int64, device=dev)
         if payload is None:
             payload = torch.empty((int(total * 1.25) + 64 * nb + 4096,), dtype=torch.uint8, device=dev)
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_encode_blocks(self.ctx, data.data_ptr(), total, block_size, headers.data_ptr(), offsets.data_ptr(),
                                        payload.data_ptr(), payload.numel(), s)
         if rc == -2:
@@ -327,7 +327,7 @@ class BlockCodec:
 
         if out is None:
             out = torch.empty((total,), dtype=torch.uint8, device=headers.device)
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_decode_blocks(self.ctx, headers.data_ptr(), offsets.data_ptr(), payload.data_ptr(), total, block_size,
                                        out.data_ptr(), s)
         if rc != 0:
@@ -340,7 +340,7 @@ class BlockCodec:
         import torch
 
         out = torch.empty((1,), dtype=torch.int32, device=data.device)
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         if lib.bra_gpu_crc32c(self.ctx, data.data_ptr(), data.numel(), prev, out.data_ptr(), s) != 0:
             raise RuntimeError("bra_gpu_crc32c failed")
         return int(out.item()) & 0xFFFFFFFF
@@ -350,7 +350,7 @@ class BlockCodec:
         import torch
 
         out = torch.empty((1,), dtype=torch.int32, device=data.device)
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         if lib.bra_gpu_chunks_crc32c(self.ctx, data.data_ptr(), data.numel(), block_size, headers.data_ptr(), prev, out.data_ptr(), s) != 0:
             raise RuntimeError("bra_gpu_chunks_crc32c failed")
         return int(out.item()) & 0xFFFFFFFF
@@ -364,7 +364,7 @@ class BlockCodec:
         if out is None:
             out = torch.empty((max(need, 1),), dtype=torch.uint8, device=headers.device)
         size = C.c_uint64()
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_frame_chunks(self.ctx, headers.data_ptr(), offsets.data_ptr(), payload.data_ptr(), nb, out.data_ptr(), out.numel(),
                                       C.byref(size), s)
         if rc != 0:
@@ -380,7 +380,7 @@ class BlockCodec:
         hdr = torch.empty((max(cap, 1), HEADER_BYTES), dtype=torch.uint8, device=stream_t.device)
         off = torch.empty((cap + 1,), dtype=torch.int64, device=stream_t.device)
         n = C.c_uint32()
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_unframe_chunks(self.ctx, stream_t.data_ptr(), size, cap, hdr.data_ptr(), off.data_ptr(), C.byref(n), s)
         if rc != 0:
             raise ValueError(f"bra_gpu_unframe_chunks rejected the stream ({rc}, {n.value} records)")
@@ -395,7 +395,7 @@ class BlockCodec:
         if out is None or out.numel() < cap:
             out = torch.empty((cap,), dtype=torch.uint8, device=data.device)
         size, crc = C.c_uint64(), C.c_uint32()
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_compress_chunks(self.ctx, data.data_ptr(), total, block_size, out.data_ptr(), out.numel(), C.byref(size), C.byref(crc), s)
         if rc < 0:
             raise RuntimeError(f"bra_gpu_compress_chunks failed ({rc})")
@@ -410,7 +410,7 @@ class BlockCodec:
             out_cap = (size // 268 + 1) * block_size
         out = torch.empty((max(out_cap, 1),), dtype=torch.uint8, device=stream_t.device)
         osz, crc = C.c_uint64(), C.c_uint32()
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_decompress_chunks(self.ctx, stream_t.data_ptr(), size, block_size, out.data_ptr(), out_cap, C.byref(osz), prev_crc,
                                            C.byref(crc), s)
         if rc != 0:
@@ -426,7 +426,7 @@ class BlockCodec:
 
         if out is None:
             out = torch.empty((1,), dtype=torch.int32, device=data.device)
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_chunks_crc32c_shard(self.ctx, data.data_ptr(), data.numel(), block_size, headers.data_ptr(), first_chunk,
                                              chunk_stride, global_total, prev, 1 if with_init else 0, out.data_ptr(), s)
         if rc != 0:
@@ -454,7 +454,7 @@ class BlockCodec:
         op = arr(*[o.data_ptr() for _, o, _ in parts])
         pp = arr(*[p.data_ptr() for _, _, p in parts])
         nn = (C.c_uint32 * P)(*nbs)
-        s = stream.cuda_stream if stream is not None else None
+        s = _stream_handle(stream)
         rc = lib.bra_gpu_assemble_shards(self.ctx, P, hp, op, pp, nn, 1 if round_robin else 0, headers.data_ptr(), offsets.data_ptr(),
                                          payload.data_ptr(), payload.numel(), s)
         if rc != 0:
@@ -510,6 +510,16 @@ class BlockCodec:
         if rc != 0:
             raise RuntimeError(f"hipMemcpy failed ({rc})")
         return out
+
+
+def _stream_handle(stream):
+    """The HIP stream a call runs on: the given torch stream, else torch's current stream -- so that
+    a call without a stream is ordered with the torch work around it (allocations, copies, reads of
+    the results); the context's own stream is not, and a caller reading a result tensor on torch's
+    stream could see it before the call's last kernels had written it."""
+    import torch
+
+    return (stream if stream is not None else torch.cuda.current_stream()).cuda_stream
 
 
 def parse_header(h: bytes):

@@ -403,41 +403,10 @@ __device__ __forceinline__ void cx64_pair(uint32_t& a0, uint32_t& a1, uint32_t& 
     b0 = m0, b1 = m1;
 }
 
-// cx64 against the partner lane (lane ^ LM, LM = 1, 2 or 8) with the lane exchange folded into the
-// VALU operations as DPP source modifiers: 2 subtractions and 2 selects read the partner's dwords
-// directly (4 VALU against 6 with separate DPP moves).  A select with a DPP operand takes it as
-// src0, so VCC is inverted (set = keep the own key): the lanes whose (k > o) equals their bit of
-// `keep_min` take o, as in cx64.  The s_nops cover the VALU-write -> DPP-read hazards on both sides
-// (the previous stage's writes; a compiler DPP reading k0 / k1 right after the block -- the hazard
-// recognizer does not look into inline assembly).
-#define BRA_DPP_CX64(CTL)                                                                                \
-    asm volatile("s_nop 1\n\t"                                                                            \
-                 "v_sub_co_u32_dpp %[t], vcc, %[k0], %[k0] " CTL "\n\t"                                  \
-                 "v_subb_co_u32_dpp %[t], vcc, %[k1], %[k1], vcc " CTL "\n\t"                            \
-                 "s_xor_b64 vcc, vcc, %[km]\n\t"                                                         \
-                 "v_cndmask_b32_dpp %[k0], %[k0], %[k0], vcc " CTL "\n\t"                                \
-                 "v_cndmask_b32_dpp %[k1], %[k1], %[k1], vcc " CTL "\n\t"                                \
-                 "s_nop 1"                                                                               \
-                 : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1)                                           \
-                 : [km] "s"(keep_min)                                                                   \
-                 : "vcc")
-
-template <int LM>
-__device__ __forceinline__ void cx64_dpp(uint32_t& k0, uint32_t& k1, uint64_t keep_min)
-{
-    uint32_t t;
-    if constexpr (LM == 1)
-        BRA_DPP_CX64("quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf");
-    else if constexpr (LM == 2)
-        BRA_DPP_CX64("quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf");
-    else
-    {
-        static_assert(LM == 8, "DPP lane distances 1, 2, 8");
-        BRA_DPP_CX64("row_ror:8 row_mask:0xf bank_mask:0xf");
-    }
-}
-#undef BRA_DPP_CX64
-
+// (Folding the lane exchange into the compare-exchange as DPP source operands -- v_sub_co / v_subb_co /
+// v_cndmask with a DPP src0, 4 VALU instead of 6 -- sorted wrongly now and then: one 8 MiB sym16
+// block of 32 differed from the reference in 4 of 6 identical runs, with s_nops around the block
+// or not; the separate DPP moves stay.)
 template <int LM>
 __device__ __forceinline__ uint64_t xlane64(uint64_t x)
 {

@@ -1687,13 +1687,6 @@ __device__ __forceinline__ void cxk_pair(uint32_t (&a)[KD], uint32_t (&b)[KD], u
 template <int LM, int KD>
 __device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[KD][4], uint64_t keep_min)
 {
-    if constexpr (KD == 2 && LM != 4)
-    {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            cx64_dpp<LM>(k[0][r], k[1][r], keep_min);
-        return;
-    }
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
