@@ -229,18 +229,22 @@ __device__ __forceinline__ uint64_t pk_load64(const uint8_t* __restrict__ pk, ui
     return sh ? (hi << sh) | ((uint64_t) p[8] >> (8 - sh)) : hi;
 }
 
-// STRING-mode payload (64 bits): the rotation index in bits 0-23 and CARRY digits, virtual bytes
-// [kd, kd + CARRY) of the rotation, big-endian in bits 24-63.  A bucket at depth d reads digit
+// STRING-mode payload (64 bits): the rotation index in bits 0-23, the rotation's BWT output byte
+// (the input byte before it, cyclically) in bits 24-31, and CARRY digits, virtual bytes
+// [kd, kd + CARRY) of the rotation, big-endian in bits 32-63.  A bucket at depth d reads digit
 // d - kd; the scatter that moves an element into a bucket at depth kd + CARRY gathers the next
 // CARRY digits (one 64-bit packed load), so an element costs one gather per CARRY MSD levels.
-constexpr uint32_t CARRY = 5;
+// The output byte rides along from level 0 (read there from the tile's input bytes), so the job
+// that finally places the rotation needs no gather for it (5 carried digits without it cost one
+// more random byte load per element in the jobs than 4 digits cost in extra MSD re-gathers).
+constexpr uint32_t CARRY = 4;
 __device__ __forceinline__ uint32_t p_idx(uint64_t P) { return (uint32_t) P & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t p_digit(uint64_t P, uint32_t j) { return (uint32_t) (P >> (56 - 8 * j)) & 0xFFu; }
-// payload carrying virtual bytes [vd, vd + CARRY) of rotation idx
-__device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ pk, uint32_t b, uint32_t nbits, uint32_t vd, uint32_t idx)
+// payload P re-carrying virtual bytes [vd, vd + CARRY) of its rotation (index and output byte kept)
+__device__ __forceinline__ uint64_t p_make(const uint8_t* __restrict__ pk, uint32_t b, uint32_t nbits, uint32_t vd, uint64_t P)
 {
-    const uint64_t k = pk_load64(pk, pk_bitpos(b, nbits, idx, vd));
-    return (k & 0xFFFFFFFFFF000000ull) | idx;
+    const uint64_t k = pk_load64(pk, pk_bitpos(b, nbits, p_idx(P), vd));
+    return (k & 0xFFFFFFFF00000000ull) | (P & 0xFFFFFFFFull);
 }
 
 // Counters of one call: slot 0 holds the call-wide lists (jobs, workgroup jobs, fallback groups,
@@ -1216,8 +1220,10 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
     }
 }
 
-// Level 0: every element gets its payload carrying virtual bytes 1..CARRY (the next digits).
-__global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ packed, const BlockDesc* __restrict__ blocks,
+// Level 0: every element gets its payload carrying virtual bytes 1..CARRY (the next digits) and its
+// BWT output byte.
+__global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ in, const uint32_t* __restrict__ amask,
+                                                    const uint8_t* __restrict__ packed, const BlockDesc* __restrict__ blocks,
                                                     const PackDesc* __restrict__ pkd, const L0Tile* __restrict__ tiles, uint32_t ntiles,
                                                     const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay,
                                                     uint8_t* __restrict__ odig)
@@ -1225,6 +1231,8 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
     uint8_t*     win = reinterpret_cast<uint8_t*>(smem + sizeof(TileStageL0));  // TILE + 48 bytes, 16-aligned
+    __shared__ uint8_t  inv_s[256];
+    __shared__ uint32_t prev_s;
     // XCD-major tile order: workgroup w runs on XCD w % 8 and takes tiles from the XCD's contiguous
     // eighth of the list, so the neighbouring output runs that adjacent tiles write to one digit's
     // sub-bucket meet in the same L2 (in list order they went to eight different L2s and reached
@@ -1242,6 +1250,18 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
         load_window(packed + P.poff, T.start, cnt, P.b, win);
         stage_zero(S);
         S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x] & ~NEXT_FLAG;
+        {
+            // alphabet rank -> byte value (the packing's map, inverted): thread v = byte value v
+            const uint32_t  vv = threadIdx.x;
+            const uint32_t* m  = amask + 8 * T.block;
+            uint32_t        r  = __popc(m[vv >> 5] & ((1u << (vv & 31)) - 1u));
+            for (uint32_t k = 0; k < (vv >> 5); ++k)
+                r += __popc(m[k]);
+            if ((m[vv >> 5] >> (vv & 31)) & 1u)
+                inv_s[r] = (uint8_t) vv;
+            if (threadIdx.x == 0)
+                prev_s = in[B.off + (T.start ? T.start - 1 : B.len - 1)];
+        }
         __syncthreads();
         uint32_t v[PER_THREAD], dg[PER_THREAD];
 #pragma unroll
@@ -1262,9 +1282,13 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                 const uint32_t dd   = vv >> 24, e = vv & 0xFFFFFFu;
                 const uint32_t slot = S.goff[dd] + (q - S.base[dd]);
                 const uint64_t kk   = win_bits64(win, e * P.b);  // virtual bytes 0..7: keep bytes 1..CARRY
+                const uint32_t pos  = T.start + e;
+                // the output byte: the character before the element in the packed window, mapped
+                // back from its alphabet rank (the tile's first element: the byte read ahead)
+                const uint32_t lb = e ? inv_s[(uint32_t) (win_bits64(win, (e - 1) * P.b) >> (64 - P.b))] : prev_s;
                 if (BRA_DCHECK(slot >= B.off && slot < B.off + B.len, "l0 scatter slot %u outside block %u", slot, T.block))
                 {
-                    opay[slot] = ((kk << 8) & 0xFFFFFFFFFF000000ull) | (T.start + e);
+                    opay[slot] = ((kk << 8) & 0xFFFFFFFF00000000ull) | ((uint64_t) lb << 24) | pos;
                     odig[slot] = (uint8_t) (kk >> 48);  // virtual byte 1: the level-1 digit
                 }
             }
@@ -1324,8 +1348,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                 const uint32_t e = threadIdx.x + i * TPB;
                 if (e < cnt)
                 {
-                    const uint32_t idx = p_idx(v[i]);
-                    const uint64_t np  = p_make(pk, D.pb, D.nbits, dn, idx);
+                    const uint64_t np = p_make(pk, D.pb, D.nbits, dn, v[i]);
                     ip[e]             = np;
                     id[e]             = (uint8_t) p_digit(np, 0);
                 }
@@ -1361,7 +1384,7 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                 uint64_t       nv   = vv;
                 if (rg && (g & NEXT_FLAG))
                 {
-                    nv = p_make(pk, D.pb, D.nbits, dn, p_idx(vv));
+                    nv = p_make(pk, D.pb, D.nbits, dn, vv);
                 }
                 if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
                 {
@@ -2078,7 +2101,6 @@ template <int W>
 __device__ __forceinline__ void job_gather1(const JobArgs& a, const Job& J, const BlockDesc& BD, const PackDesc& PK, const uint32_t (&pay)[4],
                                             int wj, JobPre& p)
 {
-    const uint8_t* blk    = a.in + BD.off;
     const uint8_t* pkb    = a.packed + PK.poff;
     const bool     single = W > 1 || J.kd == 1u;  // one shared sub-bucket: the key starts at byte d
     const uint32_t vd     = single ? J.d : J.d - 1;
@@ -2090,12 +2112,11 @@ __device__ __forceinline__ void job_gather1(const JobArgs& a, const Job& J, cons
         p.w0[r] = p.w1[r] = 0;
         if (c < J.len)
         {
-            uint32_t idx = pay[r] & 0xFFFFFFu;
-            if (!BRA_DCHECK(idx < BD.len, "job payload idx %u >= n %u (buf %u slot %u)", idx, BD.len, J.buf, J.start + c))
-                idx = 0;
-            const uint8_t lb = blk[idx ? idx - 1 : BD.len - 1];
-            pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, idx, vd), p.w0[r], p.w1[r]);
-            p.v[r] = ((uint32_t) lb << 24) | idx;
+            uint32_t v = pay[r];  // output byte << 24 | rotation (the payload's low word)
+            if (!BRA_DCHECK((v & 0xFFFFFFu) < BD.len, "job payload idx %u >= n %u (buf %u slot %u)", v & 0xFFFFFFu, BD.len, J.buf, J.start + c))
+                v = 0;
+            pk_load128(pkb, pk_bitpos(PK.b, PK.nbits, v & 0xFFFFFFu, vd), p.w0[r], p.w1[r]);
+            p.v[r] = v;
         }
     }
 }
@@ -2105,7 +2126,6 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
 {
     using G                 = JobGeom<W>;
     const int       lane    = lane_id();
-    const uint8_t*  blk     = a.in + BD.off;  // raw bytes: the BWT output byte of a rotation
     const uint8_t*  pkb     = a.packed + PK.poff;
     const uint64_t* K       = J.buf ? a.key1 : a.key0;
     const uint32_t* V       = J.buf ? a.pay1 : a.pay0;
@@ -3370,7 +3390,7 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
-        hipLaunchKernelGGL(k_l0_scatter, dim3(nt0 >= 8 ? std::min<uint32_t>(nt0, grid) & ~7u : nt0), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, w.packed, d_blocks,
+        hipLaunchKernelGGL(k_l0_scatter, dim3(nt0 >= 8 ? std::min<uint32_t>(nt0, grid) & ~7u : nt0), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, d_in, w.amask, w.packed, d_blocks,
                            w.pkd, w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
