@@ -201,8 +201,10 @@ __device__ __forceinline__ uint32_t pk_bitpos(uint32_t b, uint32_t nbits, uint32
     return bp;
 }
 
-// 128 bits of a packed string from bit bp: w0 = bits [bp, bp + 64), w1 = the next 64 (one 16-byte
-// load and one byte: the same latency as 64 bits)
+// 128 bits of a packed string from bit bp: w0 = bits [bp, bp + 64), w1 = the next 64 except its
+// lowest bp % 8 bits (zero): one unaligned 16-byte load.  The consumers use at most the top 56
+// bits of w1 (the round-2 key bits of a job), so the byte after the 16 is not loaded (that second
+// load per element cost as much as the first in the job kernels' memory requests).
 __device__ __forceinline__ void pk_load128(const uint8_t* __restrict__ pk, uint32_t bp, uint64_t& w0, uint64_t& w1)
 {
     const uint8_t* p  = pk + (bp >> 3);
@@ -212,21 +214,19 @@ __device__ __forceinline__ void pk_load128(const uint8_t* __restrict__ pk, uint3
     const uint32_t sh = bp & 7;
     if (sh)
     {
-        const uint64_t e = p[16];
-        a                = (a << sh) | (c >> (64 - sh));
-        c                = (c << sh) | (e >> (8 - sh));
+        a = (a << sh) | (c >> (64 - sh));
+        c <<= sh;
     }
     w0 = a;
     w1 = c;
 }
 
-// 64 bits of a packed string from bit bp (bit bp in the MSB)
+// 64 bits of a packed string from bit bp (bit bp in the MSB), except the lowest bp % 8 bits (zero):
+// one unaligned 8-byte load.  The consumers use the top 48 (job keys) or 32 (MSD payload digits).
 __device__ __forceinline__ uint64_t pk_load64(const uint8_t* __restrict__ pk, uint32_t bp)
 {
-    const uint8_t* p  = pk + (bp >> 3);
-    const uint64_t hi = __builtin_bswap64(*reinterpret_cast<const u64_unaligned*>(p));
-    const uint32_t sh = bp & 7;
-    return sh ? (hi << sh) | ((uint64_t) p[8] >> (8 - sh)) : hi;
+    const uint8_t* p = pk + (bp >> 3);
+    return __builtin_bswap64(*reinterpret_cast<const u64_unaligned*>(p)) << (bp & 7);
 }
 
 // STRING-mode payload (64 bits): the rotation index in bits 0-23, the rotation's BWT output byte
