@@ -250,10 +250,12 @@ def main():
             if world > 1:
                 parts = gather(hdr, off, pay, crc_share)
             else:
-                parts = [(hdr, off, pay[: int(off[nb].item())], crc_share)]
+                parts = [(hdr, off, pay, crc_share)]  # the payload's capacity: no host read of its size
             if rank == 0:
+                # assembled on the stream and the CRC shares merged on the device: a step has no host
+                # wait of its own (world 1), so the host queues the next step while this one runs
                 result["stream"] = dmod.assemble(codec, parts, round_robin=True)
-                result["crc"] = dmod.merge_crc(parts)
+                result["crc_t"] = dmod.merge_crc_device(parts)
 
     # ---- find the dominant kernel (one untimed, fully profiled pass) ----
     kernel_slots = [s for s in codec.SLOTS if not s.startswith(("stage.", "dec."))]
@@ -298,6 +300,7 @@ def main():
     line = None
     if rank == 0:
         H, O, P = result["stream"]
+        result["crc"] = int(result["crc_t"].item()) & 0xFFFFFFFF
         off_h = O.cpu().numpy()
         hdr_h = H.cpu().numpy()
         payload_bytes = int(off_h[nbg])

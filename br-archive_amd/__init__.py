@@ -447,7 +447,8 @@ class BlockCodec:
             headers = torch.empty((nb, HEADER_BYTES), dtype=torch.uint8, device=dev)
         if offsets is None:
             offsets = torch.empty((nb + 1,), dtype=torch.int64, device=dev)
-        if payload is None:
+        given = payload is not None
+        if payload is None:  # the parts' payload capacities: the assembly cannot overflow it
             payload = torch.empty((max(total_pay, 1),), dtype=torch.uint8, device=dev)
         arr = C.c_void_p * P
         hp = arr(*[h.data_ptr() for h, _, _ in parts])
@@ -459,6 +460,8 @@ class BlockCodec:
                                          payload.data_ptr(), payload.numel(), s)
         if rc != 0:
             raise RuntimeError(f"bra_gpu_assemble_shards failed ({rc})")
+        if given and int(offsets[nb].item()) == -1:  # the asynchronous call's overflow marker
+            raise RuntimeError("bra_gpu_assemble_shards: payload capacity too small")
         return headers, offsets, payload
 
     def prof_enable(self, mask: int):

@@ -16,6 +16,14 @@ const uint32_t* bwt_alpha_masks(const BwtWorkspace* w);
 // BWT of every block: d_L[off..off+len) = last column, d_pi[b] = primary index (block-local).
 bool bwt_encode_device(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s);
+// The same in two halves: _enqueue queues everything up to the jobs without waiting for them;
+// _finish waits for the jobs' mailbox and, when groups are still tied (periodic or highly repetitive
+// blocks), runs the prefix-doubling fallback, which rewrites those blocks' L and pi on the stream
+// (*fallback_ran tells the caller that work it queued in between read the earlier L).
+bool bwt_encode_enqueue(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
+                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s);
+bool bwt_encode_finish(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
+                       uint8_t* d_L, uint32_t* d_pi, hipStream_t s, bool* fallback_ran);
 
 // BWT of one block of any length >= 1 (bwt_large.hip: prefix doubling with rocPRIM radix sorts), used
 // by the single-block C-ABI for blocks of 2^24 bytes or more; synchronises the stream.

@@ -3289,6 +3289,13 @@ static bool account_levels(BwtWorkspace& w, hipStream_t s)
 bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s)
 {
+    return bwt_encode_enqueue(wp, d_in, d_blocks, h_blocks, nblocks, d_L, d_pi, s) &&
+           bwt_encode_finish(wp, d_in, d_blocks, h_blocks, nblocks, d_L, d_pi, s, nullptr);
+}
+
+bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
+                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s)
+{
     BwtWorkspace& w = *wp;
     uint64_t      N = 0;
     for (uint32_t b = 0; b < nblocks; ++b)
@@ -3426,6 +3433,18 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
             fprintf(stderr, "[bwt levels] slot %u: buckets %u tiles %u elems %u moved(into) %u\n", k, w.h_ctr[k].n_big, w.h_ctr[k].n_tiles_next,
                     w.h_ctr[k].n_elems_next, w.h_ctr[k].n_moved);
     }
+    return true;
+}
+
+bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
+                       uint8_t* d_L, uint32_t* d_pi, hipStream_t s, bool* fallback_ran)
+{
+    BwtWorkspace& w = *wp;
+    uint64_t      N = 0;
+    for (uint32_t b = 0; b < nblocks; ++b)
+        N = std::max<uint64_t>(N, h_blocks[b].off + h_blocks[b].len);
+    if (fallback_ran)
+        *fallback_ran = false;
     Mail mc{};
     if (!post_wait(w, 0, s, mc))
         return false;
@@ -3454,6 +3473,8 @@ bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     uint32_t ng = mc.n_groups;
     if (ng == 0)
         return true;
+    if (fallback_ran)
+        *fallback_ran = true;
     BRA_PROF(P_BWT_FALLBACK, s);
     int gcur = 0;
     hipLaunchKernelGGL(k_group_depth_chars, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pkd);

@@ -297,43 +297,62 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
             return -1;
         c->enc_geo = hb;
     }
+    // The BWT is queued without waiting for its jobs; MTF, RLE and Huffman follow on the stream at
+    // once.  Only then does the host wait for the jobs' mailbox: blocks whose rotations stayed tied
+    // (periodic, highly repetitive) go through the prefix-doubling fallback, which rewrites their
+    // L and pi, and the later stages are queued again.  With a payload capacity above the Huffman
+    // bound (RLE bytes + a word per block) the chain has no other host wait, so the device never
+    // idles while the host catches up.
+    const bool cap_ok = payload_cap >= R + 16ull * nb + 64;
+    uint64_t   total  = 0;
+    const auto later_stages = [&]() -> int {
+        {
+            BRA_PROF(P_STAGE_MTF, s);
+            // the BWT's per-block presence masks are the alphabets of its output too
+            if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s, bwt_alpha_masks(c->bwt)))
+                return -1;
+        }
+        {
+            BRA_PROF(P_STAGE_RLE, s);
+            if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_enc_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
+                return -1;
+        }
+        bool hok = false;
+        {
+            BRA_PROF(P_STAGE_HUF, s);
+            hok = huff_encode_device(c->huf, c->d_rle, rle_blocks.data(), nb, c->d_hist, c->d_rle_size, c->d_meta, d_payload_off, d_payload,
+                                     payload_cap, &total, s, cap_ok);
+        }
+        if (!hok)
+        {
+            if (needed)
+                *needed = total;
+            return total + 8 > payload_cap ? -2 : -1;
+        }
+        hipLaunchKernelGGL(k_headers, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, c->d_pi, c->d_meta, nb, d_headers);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    };
+    bool fallback = false;
     {
         BRA_PROF(P_STAGE_BWT, s);
-        if (!bwt_encode_device(c->bwt, d_in, c->d_enc_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
+        if (!bwt_encode_enqueue(c->bwt, d_in, c->d_enc_blocks, hb.data(), nb, c->d_L, c->d_pi, s))
             return -1;
     }
-    {
-        BRA_PROF(P_STAGE_MTF, s);
-        // the BWT's per-block presence masks are the alphabets of its output too
-        if (!mtf_encode_device(c->mtf, c->d_L, c->d_mtf, hb.data(), nb, s, bwt_alpha_masks(c->bwt)))
-            return -1;
-    }
-    {
-        BRA_PROF(P_STAGE_RLE, s);
-        if (!rle_encode_device(c->rle, c->d_mtf, hb.data(), nb, c->d_enc_rle_base, c->d_rle, c->d_rle_size, c->d_hist, s))
-            return -1;
-    }
-    uint64_t total = 0;
-    bool     hok   = false;
-    {
-        BRA_PROF(P_STAGE_HUF, s);
-        hok = huff_encode_device(c->huf, c->d_rle, rle_blocks.data(), nb, c->d_hist, c->d_rle_size, c->d_meta, d_payload_off, d_payload,
-                                 payload_cap, &total, s);
-    }
-    if (!hok)
-    {
-        if (needed)
-            *needed = total;
-        return total + 8 > payload_cap ? -2 : -1;
-    }
-    hipLaunchKernelGGL(k_headers, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, c->d_pi, c->d_meta, nb, d_headers);
-    if (hipGetLastError() != hipSuccess)
+    int rc = later_stages();
+    // (the fallback, when it runs, is timed by its own slot: one stage scope per call keeps the
+    // stage slots' per-launch averages per step)
+    if (!bwt_encode_finish(c->bwt, d_in, c->d_enc_blocks, hb.data(), nb, c->d_L, c->d_pi, s, &fallback))
         return -1;
+    if (fallback)
+        rc = later_stages();  // L changed
+    if (rc != 0)
+        return rc;
     if (g_prof && g_prof->mask)
     {
         // sizes of the RLE outputs for the byte accounting of rle.write / huf.* (profiling only)
         std::vector<uint32_t> rs(nb);
-        if (hipMemcpyAsync(rs.data(), c->d_rle_size, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        if (hipMemcpyAsync(rs.data(), c->d_rle_size, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(&total, d_payload_off + nb, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
             return -1;
         double Rt = 0;
         for (uint32_t v : rs)
@@ -349,7 +368,12 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
     }
     c->last_nblocks = nb;
     if (needed)
+    {
+        // the caller wants the payload size on the host (the chunk loop frames and sizes its output)
+        if (hipMemcpyAsync(&total, d_payload_off + nb, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+            return -1;
         *needed = total;
+    }
     return 0;
 }
 
@@ -897,6 +921,8 @@ int bra_gpu_assemble_shards(bra_gpu_ctx_t* c, uint32_t nparts, const bra_io_chun
         !assemble_shards_device(P, (uint32_t) nb, reinterpret_cast<uint8_t*>(d_headers_out), d_payload_off_out, d_payload_out, payload_cap,
                                 c->d_word + 3, s))
         return -1;
+    if (stream)
+        return 0;  // asynchronous: an overflow shows as d_payload_off_out[nb] == UINT64_MAX
     uint32_t err = 1;
     if (hipMemcpyAsync(&err, c->d_word + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         return -1;

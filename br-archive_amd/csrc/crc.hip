@@ -364,8 +364,9 @@ __device__ __forceinline__ void shard_src(const ShardParts& P, uint32_t g, uint3
 __device__ __forceinline__ uint32_t hdr_encoded_size(const uint8_t* h) { return rd32(h + CHUNK_HDR_MEM - 4); }
 
 // One workgroup: exclusive scan of the encoded sizes in global block order -> out offsets
-// (nb + 1 entries; the last one is the total payload).
-__global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t nb, uint64_t* __restrict__ off_out)
+// (nb + 1 entries; the last one is the total payload, or UINT64_MAX when it exceeds cap: then the
+// last block is not copied and the caller sees the overflow without a host round trip).
+__global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t nb, uint64_t* __restrict__ off_out, uint64_t cap)
 {
     __shared__ uint64_t part_sum[1024 / WAVE];
     __shared__ uint64_t carry_s;
@@ -409,7 +410,7 @@ __global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t n
         __syncthreads();
     }
     if (threadIdx.x == 0)
-        off_out[nb] = carry_s;
+        off_out[nb] = carry_s > cap ? ~0ull : carry_s;
 }
 
 // One workgroup per global block: its 268-byte header and payload into global order.  A block that
@@ -543,7 +544,7 @@ bool assemble_shards_device(const ShardParts& parts, uint32_t nb, uint8_t* d_hdr
     if (parts.n == 0 || parts.n > MAX_SHARDS || nb == 0)
         return false;
     BRA_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
-    hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(1024), 0, s, parts, nb, d_off_out);
+    hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(1024), 0, s, parts, nb, d_off_out, cap);
     BRA_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_shard_copy, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, parts, nb, d_off_out, d_hdr_out, d_pay_out, cap, d_err);
     BRA_HIP_CHECK(hipGetLastError());

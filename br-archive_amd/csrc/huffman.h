@@ -52,7 +52,8 @@ struct HuffWorkspace
 // the total, also returned in *h_total).  d_meta[b] receives the bra_huffman_t of the block.
 bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc* h_rle_cap_blocks, uint32_t nblocks, const uint32_t* d_hist,
                         const uint32_t* d_rle_size, HuffMetaRec* d_meta, uint64_t* d_payload_off, uint8_t* d_payload, uint64_t payload_cap,
-                        uint64_t* h_total, hipStream_t s);
+                        uint64_t* h_total, hipStream_t s,
+                        bool cap_sufficient = false);
 
 // Decode every block: d_out + d_out_base[b] receives meta[b].orig_size bytes; d_status[b] != 0 on
 // a stream the reference would reject.  h_encoded_size: host copy of meta[b].encoded_size.

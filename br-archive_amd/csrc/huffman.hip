@@ -1632,7 +1632,7 @@ void HuffWorkspace::release()
 
 bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc* h_rle_cap_blocks, uint32_t nblocks,
                         const uint32_t* d_hist, const uint32_t* d_rle_size, HuffMetaRec* d_meta, uint64_t* d_payload_off,
-                        uint8_t* d_payload, uint64_t payload_cap, uint64_t* h_total, hipStream_t s)
+                        uint8_t* d_payload, uint64_t payload_cap, uint64_t* h_total, hipStream_t s, bool cap_sufficient)
 {
     if (!w.tiling.build(h_rle_cap_blocks, nblocks, RLE_TILE, s))
         return false;
@@ -1657,9 +1657,16 @@ bool huff_encode_device(HuffWorkspace& w, const uint8_t* d_rle, const BlockDesc*
         hipLaunchKernelGGL(k_huff_tilescan, dim3(std::min<uint32_t>(nblocks, 4096)), dim3(64), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks,
                            d_payload_off, w.tbits, w.tbit0);
     }
-    BRA_HIP_CHECK(hipMemcpyAsync(h_total, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s));
-    BRA_HIP_CHECK(hipStreamSynchronize(s));
-    if (*h_total + 8 > payload_cap)
+    // The payload is at most the RLE bytes plus a word per block (an optimal prefix code over byte
+    // symbols is never longer than the 8-bit one): a caller whose capacity covers that bound needs
+    // no check, and the stream is not stopped here for it.
+    *h_total = 0;
+    if (!cap_sufficient)
+    {
+        BRA_HIP_CHECK(hipMemcpyAsync(h_total, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    if (!cap_sufficient && *h_total + 8 > payload_cap)
     {
         bra_hip_report("huffman: payload capacity %llu too small for %llu bytes", (unsigned long long) payload_cap,
                        (unsigned long long) *h_total);

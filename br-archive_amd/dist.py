@@ -104,6 +104,14 @@ def merge_crc(parts) -> int:
     return v
 
 
+def merge_crc_device(parts):
+    """merge_crc on the device: the XOR of the ranks' int32 shares, without a host round trip."""
+    v = parts[0][3]
+    for p in parts[1:]:
+        v = v ^ p[3]
+    return v
+
+
 def assemble(codec, parts, round_robin: bool = True, stream=None):
     """Device assembly on rank 0: (headers [N, 268], offsets [N + 1], payload) in global block order.
 
