@@ -60,7 +60,7 @@ constexpr int      TILE         = BRA_TILE;  // elements per MSD tile (256 threa
 constexpr int      TPB          = 256;
 constexpr int      PER_THREAD   = TILE / TPB;
 constexpr uint32_t JOB_MAX      = 256;  // elements one wave sorts in registers
-constexpr int      MJ_WAVES_DEF = 4;    // waves of a workgroup job (2, 4, 8 or 16)
+constexpr int      MJ_WAVES_DEF = 4;    // waves of the largest workgroup job (2 or 4; 8 / 16 -- jobs of up to 4096 -- measured slower, removed)
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
@@ -2459,9 +2459,9 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
         JT_FLUSH(1);
 }
 
-// Workgroup-job size classes: a job of (256, 512] elements runs on 2 waves, (512, 1024] on 4,
-// (1024, 2048] on 8, (2048, 4096] on 16 (never more waves than the job's network needs).
-constexpr uint32_t MJ_CLASSES = 4;
+// Workgroup-job size classes: a job of (256, 512] elements runs on 2 waves, (512, 1024] on 4 (never
+// more waves than the job's network needs).
+constexpr uint32_t MJ_CLASSES = 2;
 __device__ __forceinline__ uint32_t mjob_class(uint32_t len, uint32_t classes)
 {
     const uint32_t lg = 32u - (uint32_t) __builtin_clz(max(len, 257u) - 1u);  // ceil(log2(len)) >= 9
@@ -2919,7 +2919,7 @@ struct BwtWorkspace
     uint32_t  jobq_chunk = BRA_JQ_CHUNK;  // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
-    uint32_t  mj_classes() const { return mj_waves >= 16 ? 4u : mj_waves >= 8 ? 3u : mj_waves >= 4 ? 2u : 1u; }
+    uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
@@ -3032,11 +3032,7 @@ static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
     // about the resident capacity: 6144 waves (24 per CU)
     const uint32_t cap = 6144u / (uint32_t) waves;
     const dim3     g(round8(std::min<uint32_t>(n, cap)));
-    if (waves == 16)
-        hipLaunchKernelGGL((k_mjobs<MODE, 16>), g, dim3(64 * 16), sizeof(JobLds<16>) + 16, s, a);
-    else if (waves == 8)
-        hipLaunchKernelGGL((k_mjobs<MODE, 8>), g, dim3(64 * 8), sizeof(JobLds<8>) + 16, s, a);
-    else if (waves == 4)
+    if (waves == 4)
         hipLaunchKernelGGL((k_mjobs<MODE, 4>), g, dim3(64 * 4), sizeof(JobLds<4>) + 16, s, a);
     else
         hipLaunchKernelGGL((k_mjobs<MODE, 2>), g, dim3(64 * 2), sizeof(JobLds<2>) + 16, s, a);
@@ -3344,10 +3340,6 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageL0) + TILE + 64)));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<16>) + 16));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_STRING, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_mjobs<MODE_RANK, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(JobLds<8>) + 16));
         attr_set.fetch_or(dev_bit);
     }
     const int grid = w.grid;

@@ -421,7 +421,8 @@ def test_mtf_start_tables_straddling_2_24(bra, orc):
     """The MTF start-table sort for positions at or past 2^24 (csrc/mtf.hip start_table_dword: two
     passes over 24-bit digits when a last occurrence reaches 0xFFFFFE): a 17 MiB block whose
     distinct symbols' last occurrences fall on 2^24 - 3 .. 2^24 + 2, so a segment's start table
-    mixes occurrences just below and just above the 24-bit limit; small and large alphabets."""
+    mixes occurrences just below and just above the 24-bit limit; a small alphabet (the
+    position-table path: int32 last occurrences) and a large one (the wave kernel's two-pass sort)."""
     n = 17 << 20
     base = (1 << 24) - 3
     rng = np.random.default_rng(2424)
