@@ -306,7 +306,7 @@ def main():
         payload_bytes = int(off_h[nbg])
         rle_bytes = int(hdr_h[:, 260:264].copy().view(np.uint32).sum())
         pipeline_alg = 14 * global_total + 3 * rle_bytes + payload_bytes + 267 * nbg  # SURVEY 8.1 row d
-        stage_ms = {s.split(".")[1]: round(prof[s][0] / max(1, prof[s][1]), 3) for s in stage_slots}
+        stage_ms = {s.split(".")[1]: round(prof[s][0] / args.steps, 3) for s in stage_slots}  # device ms per step (a stage may open several scopes per step)
         check, secondary = None, {}
         if not args.no_check:
             # decode the assembled global stream; its chunk-stream CRC must equal the merged shares

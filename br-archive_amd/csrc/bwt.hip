@@ -75,6 +75,9 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_PIPE
 #define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
 #endif
+#ifndef BRA_HIST_GRID
+#define BRA_HIST_GRID 0  // workgroups of the MSD histogram (0: the tile-kernel grid)
+#endif
 #ifndef BRA_JQ_CHUNK
 #define BRA_JQ_CHUNK 2  // wave jobs a wave claims with one atomic
 #endif
@@ -3217,7 +3220,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             }
             {
                 BRA_PROF(P_BWT_HIST, s);
-                hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
+                hipLaunchKernelGGL(k_hist<MODE>, dim3(BRA_HIST_GRID ? BRA_HIST_GRID : grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
                                    w.pay[1], w.tile_hist, lin, to, w.dig[0], w.dig[1]); BRA_DSYNC(s);
             }
             ScanArgs a{d_blocks, w.big[cur],  0,           w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
