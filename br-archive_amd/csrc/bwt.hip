@@ -72,11 +72,14 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_NC
 #define BRA_HIST_NC 4  // counter copies of the MSD histogram (copy = lane & (NC - 1))
 #endif
-#ifndef BRA_HIST_PIPE
-#define BRA_HIST_PIPE 1                  // MSD histogram: next tile loaded while the current one is counted (0: one tile at a time)
+#ifndef BRA_HIST_WAVE
+#define BRA_HIST_WAVE 1  // MSD histogram: one wave per tile (0: one workgroup per tile)
 #endif
 #ifndef BRA_HIST_GRID
 #define BRA_HIST_GRID 0  // workgroups of the MSD histogram (0: the tile-kernel grid)
+#endif
+#ifndef BRA_JOB_STREAMS
+#define BRA_JOB_STREAMS 0  // measurement: job classes on concurrent streams
 #endif
 #ifndef BRA_JQ_CHUNK
 #define BRA_JQ_CHUNK 2  // wave jobs a wave claims with one atomic
@@ -167,6 +170,20 @@ __device__ __forceinline__ uint32_t tile_pos(const TileOrder& o, uint32_t i, uin
         return t < ntiles ? t : ~0u;
     }
     const uint32_t x = blockIdx.x & 7, l = blockIdx.x >> 3, g = gridDim.x >> 3;
+    const uint32_t p = o.xseg[x] + l + i * g;
+    return p < o.xseg[x + 1] ? p : ~0u;
+}
+
+// List position of wave wv's i-th tile when every wave of a workgroup takes tiles on its own (the
+// workgroup's XCD part is shared by its waves as if they were 4 x as many workgroups).
+__device__ __forceinline__ uint32_t tile_pos_wave(const TileOrder& o, uint32_t i, uint32_t ntiles, uint32_t wv, uint32_t wpg)
+{
+    if (!o.desc || o.natural)
+    {
+        const uint32_t t = blockIdx.x * wpg + wv + i * gridDim.x * wpg;
+        return t < ntiles ? t : ~0u;
+    }
+    const uint32_t x = blockIdx.x & 7, l = (blockIdx.x >> 3) * wpg + wv, g = (gridDim.x >> 3) * wpg;
     const uint32_t p = o.xseg[x] + l + i * g;
     return p < o.xseg[x + 1] ? p : ~0u;
 }
@@ -571,13 +588,13 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
 {
     const uint32_t ntiles = dev_count(&lv->n_tiles_next);
     __shared__ uint32_t h[256];
-    __shared__ uint32_t hc[BRA_HIST_NC * CSTRIDE];  // per-copy counters (copy = lane & (NC - 1), see TileStagePN)
-    if (MODE == MODE_STRING && BRA_HIST_PIPE)
+    if (MODE == MODE_STRING && !BRA_HIST_WAVE)
     {
         // software-pipelined over the workgroup's tiles: the next tile's descriptor and payloads
         // are loaded before the current tile's LDS histogram is built
         // STRING digits come from the byte array the previous scatter wrote beside the payloads
         // (dig[buf][slot] = the element's digit at this level): 16 contiguous digits per thread.
+        __shared__ uint32_t hc[BRA_HIST_NC * CSTRIDE];
         uint32_t p = tile_pos(to, 0, ntiles);
         TileDesc D{};
         uint4    w;
@@ -632,6 +649,96 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
             p = pn;
             D = Dn;
             w = wn;
+        }
+        return;
+
+    }
+    if (MODE == MODE_STRING)
+    {
+        // One wave per tile (no workgroup barriers: most tiles past level 1 are a small bucket's only
+        // tile, and the workgroup form spent its time in the two barriers and the per-tile setup).
+        // STRING digits come from the byte array the previous scatter wrote beside the payloads
+        // (dig[buf][slot] = the element's digit at this level): 16 contiguous digits per lane and
+        // 1 KiB step, 4 steps per tile.  The next tile's descriptor is loaded before the current one
+        // is counted.
+        __shared__ __attribute__((aligned(16))) uint32_t hw[TPB / 64][BRA_HIST_NC * CSTRIDE];  // 16-aligned: read back as uint4
+        const uint32_t      wv = threadIdx.x >> 6, lane = (uint32_t) lane_id();
+        uint32_t* const     hc = hw[wv];
+        const uint32_t      cp = (lane & (BRA_HIST_NC - 1)) * CSTRIDE;
+        uint32_t            p  = tile_pos_wave(to, 0, ntiles, wv, TPB / 64);
+        TileDesc            D{};
+        if (p != ~0u)
+            D = to.desc[p];
+        for (uint32_t it = 1; p != ~0u; ++it)
+        {
+            const uint32_t pn = tile_pos_wave(to, it, ntiles, wv, TPB / 64);
+            TileDesc       Dn{};
+            if (pn != ~0u)
+                Dn = to.desc[pn];
+            for (uint32_t c = lane; c < BRA_HIST_NC * CSTRIDE; c += 64)
+                hc[c] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): without it the wave's own LDS phases overlapped (wrong counts, GPU-measured)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (D.pdig)
+            {
+                // digits still in the payloads (the bucket did not move at the previous level)
+                const uint64_t* pay = (D.buf ? key1 : key0) + D.s0;
+                const uint32_t  jj  = D.d - D.kd;
+                for (uint32_t i = lane; i < D.cnt; i += 64)
+                    atomicAdd(&hc[cp + p_digit(pay[i], jj)], 1u);
+            }
+            else
+            {
+                const uint8_t* g = (D.buf ? dig1 : dig0) + D.s0;
+                uint4          w4[TILE / 1024];
+#pragma unroll
+                for (int j = 0; j < TILE / 1024; ++j)
+                {
+                    const uint32_t e = (uint32_t) j * 1024 + lane * 16;
+                    if (e + 16 <= D.cnt)
+                        w4[j] = *reinterpret_cast<const uint4_u*>(g + e);
+                    else
+                    {
+                        uint32_t x[4] = {0, 0, 0, 0};
+                        for (uint32_t i = 0; e + i < D.cnt && i < 16; ++i)
+                            x[i >> 2] |= (uint32_t) g[e + i] << (8 * (i & 3));
+                        w4[j] = make_uint4(x[0], x[1], x[2], x[3]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < TILE / 1024; ++j)
+                {
+                    const uint32_t wd[4] = {w4[j].x, w4[j].y, w4[j].z, w4[j].w};
+                    const uint32_t e     = (uint32_t) j * 1024 + lane * 16;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if (e + i < D.cnt)
+                            atomicAdd(&hc[cp + ((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): without it the wave's own LDS phases overlapped (wrong counts, GPU-measured)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint4 tot = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int c = 0; c < BRA_HIST_NC; ++c)
+            {
+                const uint4 h = *reinterpret_cast<const uint4*>(&hc[c * CSTRIDE + lane * 4]);
+                tot.x += h.x;
+                tot.y += h.y;
+                tot.z += h.z;
+                tot.w += h.w;
+            }
+            reinterpret_cast<uint4*>(tile_hist + (size_t) D.t * 256)[lane] = tot;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): without it the wave's own LDS phases overlapped (wrong counts, GPU-measured)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            p = pn;
+            D = Dn;
         }
         return;
     }
@@ -706,6 +813,8 @@ struct ScanArgs
     const Counters* lin;       // this level's bucket count (n_big); null: nbuckets (level 0)
     Counters*       lout;      // the next level's buckets / tiles / byte accounting
     const PackDesc* pk;        // STRING: packed key strings per block
+    const uint32_t* btot;      // level 0: per-bucket digit totals (k_l0_colscan) instead of the tile rows
+    uint32_t*       bbase;     // level 0: per-bucket sub-bucket starts (| NEXT_FLAG), added to the tiles' running counts by the scatter
 };
 
 // One wave per bucket (SCAN_WAVES buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
@@ -769,9 +878,14 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
                        bi, B.start, B.len, B.block, (unsigned long long) BD.off, BD.len, B.d);
         }
 #endif
-        const uint32_t ntiles = active ? div_up(B.len, TILE) : 0;
+        const uint32_t ntiles = (active && !a.btot) ? div_up(B.len, TILE) : 0;
         const uint4*   th     = reinterpret_cast<const uint4*>(a.tile_hist + (size_t) B.tile0 * 256) + lane;
         uint32_t       tot[4] = {0, 0, 0, 0};
+        if (a.btot && active)
+        {
+            const uint4 q = reinterpret_cast<const uint4*>(a.btot + (size_t) bi * 256)[lane];
+            tot[0] = q.x, tot[1] = q.y, tot[2] = q.z, tot[3] = q.w;
+        }
         {
             uint32_t t = 0;
             for (; t + 8 <= ntiles; t += 8)
@@ -812,6 +926,9 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES, BRA_SCAN_MIN_WAVES) k_scan(Sc
             }
             uint4*   to     = reinterpret_cast<uint4*>(a.tile_off + (size_t) B.tile0 * 256) + lane;
             uint32_t run[4] = {B.start + base[0], B.start + base[1], B.start + base[2], B.start + base[3]};
+            if (a.bbase && active)
+                reinterpret_cast<uint4*>(a.bbase + (size_t) bi * 256)[lane] =
+                    make_uint4(run[0] | flag[0], run[1] | flag[1], run[2] | flag[2], run[3] | flag[3]);
             for (uint32_t t = 0; t < ntiles; ++t)
             {
                 const uint4 h        = th[(size_t) t * 64];
@@ -1223,13 +1340,80 @@ __device__ __forceinline__ void stage_and_write(TileStage& S, const uint64_t (&k
     }
 }
 
+// Level 0, per block: each tile's running per-digit count over the block's earlier tiles (into
+// tile_off) and the block's digit totals.  The level-0 scan then reads 1 KiB per block instead of
+// walking the block's tile rows twice with one wave (256 tiles of 1 MiB blocks: the round-3 scan
+// took 116 us for 256 waves); the scatter adds the scan's sub-bucket starts.  Four thread groups
+// take a quarter of the tiles each.
+constexpr uint32_t L0CS_GROUPS = 4;
+__global__ void __launch_bounds__(256 * L0CS_GROUPS) k_l0_colscan(const Bucket* __restrict__ l0b, uint32_t nblocks, const uint32_t* __restrict__ tile_hist,
+                                                                  uint32_t* __restrict__ tile_off, uint32_t* __restrict__ btot)
+{
+    __shared__ uint32_t part[L0CS_GROUPS][256];
+    const uint32_t      d = threadIdx.x & 255u, g = threadIdx.x >> 8;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
+    {
+        const Bucket    B   = l0b[b];
+        const uint32_t  nt  = div_up(B.len, TILE);
+        const uint32_t  per = div_up(nt, L0CS_GROUPS);
+        const uint32_t  t0 = min(nt, g * per), t1 = min(nt, t0 + per);
+        const uint32_t* th = tile_hist + (size_t) B.tile0 * 256 + d;
+        uint32_t*       to = tile_off + (size_t) B.tile0 * 256 + d;
+        uint32_t        sum = 0, t = t0;
+        for (; t + 8 <= t1; t += 8)
+        {
+            uint32_t h[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                h[u] = th[(size_t) (t + u) * 256];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                sum += h[u];
+        }
+        for (; t < t1; ++t)
+            sum += th[(size_t) t * 256];
+        part[g][d] = sum;
+        __syncthreads();
+        uint32_t run = 0, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < L0CS_GROUPS; ++k)
+        {
+            const uint32_t x = part[k][d];
+            run += k < g ? x : 0u;
+            tot += x;
+        }
+        for (t = t0; t + 8 <= t1; t += 8)
+        {
+            uint32_t h[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                h[u] = th[(size_t) (t + u) * 256];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+            {
+                to[(size_t) (t + u) * 256] = run;
+                run += h[u];
+            }
+        }
+        for (; t < t1; ++t)
+        {
+            const uint32_t h = th[(size_t) t * 256];
+            to[(size_t) t * 256] = run;
+            run += h;
+        }
+        if (g == 0)
+            btot[(size_t) b * 256 + d] = tot;
+        __syncthreads();
+    }
+}
+
 // Level 0: every element gets its payload carrying virtual bytes 1..CARRY (the next digits) and its
 // BWT output byte.
 __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ in, const uint32_t* __restrict__ amask,
                                                     const uint8_t* __restrict__ packed, const BlockDesc* __restrict__ blocks,
                                                     const PackDesc* __restrict__ pkd, const L0Tile* __restrict__ tiles, uint32_t ntiles,
-                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ opay,
-                                                    uint8_t* __restrict__ odig)
+                                                    const uint32_t* __restrict__ tile_off, const uint32_t* __restrict__ l0base,
+                                                    uint64_t* __restrict__ opay, uint8_t* __restrict__ odig)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
@@ -1252,7 +1436,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
         load_window(packed + P.poff, T.start, cnt, P.b, win);
         stage_zero(S);
-        S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x] & ~NEXT_FLAG;
+        S.goff[threadIdx.x] = (tile_off[(size_t) t * 256 + threadIdx.x] + l0base[(size_t) T.block * 256 + threadIdx.x]) & ~NEXT_FLAG;
         {
             // alphabet rank -> byte value (the packing's map, inverted): thread v = byte value v
             const uint32_t  vv = threadIdx.x;
@@ -2909,6 +3093,8 @@ struct BwtWorkspace
     PackDesc* pkd            = nullptr;  // per block
     uint32_t* amask          = nullptr;  // per block: 256-bit presence mask of the byte values
     uint32_t* tmask          = nullptr;  // per level-0 tile: the same mask
+    uint32_t* l0tot          = nullptr;  // per block: level-0 digit totals (k_l0_colscan)
+    uint32_t* l0base         = nullptr;  // per block: level-0 sub-bucket starts (k_scan)
     std::vector<BlockDesc> geo;          // block geometry the level-0 tiles / buckets on the device were built for
     uint32_t  nt0 = 0;
     uint32_t  cap_tiles = 0, cap_big = 0, cap_jobs = 0, cap_mjobs = 0, cap_groups = 0, cap_l0 = 0;
@@ -2922,6 +3108,8 @@ struct BwtWorkspace
     uint32_t  jobq_chunk = BRA_JQ_CHUNK;  // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
+    hipStream_t js[3]    = {nullptr, nullptr, nullptr};  // BRA_JOB_STREAMS: one stream per job class (forked from the call's stream)
+    hipEvent_t  jev[4]   = {nullptr, nullptr, nullptr, nullptr};
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -3058,14 +3246,26 @@ static void ws_free(BwtWorkspace& w)
         (void) hipFree(w.dig[i]);
     }
     void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
-                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask};
+                   w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask, w.l0tot, w.l0base};
     for (void* p : dev)
         (void) hipFree(p);
     if (w.h_ctr)
         (void) hipHostFree(w.h_ctr);
     if (w.h_mail)
         (void) hipHostFree(w.h_mail);
-    w = BwtWorkspace{};
+    for (hipStream_t st : w.js)
+        if (st)
+            (void) hipStreamDestroy(st);
+    for (hipEvent_t e : w.jev)
+        if (e)
+            (void) hipEventDestroy(e);
+    // The mailbox sequence survives a reallocation: a new pinned record block can be the memory of
+    // the old one (the host allocator reuses it) with the old records still in it, and a counter that
+    // restarted at 1 would meet their sequence numbers again -- wait_mail then took a stale record
+    // for the device's answer (order- and timing-dependent wrong level counts / fallback groups).
+    const uint32_t seq = w.mail_seq;
+    w                  = BwtWorkspace{};
+    w.mail_seq         = seq;
 }
 
 BwtWorkspace* bwt_workspace_create() { return new BwtWorkspace(); }
@@ -3111,11 +3311,13 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
          dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
          dev_alloc(w.jobq, (1 + MJ_CLASSES) * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
          dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B) &&
-         dev_alloc(w.tmask, 8ull * w.cap_l0);
+         dev_alloc(w.tmask, 8ull * w.cap_l0) && dev_alloc(w.l0tot, 256ull * B) && dev_alloc(w.l0base, 256ull * B);
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
         w.h_mail = nullptr, ok = false;
+    if (ok)
+        std::memset(w.h_mail, 0, MAX_LEVELS * sizeof(Mail));  // no record left from an earlier owner of the memory (seq 0 is never posted)
     if (!ok)
     {
         (void) hipGetLastError();
@@ -3151,6 +3353,35 @@ static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
         ord[k].jq       = w.jobq + k * 8 * 32;
         ord[k].jq_chunk = w.jobq_chunk;
     }
+#if BRA_JOB_STREAMS
+    // the three job classes on their own streams: the tail of one kernel overlaps the others
+    if (!w.js[0])
+    {
+        for (auto& st : w.js)
+            BRA_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        for (auto& e : w.jev)
+            BRA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    BRA_HIP_CHECK(hipEventRecord(w.jev[3], s));
+    for (uint32_t k = 0; k < 1 + w.mj_classes(); ++k)
+        BRA_HIP_CHECK(hipStreamWaitEvent(w.js[k], w.jev[3], 0));
+    {
+        BRA_PROF(P_BWT_JOBS, w.js[0]);
+        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, w.js[0], ord[0]);
+    }
+    for (uint32_t c = 0; c < w.mj_classes(); ++c)
+    {
+        BRA_PROF(P_BWT_MJOBS, w.js[1 + c]);
+        launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], w.js[1 + c]);
+    }
+    for (uint32_t k = 0; k < 1 + w.mj_classes(); ++k)
+    {
+        BRA_HIP_CHECK(hipEventRecord(w.jev[k], w.js[k]));
+        BRA_HIP_CHECK(hipStreamWaitEvent(s, w.jev[k], 0));
+    }
+    BRA_HIP_CHECK(hipGetLastError());
+    return true;
+#endif
     {
         BRA_PROF(P_BWT_JOBS, s);
         hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, s, ord[0]);
@@ -3226,7 +3457,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             ScanArgs a{d_blocks, w.big[cur],  0,           w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],
                        w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
                        w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
-                       (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout, w.pkd};
+                       (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout, w.pkd, nullptr, nullptr};
             {
                 BRA_PROF(P_BWT_SCAN, s);
                 hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
@@ -3385,15 +3616,19 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     }
     ScanArgs a0{d_blocks, w.l0b,     nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
-                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1, w.pkd};
+                w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1, w.pkd,
+                w.l0tot,          w.l0base};
     {
         BRA_PROF(P_BWT_SCAN, s);
+        hipLaunchKernelGGL(k_l0_colscan, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(256 * L0CS_GROUPS), 0, s, w.l0b, nblocks, w.tile_hist,
+                           w.tile_off, w.l0tot);
+        BRA_DSYNC(s);
         hipLaunchKernelGGL(k_scan<MODE_STRING>, dim3(std::min<uint32_t>(div_up(nblocks, SCAN_WAVES), 65535u)), dim3(64 * SCAN_WAVES), 0, s, a0); BRA_DSYNC(s);
     }
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
         hipLaunchKernelGGL(k_l0_scatter, dim3(nt0 >= 8 ? std::min<uint32_t>(nt0, grid) & ~7u : nt0), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, d_in, w.amask, w.packed, d_blocks,
-                           w.pkd, w.l0tiles, nt0, w.tile_off, w.key[0], w.dig[0]); BRA_DSYNC(s);
+                           w.pkd, w.l0tiles, nt0, w.tile_off, w.l0base, w.key[0], w.dig[0]); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     prof_bytes(P_BWT_PACK, 3.0 * (double) N);  // input read twice, packed string written (<= N)
@@ -3466,6 +3701,9 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
 
     // ---- fallback: prefix doubling on the groups still tied ----
     uint32_t ng = mc.n_groups;
+    static const bool level_stats = getenv("BRA_LEVEL_STATS") != nullptr;  // diagnostic
+    if (level_stats)
+        fprintf(stderr, "[bwt finish] mail seq %u groups %u jobs %u mjobs %u hmin %u\n", mc.seq, mc.n_groups, mc.n_jobs, mc.n_mjobs, mc.hmin);
     if (ng == 0)
         return true;
     if (fallback_ran)
@@ -3545,6 +3783,8 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
             keep.push_back(g);
         }
         ng = (uint32_t) keep.size();
+        if (level_stats)
+            fprintf(stderr, "[bwt fallback] round %d: big groups %u jobs %u mjobs %u -> groups %u kept %u hmin %u\n", round, ng_big, nj, nmj, ng_new, ng, m);
         if (ng)
             BRA_HIP_CHECK(hipMemcpyAsync(gnext, keep.data(), ng * sizeof(Group), hipMemcpyHostToDevice, s));
         BRA_HIP_CHECK(hipStreamSynchronize(s));

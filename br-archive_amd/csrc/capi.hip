@@ -218,6 +218,7 @@ struct bra_gpu_ctx_s
     uint64_t       cap_hin = 0, cap_hout = 0;
     uint64_t*      d_enc_rle_base = nullptr;
     uint64_t       cap_eb = 0, cap_erb = 0;
+    hipEvent_t     null_ev = nullptr;  // CallStream: the null stream's position at a NULL-stream call
     Prof           prof;
 };
 
@@ -228,6 +229,7 @@ static bool ctx_init(bra_gpu_ctx_s* c, int device)
     if (!dg.ok)
         return false;
     BRA_HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    BRA_HIP_CHECK(hipEventCreateWithFlags(&c->null_ev, hipEventDisableTiming));
     c->bwt = bwt_workspace_create();
     return c->bwt != nullptr;
 }
@@ -248,7 +250,33 @@ static void ctx_free(bra_gpu_ctx_s* c)
         (void) hipFree(p);
     if (c->stream)
         (void) hipStreamDestroy(c->stream);
+    if (c->null_ev)
+        (void) hipEventDestroy(c->null_ev);
 }
+
+// The stream a batch call runs on (include/bra_hip.h, Part 2/3).  An explicit stream orders the
+// call on that stream.  NULL means the context's stream, started after the work already queued on
+// the null (legacy default) stream -- the caller's preceding copies, and torch's default stream,
+// whose handle is NULL -- and complete when the call returns.  (The context stream is
+// non-blocking: without the two joins a NULL-stream caller could read the results before the
+// call's last kernels had written them -- the encode chain queues MTF / RLE / Huffman after its
+// last host wait -- or the call could read inputs still in flight on the null stream.)
+struct CallStream
+{
+    hipStream_t s;
+    bool        own;
+    CallStream(bra_gpu_ctx_s* c, void* stream) : s(stream ? (hipStream_t) stream : c->stream), own(stream == nullptr)
+    {
+        if (own && hipEventRecord(c->null_ev, nullptr) == hipSuccess)
+            (void) hipStreamWaitEvent(s, c->null_ev, 0);
+    }
+    ~CallStream()
+    {
+        if (own)
+            (void) hipStreamSynchronize(s);
+    }
+    operator hipStream_t() const { return s; }
+};
 
 static std::vector<BlockDesc> geometry(uint64_t total, uint32_t block_size)
 {
@@ -576,7 +604,8 @@ int bra_gpu_encode_blocks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t total,
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     g_prof       = c->prof.mask ? &c->prof : nullptr;
     const int rc = encode_impl(c, d_in, geometry(total, block_size), d_headers, d_payload_off, d_payload, payload_cap, s, nullptr);
     g_prof       = nullptr;
@@ -591,7 +620,8 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_heade
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     g_prof       = c->prof.mask ? &c->prof : nullptr;
     const int rc = decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
     g_prof       = nullptr;
@@ -605,7 +635,8 @@ int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t 
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     if (!crc_stream_device(static_cast<const uint8_t*>(d_data), len, 0, nullptr, prev, d_crc, s))
         return -1;
     return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;  // NULL stream: complete on return
@@ -619,7 +650,8 @@ int bra_gpu_chunks_crc32c(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_t tota
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     if (!crc_stream_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), prev, d_crc, s))
         return -1;
     return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
@@ -649,7 +681,8 @@ int bra_gpu_frame_chunks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_header
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     uint64_t    P = 0;
     if (hipMemcpyAsync(&P, d_payload_off + nblocks, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         return -1;
@@ -671,7 +704,8 @@ int bra_gpu_unframe_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t s
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     if (!grow(c->d_word, c->cap_word, 4))
         return -1;
     uint32_t st[2] = {0, 0};
@@ -697,7 +731,8 @@ int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t    s  = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t    s  = cs_;
     const auto     hb = geometry(data_size, block_size);
     const uint32_t nb = (uint32_t) hb.size();
     const uint64_t pb = bra_gpu_payload_bound(data_size, block_size);
@@ -763,7 +798,8 @@ static int decompress_chunks_impl(bra_gpu_ctx_t* c, const uint8_t* d_stream, uin
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t    s        = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t    s        = cs_;
     const uint32_t max_recs = (uint32_t) std::min<uint64_t>(stream_size / (CHUNK_HDR_DISK + 1) + 1, 1u << 26);
     if (!grow(c->d_hdr, c->cap_hdr, max_recs) || !grow(c->d_off, c->cap_off, max_recs + 1) || !grow(c->d_word, c->cap_word, 4))
         return -1;
@@ -878,7 +914,8 @@ int bra_gpu_chunks_crc32c_shard(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     if (!crc_stream_shard_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), first_chunk, chunk_stride, global_total,
                                  prev, with_init != 0, d_crc, s))
         return -1;
@@ -916,7 +953,8 @@ int bra_gpu_assemble_shards(bra_gpu_ctx_t* c, uint32_t nparts, const bra_io_chun
     DevGuard dg(c->device);
     if (!dg.ok)
         return -1;
-    hipStream_t s = stream ? (hipStream_t) stream : c->stream;
+    CallStream cs_(c, stream);
+    hipStream_t s = cs_;
     if (!grow(c->d_word, c->cap_word, 4) ||
         !assemble_shards_device(P, (uint32_t) nb, reinterpret_cast<uint8_t*>(d_headers_out), d_payload_off_out, d_payload_out, payload_cap,
                                 c->d_word + 3, s))
