@@ -72,15 +72,6 @@ constexpr int      SCATTER_NC = BRA_SCATTER_NC;
 #ifndef BRA_HIST_NC
 #define BRA_HIST_NC 4  // counter copies of the MSD histogram (copy = lane & (NC - 1))
 #endif
-#ifndef BRA_HIST_WAVE
-#define BRA_HIST_WAVE 1  // MSD histogram: one wave per tile (0: one workgroup per tile)
-#endif
-#ifndef BRA_HIST_GRID
-#define BRA_HIST_GRID 0  // workgroups of the MSD histogram (0: the tile-kernel grid)
-#endif
-#ifndef BRA_JOB_STREAMS
-#define BRA_JOB_STREAMS 0  // measurement: job classes on concurrent streams
-#endif
 #ifndef BRA_JQ_CHUNK
 #define BRA_JQ_CHUNK 2  // wave jobs a wave claims with one atomic
 #endif
@@ -588,71 +579,6 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
 {
     const uint32_t ntiles = dev_count(&lv->n_tiles_next);
     __shared__ uint32_t h[256];
-    if (MODE == MODE_STRING && !BRA_HIST_WAVE)
-    {
-        // software-pipelined over the workgroup's tiles: the next tile's descriptor and payloads
-        // are loaded before the current tile's LDS histogram is built
-        // STRING digits come from the byte array the previous scatter wrote beside the payloads
-        // (dig[buf][slot] = the element's digit at this level): 16 contiguous digits per thread.
-        __shared__ uint32_t hc[BRA_HIST_NC * CSTRIDE];
-        uint32_t p = tile_pos(to, 0, ntiles);
-        TileDesc D{};
-        uint4    w;
-        const auto load = [&](uint32_t pp, TileDesc& DD, uint4& ww) {
-            if (pp == ~0u)
-                return;
-            DD               = to.desc[pp];
-            const uint8_t* g = (DD.buf ? dig1 : dig0) + DD.s0 + threadIdx.x * 16;
-            if (DD.pdig)
-            {
-                // digits still in the payloads (the bucket did not move at the previous level)
-                const uint64_t* pay = (DD.buf ? key1 : key0) + DD.s0 + threadIdx.x * 16;
-                const uint32_t  jj  = DD.d - DD.kd;
-                uint32_t        x[4] = {0, 0, 0, 0};
-                for (uint32_t i = 0; threadIdx.x * 16 + i < DD.cnt && i < 16; ++i)
-                    x[i >> 2] |= p_digit(pay[i], jj) << (8 * (i & 3));
-                ww = make_uint4(x[0], x[1], x[2], x[3]);
-            }
-            else if (threadIdx.x * 16 + 16 <= DD.cnt)
-                ww = *reinterpret_cast<const uint4_u*>(g);
-            else
-            {
-                uint32_t x[4] = {0, 0, 0, 0};
-                for (uint32_t i = 0; threadIdx.x * 16 + i < DD.cnt && i < 16; ++i)
-                    x[i >> 2] |= (uint32_t) g[i] << (8 * (i & 3));
-                ww = make_uint4(x[0], x[1], x[2], x[3]);
-            }
-        };
-        load(p, D, w);
-        for (uint32_t it = 1; p != ~0u; ++it)
-        {
-            const uint32_t pn = tile_pos(to, it, ntiles);
-            TileDesc       Dn{};
-            uint4          wn;
-            load(pn, Dn, wn);
-#pragma unroll
-            for (int c = 0; c < BRA_HIST_NC; ++c)
-                hc[c * CSTRIDE + threadIdx.x] = 0;
-            __syncthreads();
-            const uint32_t cp   = (uint32_t) (lane_id() & (BRA_HIST_NC - 1)) * CSTRIDE;
-            const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (threadIdx.x * 16 + i < D.cnt)
-                    atomicAdd(&hc[cp + ((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
-            __syncthreads();
-            uint32_t tot = 0;
-#pragma unroll
-            for (int c = 0; c < BRA_HIST_NC; ++c)
-                tot += hc[c * CSTRIDE + threadIdx.x];
-            tile_hist[(size_t) D.t * 256 + threadIdx.x] = tot;
-            p = pn;
-            D = Dn;
-            w = wn;
-        }
-        return;
-
-    }
     if (MODE == MODE_STRING)
     {
         // One wave per tile (no workgroup barriers: most tiles past level 1 are a small bucket's only
@@ -3108,8 +3034,6 @@ struct BwtWorkspace
     uint32_t  jobq_chunk = BRA_JQ_CHUNK;  // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
-    hipStream_t js[3]    = {nullptr, nullptr, nullptr};  // BRA_JOB_STREAMS: one stream per job class (forked from the call's stream)
-    hipEvent_t  jev[4]   = {nullptr, nullptr, nullptr, nullptr};
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -3253,12 +3177,6 @@ static void ws_free(BwtWorkspace& w)
         (void) hipHostFree(w.h_ctr);
     if (w.h_mail)
         (void) hipHostFree(w.h_mail);
-    for (hipStream_t st : w.js)
-        if (st)
-            (void) hipStreamDestroy(st);
-    for (hipEvent_t e : w.jev)
-        if (e)
-            (void) hipEventDestroy(e);
     // The mailbox sequence survives a reallocation: a new pinned record block can be the memory of
     // the old one (the host allocator reuses it) with the old records still in it, and a counter that
     // restarted at 1 would meet their sequence numbers again -- wait_mail then took a stale record
@@ -3353,35 +3271,6 @@ static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
         ord[k].jq       = w.jobq + k * 8 * 32;
         ord[k].jq_chunk = w.jobq_chunk;
     }
-#if BRA_JOB_STREAMS
-    // the three job classes on their own streams: the tail of one kernel overlaps the others
-    if (!w.js[0])
-    {
-        for (auto& st : w.js)
-            BRA_HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-        for (auto& e : w.jev)
-            BRA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    BRA_HIP_CHECK(hipEventRecord(w.jev[3], s));
-    for (uint32_t k = 0; k < 1 + w.mj_classes(); ++k)
-        BRA_HIP_CHECK(hipStreamWaitEvent(w.js[k], w.jev[3], 0));
-    {
-        BRA_PROF(P_BWT_JOBS, w.js[0]);
-        hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, w.js[0], ord[0]);
-    }
-    for (uint32_t c = 0; c < w.mj_classes(); ++c)
-    {
-        BRA_PROF(P_BWT_MJOBS, w.js[1 + c]);
-        launch_mjobs<MODE_STRING>(2 << c, ~0u, ord[1 + c], w.js[1 + c]);
-    }
-    for (uint32_t k = 0; k < 1 + w.mj_classes(); ++k)
-    {
-        BRA_HIP_CHECK(hipEventRecord(w.jev[k], w.js[k]));
-        BRA_HIP_CHECK(hipStreamWaitEvent(s, w.jev[k], 0));
-    }
-    BRA_HIP_CHECK(hipGetLastError());
-    return true;
-#endif
     {
         BRA_PROF(P_BWT_JOBS, s);
         hipLaunchKernelGGL(k_jobs<MODE_STRING>, dim3(round8(w.jobs_grid)), dim3(256), 0, s, ord[0]);
@@ -3451,7 +3340,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
             }
             {
                 BRA_PROF(P_BWT_HIST, s);
-                hipLaunchKernelGGL(k_hist<MODE>, dim3(BRA_HIST_GRID ? BRA_HIST_GRID : grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
+                hipLaunchKernelGGL(k_hist<MODE>, dim3(grid), dim3(TPB), 0, s, w.big[cur], w.tile_bucket[cur], w.key[0], w.key[1], w.pay[0],
                                    w.pay[1], w.tile_hist, lin, to, w.dig[0], w.dig[1]); BRA_DSYNC(s);
             }
             ScanArgs a{d_blocks, w.big[cur],  0,           w.tile_hist, w.tile_off,  w.nomove,     w.big[cur ^ 1],

@@ -268,6 +268,30 @@ def test_batch_encode_is_deterministic(bra, codec):
         assert got == first, "encode output changed between runs of the same batch"
 
 
+def test_default_stream_results_complete_on_return(bra, codec, golden):
+    """A call without a stream runs on the context's stream, ordered after torch's default (null)
+    stream and complete when it returns (include/bra_hip.h, CallStream in csrc/capi.hip).  The
+    encode chain queues MTF / RLE / Huffman after its last host wait, and a fallback block queues
+    them twice: read at once on the default stream, the headers of the config-1 block came from the
+    first pass (the pre-fallback L and a stale pi) whenever the previous call had left the device
+    busy long enough.  The sequence here -- a fallback-heavy batch of another geometry, then the
+    config-1 block, read immediately -- failed 7 of 9 runs before the fix."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    bs = 1 << 18
+    text = bra.synth_fill(0, 4 * bs, bs, first_block=9)
+    d0 = torch.from_numpy(np.concatenate([text, _dup_blocks(rng, bs, 32 << 10, text)])).cuda()
+    g = golden["cfg1_tiled_65536"]
+    d1 = torch.from_numpy(np.frombuffer(g["input"], np.uint8).copy()).cuda()
+    for _ in range(3):
+        codec.encode(d0, bs)
+        hdr, off, pay = codec.encode(d1, 65536)
+        pi, lens, osz, esz = bra.parse_header(hdr[0].cpu().numpy().tobytes())
+        assert (pi, lens, osz, esz) == (g["pi"], g["lengths"], g["orig_size"], g["encoded_size"])
+        assert pay[:esz].cpu().numpy().tobytes() == g["payload"]
+
+
 def _alphabet_block(rng, bs: int, vals: np.ndarray) -> np.ndarray:
     """A block over the byte values vals, Zipf-weighted, with a 300-byte phrase repeated 6 times (ties
     that go past the first MSD levels)."""
