@@ -270,9 +270,21 @@ struct CallStream
         if (own && hipEventRecord(c->null_ev, nullptr) == hipSuccess)
             (void) hipStreamWaitEvent(s, c->null_ev, 0);
     }
-    ~CallStream()
+    // The call's result folded with the completion of a NULL-stream call: a kernel of the chain
+    // that failed after the last host wait shows only at this synchronisation.
+    int finish(int rc)
     {
         if (own)
+        {
+            own = false;
+            if (hipStreamSynchronize(s) != hipSuccess && rc >= 0)
+                rc = -1;
+        }
+        return rc;
+    }
+    ~CallStream()
+    {
+        if (own)  // an early (error) return: still leave nothing queued behind the caller
             (void) hipStreamSynchronize(s);
     }
     operator hipStream_t() const { return s; }
@@ -609,7 +621,7 @@ int bra_gpu_encode_blocks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t total,
     g_prof       = c->prof.mask ? &c->prof : nullptr;
     const int rc = encode_impl(c, d_in, geometry(total, block_size), d_headers, d_payload_off, d_payload, payload_cap, s, nullptr);
     g_prof       = nullptr;
-    return rc;
+    return cs_.finish(rc);
 }
 
 int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_headers, const uint64_t* d_payload_off, const uint8_t* d_payload,
@@ -625,7 +637,7 @@ int bra_gpu_decode_blocks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_heade
     g_prof       = c->prof.mask ? &c->prof : nullptr;
     const int rc = decode_impl(c, d_headers, d_payload_off, d_payload, geometry(total, block_size), d_out, s);
     g_prof       = nullptr;
-    return rc;
+    return cs_.finish(rc);
 }
 
 int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t prev, uint32_t* d_crc, void* stream)
@@ -639,7 +651,7 @@ int bra_gpu_crc32c(bra_gpu_ctx_t* c, const void* d_data, uint64_t len, uint32_t 
     hipStream_t s = cs_;
     if (!crc_stream_device(static_cast<const uint8_t*>(d_data), len, 0, nullptr, prev, d_crc, s))
         return -1;
-    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;  // NULL stream: complete on return
+    return cs_.finish(0);  // NULL stream: complete on return
 }
 
 int bra_gpu_chunks_crc32c(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_t total, uint32_t block_size, const bra_io_chunk_header_t* d_headers,
@@ -654,7 +666,7 @@ int bra_gpu_chunks_crc32c(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_t tota
     hipStream_t s = cs_;
     if (!crc_stream_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), prev, d_crc, s))
         return -1;
-    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
+    return cs_.finish(0);
 }
 
 uint32_t bra_gpu_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return crc32c_combine_host(crc_a, crc_b, len_b); }
@@ -693,7 +705,7 @@ int bra_gpu_frame_chunks(bra_gpu_ctx_t* c, const bra_io_chunk_header_t* d_header
         return -2;
     if (!frame_chunks_device(reinterpret_cast<const uint8_t*>(d_headers), d_payload_off, d_payload, nblocks, d_out, s))
         return -1;
-    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
+    return cs_.finish(0);
 }
 
 int bra_gpu_unframe_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t max_chunks, bra_io_chunk_header_t* d_headers,
@@ -720,7 +732,7 @@ int bra_gpu_unframe_chunks(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t s
         bra_hip_report(st[1] & 2 ? "chunk header not valid" : "truncated chunk stream (%u records)", st[0]);
         return -1;
     }
-    return 0;
+    return cs_.finish(0);
 }
 
 int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data_size, uint32_t block_size, uint8_t* d_out, uint64_t out_cap,
@@ -775,7 +787,7 @@ int bra_gpu_compress_chunks(bra_gpu_ctx_t* c, const uint8_t* d_in, uint64_t data
         return rc;
     if (chunks_crc)
         *chunks_crc = crc;
-    return need < data_size ? 1 : 0;  // 0: not smaller than the input -> STORED (lib_bra_io_file_chunks.c:274-278)
+    return cs_.finish(need < data_size ? 1 : 0);  // 0: not smaller than the input -> STORED (lib_bra_io_file_chunks.c:274-278)
 }
 
 static int decompress_chunks_impl(bra_gpu_ctx_t* c, const uint8_t* d_stream, uint64_t stream_size, uint32_t block_size, uint8_t* d_out,
@@ -851,7 +863,7 @@ static int decompress_chunks_impl(bra_gpu_ctx_t* c, const uint8_t* d_stream, uin
         }
         *crc_out = crc;
     }
-    return 0;
+    return cs_.finish(0);
 }
 
 // ---- host-buffer forms for the C front end (row f1; frontend/bra_io_file_chunks_gpu.c) ----
@@ -919,7 +931,7 @@ int bra_gpu_chunks_crc32c_shard(bra_gpu_ctx_t* c, const uint8_t* d_data, uint64_
     if (!crc_stream_shard_device(d_data, total, block_size, reinterpret_cast<const uint8_t*>(d_headers), first_chunk, chunk_stride, global_total,
                                  prev, with_init != 0, d_crc, s))
         return -1;
-    return (stream || hipStreamSynchronize(s) == hipSuccess) ? 0 : -1;
+    return cs_.finish(0);
 }
 
 int bra_gpu_assemble_shards(bra_gpu_ctx_t* c, uint32_t nparts, const bra_io_chunk_header_t* const* d_headers, const uint64_t* const* d_payload_off,
@@ -955,16 +967,20 @@ int bra_gpu_assemble_shards(bra_gpu_ctx_t* c, uint32_t nparts, const bra_io_chun
         return -1;
     CallStream cs_(c, stream);
     hipStream_t s = cs_;
-    if (!grow(c->d_word, c->cap_word, 4) ||
+    // d_word: [3] overflow flag, [4..5] the payload size needed (u64)
+    if (!grow(c->d_word, c->cap_word, 8) ||
         !assemble_shards_device(P, (uint32_t) nb, reinterpret_cast<uint8_t*>(d_headers_out), d_payload_off_out, d_payload_out, payload_cap,
-                                c->d_word + 3, s))
+                                c->d_word + 3, reinterpret_cast<uint64_t*>(c->d_word + 4), s))
         return -1;
     if (stream)
         return 0;  // asynchronous: an overflow shows as d_payload_off_out[nb] == UINT64_MAX
     uint32_t err = 1;
     if (hipMemcpyAsync(&err, c->d_word + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         return -1;
-    return err ? -2 : 0;
+    // on overflow, leave the size needed where the caller reads the payload size (offsets[N])
+    if (err && hipMemcpyAsync(d_payload_off_out + nb, c->d_word + 4, 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return -1;
+    return cs_.finish(err ? -2 : 0);
 }
 
 const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)

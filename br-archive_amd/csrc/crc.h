@@ -59,8 +59,9 @@ struct ShardParts
 };
 
 // Headers, payload offsets (nb + 1 entries) and payloads of all nb global blocks in global order;
-// *d_err != 0 when the payloads need more than cap bytes (the total is in d_off_out[nb]).
+// *d_err != 0 when the payloads need more than cap bytes (d_off_out[nb] is then UINT64_MAX); *d_need
+// receives the payload size the assembly needs either way.
 bool assemble_shards_device(const ShardParts& parts, uint32_t nb, uint8_t* d_hdr_out, uint64_t* d_off_out, uint8_t* d_pay_out, uint64_t cap,
-                            uint32_t* d_err, hipStream_t s);
+                            uint32_t* d_err, uint64_t* d_need, hipStream_t s);
 
 }  // namespace bra

@@ -366,7 +366,8 @@ __device__ __forceinline__ uint32_t hdr_encoded_size(const uint8_t* h) { return 
 // One workgroup: exclusive scan of the encoded sizes in global block order -> out offsets
 // (nb + 1 entries; the last one is the total payload, or UINT64_MAX when it exceeds cap: then the
 // last block is not copied and the caller sees the overflow without a host round trip).
-__global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t nb, uint64_t* __restrict__ off_out, uint64_t cap)
+__global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t nb, uint64_t* __restrict__ off_out, uint64_t cap,
+                                                        uint64_t* __restrict__ need)
 {
     __shared__ uint64_t part_sum[1024 / WAVE];
     __shared__ uint64_t carry_s;
@@ -410,7 +411,10 @@ __global__ __launch_bounds__(1024) void k_shard_offsets(ShardParts P, uint32_t n
         __syncthreads();
     }
     if (threadIdx.x == 0)
+    {
         off_out[nb] = carry_s > cap ? ~0ull : carry_s;
+        *need       = carry_s;  // the payload size the assembly needs, also on overflow
+    }
 }
 
 // One workgroup per global block: its 268-byte header and payload into global order.  A block that
@@ -539,12 +543,12 @@ bool unframe_chunks_device(const uint8_t* d_stream, uint64_t size, uint32_t cap,
 }
 
 bool assemble_shards_device(const ShardParts& parts, uint32_t nb, uint8_t* d_hdr_out, uint64_t* d_off_out, uint8_t* d_pay_out, uint64_t cap,
-                            uint32_t* d_err, hipStream_t s)
+                            uint32_t* d_err, uint64_t* d_need, hipStream_t s)
 {
     if (parts.n == 0 || parts.n > MAX_SHARDS || nb == 0)
         return false;
     BRA_HIP_CHECK(hipMemsetAsync(d_err, 0, 4, s));
-    hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(1024), 0, s, parts, nb, d_off_out, cap);
+    hipLaunchKernelGGL(k_shard_offsets, dim3(1), dim3(1024), 0, s, parts, nb, d_off_out, cap, d_need);
     BRA_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_shard_copy, dim3(std::min<uint32_t>(nb, 65535)), dim3(256), 0, s, parts, nb, d_off_out, d_hdr_out, d_pay_out, cap, d_err);
     BRA_HIP_CHECK(hipGetLastError());

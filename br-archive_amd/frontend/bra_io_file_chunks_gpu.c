@@ -280,7 +280,15 @@ static bool decode_records_serial(bra_io_file_t* dst, const char* fn, const uint
             return false;
         }
         *orig += s;
-        if (h.primary_index >= s || s > CHUNK_SIZE)
+        if (s > CHUNK_SIZE)
+        {
+            // no reference equivalent: the reference decodes into its 256 KiB g_buf without this
+            // check; here it protects the tmp buffer
+            bra_log_error("decoded chunk size %zu exceeds BRA_MAX_CHUNK_SIZE in %s", s, fn);
+            free(rle);
+            return false;
+        }
+        if (h.primary_index >= s)
         {
             bra_log_error("invalid primary index (%u) for chunk size %zu in %s", h.primary_index, s, fn);
             free(rle);

@@ -226,9 +226,11 @@ int bra_gpu_chunks_crc32c_shard(bra_gpu_ctx_t* ctx, const uint8_t* d_data, uint6
  * context's device, into global block order: headers, payload offsets (N + 1 entries, N = sum of
  * nblocks[]) and payloads back to back.  round_robin != 0: global block g is shard g % nparts's
  * block g / nparts; otherwise shard p holds the next nblocks[p] blocks.  With stream == NULL it
- * completes before returning and returns 0, -2 when the payloads need more than payload_cap bytes,
- * -1 on error.  With a stream it returns 0 once queued (-1 on an argument error) and an overflow
- * shows on the device as d_payload_off_out[N] == UINT64_MAX (the last block is then not copied).
+ * completes before returning and returns 0, -2 when the payloads need more than payload_cap bytes
+ * (d_payload_off_out[N] then holds the payload size needed), -1 on error.  With a stream it returns 0
+ * once queued (-1 on an argument error) and an overflow shows on the device as
+ * d_payload_off_out[N] == UINT64_MAX (the blocks past payload_cap are then not copied; the size
+ * needed is the sum of the parts' d_payload_off[p][nblocks[p]]).
  */
 int bra_gpu_assemble_shards(bra_gpu_ctx_t* ctx, uint32_t nparts, const bra_io_chunk_header_t* const* d_headers,
                             const uint64_t* const* d_payload_off, const uint8_t* const* d_payload, const uint32_t* nblocks, int round_robin,

@@ -1,0 +1,91 @@
+"""Localisation helpers for the .BRa chunk-stream tests (test infrastructure, not product).
+
+A chunk record on disk is 3-byte LE pi + packed bra_huffman_t (264 B) + payload
+(lib_bra_io_file_chunks.c:76-95, 217-256).  These helpers split a device chunk stream into its
+records, compare each record with the reference digests of tests/golden/digests.json, and -- when a
+decoded chunk differs from its input -- name the first decode stage whose output differs from the
+oracle's restatement of the reference for that chunk.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REC_HDR = 267
+
+
+def load_digests() -> dict:
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        return json.load(f)
+
+
+def split_records(stream: bytes):
+    """[(pi, meta 264 B, payload)] of a chunk stream; raises on a truncated one."""
+    recs, pos = [], 0
+    while pos < len(stream):
+        if pos + REC_HDR > len(stream):
+            raise AssertionError(f"truncated record header at {pos}")
+        pi = int.from_bytes(stream[pos: pos + 3], "little")
+        meta = stream[pos + 3: pos + REC_HDR]
+        esz = int.from_bytes(meta[260:264], "little")
+        if pos + REC_HDR + esz > len(stream):
+            raise AssertionError(f"truncated payload of record {len(recs)}")
+        recs.append((pi, meta, stream[pos + REC_HDR: pos + REC_HDR + esz]))
+        pos += REC_HDR + esz
+    return recs
+
+
+def record_digest(pi: int, meta: bytes, payload: bytes) -> str:
+    """sha256(pi u32 LE || bra_huffman_t || payload): the digest make_digests.py stores."""
+    return hashlib.sha256(pi.to_bytes(4, "little") + meta + payload).hexdigest()
+
+
+def records_vs_reference(stream: bytes, w: dict):
+    """Chunk indices whose record differs from the reference digests of workload w."""
+    recs = split_records(stream)
+    if len(recs) != w["nblocks"]:
+        raise AssertionError(f"{len(recs)} records, reference has {w['nblocks']}")
+    bad = []
+    for b, (pi, meta, pay) in enumerate(recs):
+        esz = int.from_bytes(meta[260:264], "little")
+        if (pi, esz, record_digest(pi, meta, pay)) != (w["pi"][b], w["encoded_size"][b], w["sha256"][b]):
+            bad.append(b)
+    return bad
+
+
+def headers_in_memory(stream: bytes) -> bytes:
+    """The 268-byte in-memory headers of every record, back to back (the CRC input, :248-249)."""
+    return b"".join(pi.to_bytes(4, "little") + meta for pi, meta, _ in split_records(stream))
+
+
+def bad_chunks(out: np.ndarray, data: np.ndarray, bs: int):
+    """Chunk indices where the decoded bytes differ from the input."""
+    n = min(out.size, data.size)
+    diff = np.flatnonzero(out[:n] != data[:n])
+    ids = sorted(set((diff // bs).tolist()))
+    if out.size != data.size:
+        ids.append(-1)
+    return ids
+
+
+def decode_diagnosis(codec, orc, data: np.ndarray, b: int, bs: int, total: int) -> str:
+    """First decode stage of chunk b (of the codec's last decode, chunks packed at b * bs) whose
+    output differs from the oracle: RLE decode output (= MTF symbols), MTF decode output (= BWT
+    last column), else the inverse BWT."""
+    lo, hi = b * bs, min(total, (b + 1) * bs)
+    blk = data[lo:hi].tobytes()
+    ref_L, _ = orc.bwt_encode(blk)
+    ref_M = orc.mtf_encode(ref_L)
+    M = codec.stage_copy(1, total)[lo:hi]
+    d = np.flatnonzero(M != np.frombuffer(ref_M, np.uint8))
+    if d.size:
+        return f"chunk {b}: Huffman/RLE decode output differs at {d.size} bytes (first {d[:4].tolist()})"
+    L = codec.stage_copy(0, total)[lo:hi]
+    d = np.flatnonzero(L != np.frombuffer(ref_L, np.uint8))
+    if d.size:
+        return f"chunk {b}: MTF decode output differs at {d.size} bytes (first {d[:4].tolist()})"
+    return f"chunk {b}: Huffman, RLE and MTF decode ok; inverse BWT output differs"

@@ -36,6 +36,12 @@ WORKLOADS = {
     "sym16_8MiB_x32": (2, 8 << 20, 32),
     "text_1MiB_x2048": (0, 1 << 20, 2048),
     "sym16_8MiB_x256": (2, 8 << 20, 256),
+    # the .BRa geometry: bra -c always encodes 256 KiB chunks (lib_bra_io_file_chunks.c:199-201,
+    # BRA_MAX_CHUNK_SIZE, lib_bra_defs.h:93) -- 1024 chunks = the 256 MiB chunk stream of
+    # tests/test_gpu_chunks.py::test_full_size_chunk_stream
+    "text_256KiB_x1024": (0, 256 << 10, 1024),
+    "random_256KiB_x1024": (1, 256 << 10, 1024),
+    "sym16_256KiB_x1024": (2, 256 << 10, 1024),
 }
 
 

@@ -10,6 +10,8 @@ import random
 import numpy as np
 import pytest
 
+import chunkdiag
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -218,17 +220,45 @@ def test_sharded_stream_crc_merge(bra, codec):
     assert bra.crc32c_combine(c_a, c_b, data.size - cut + 268 * nb_b) == c_all
 
 
-def test_full_size_chunk_stream(bra, codec):
-    """256 MiB of text as 1024 reference-size chunks: stream round trip, encode CRC == decode CRC."""
+def _chunk_stream_check(bra, codec, orc, name):
+    """256 MiB as 1024 reference-size chunks: every chunk record against the reference digests
+    (tests/golden/digests.json), the stream CRC against the oracle, then the decode chunk by chunk;
+    a failure names the first bad chunk and stage (encode record vs decode stage)."""
     import torch
 
-    total = 256 << 20
-    d = torch.from_numpy(bra.synth_fill(0, total, CS)).cuda()
+    w = chunkdiag.load_digests()[name]
+    bs, nb = w["block_size"], w["nblocks"]
+    assert bs == CS
+    total = bs * nb
+    data = bra.synth_fill(w["kind"], total, bs)
+    d = torch.from_numpy(data).cuda()
     stream, crc, compressed = codec.compress_chunks(d, CS)
-    assert compressed
+    st = stream.cpu().numpy().tobytes()
+    bad = chunkdiag.records_vs_reference(st, w)
+    assert not bad, f"encode: {len(bad)} of {nb} chunk records differ from the reference, first {bad[:8]}"
+    assert compressed == (len(st) < total)
+    assert crc == orc.chunks_crc32c(chunkdiag.headers_in_memory(st), data.tobytes(), CS), "encode: chunk-stream CRC"
+    if not compressed:
+        return
     out, dcrc = codec.decompress_chunks(stream, CS, out_cap=total)
-    assert torch.equal(out, d)
+    bad = chunkdiag.bad_chunks(out.cpu().numpy(), data, bs)
+    if bad:
+        first = bad[0] if bad[0] >= 0 else 0
+        raise AssertionError(f"decode: {len(bad)} of {nb} chunks differ, first {bad[:8]}; "
+                             f"{chunkdiag.decode_diagnosis(codec, orc, data, first, bs, total)}")
     assert dcrc == crc
+
+
+def test_full_size_chunk_stream(bra, codec, orc):
+    """256 MiB of text as 1024 reference-size chunks (the bra -c geometry): every record vs the
+    reference, stream round trip, encode CRC == decode CRC == oracle CRC."""
+    _chunk_stream_check(bra, codec, orc, "text_256KiB_x1024")
+
+
+@pytest.mark.parametrize("name", ["random_256KiB_x1024", "sym16_256KiB_x1024"])
+def test_full_size_chunk_stream_kinds(bra, codec, orc, name):
+    """The same 1024-chunk stream for uniform-random and 16-symbol data."""
+    _chunk_stream_check(bra, codec, orc, name)
 
 
 @pytest.mark.parametrize("world,nblocks,tail", [(3, 10, 777), (8, 16, 0), (2, 3, CS - 1)])
