@@ -93,7 +93,15 @@ def cpu_sample_sizes(nb, bs, threads):
     return max(1, min(nb, (4 << 20) // bs)), max(1, min(nb, threads * max(1, (2 << 20) // bs)))
 
 
-def cpu_baseline(data_np, bs, threads, gpu_chunks):
+def cgroup_cpu_max() -> str:
+    """The cgroup v2 CPU quota of this process ("max 100000" = unlimited), or "unknown"."""
+    try:
+        return open("/sys/fs/cgroup/cpu.max").read().strip()
+    except OSError:
+        return "unknown"
+
+
+def cpu_baseline(data_np, bs, threads, gpu_chunks, all_host_cores=True):
     """The reference encoders on host cores (one block per task; ctypes drops the GIL), on a bounded
     sample of the benchmark's own blocks: single-threaded, then `threads` workers (skipped when the
     sample is one block, e.g. configs[0]'s single 64 KiB block)."""
@@ -117,6 +125,23 @@ def cpu_baseline(data_np, bs, threads, gpu_chunks):
         threads, many, dtm = 1, one, dt1
     chunks = many if nm >= n1 else one
     same = all((c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) == g for c, g in zip(chunks, gpu_chunks))
+    all_cores = None
+    if nm > 1 and all_host_cores:
+        # every host CPU this process may run on ("1-thread and all-host-cores"):
+        # one block per worker, as many blocks as workers (bounded by the batch)
+        na = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+        na_blocks = max(1, min(data_np.size // bs, na))
+        ins = blocks + [data_np[i * bs:(i + 1) * bs].tobytes() for i in range(len(blocks), na_blocks)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(min(na, na_blocks)) as ex:
+            res_all = list(ex.map(impl.encode_block, ins[:na_blocks]))
+        dta = time.perf_counter() - t0
+        ok_all = all((c.primary_index, c.lengths, c.orig_size, c.encoded_size, c.payload) ==
+                     (d.primary_index, d.lengths, d.orig_size, d.encoded_size, d.payload) for c, d in zip(res_all, chunks))
+        all_cores = {"value": round(na_blocks * bs / dta / 1e9, 6), "unit": "GB/s", "cores": min(na, na_blocks), "nproc": os.cpu_count(),
+                     "affinity_cpus": na, "cgroup_cpu_max": cgroup_cpu_max(),
+                     "sample": f"{na_blocks} x {bs} B blocks, one block per task on {min(na, na_blocks)} threads ({dta:.2f} s wall)",
+                     "same_output_as_16_thread_run": bool(ok_all)}
     return {
         "value": round(nm * bs / dtm / 1e9, 6),
         "unit": "GB/s",
@@ -128,6 +153,7 @@ def cpu_baseline(data_np, bs, threads, gpu_chunks):
                           "sample": f"{n1} x {bs} B blocks, {dt1:.2f} s", "seconds_per_block": round(dt1 / n1, 4)},
         "bit_exact_vs_gpu": bool(same),
         "blocks_checked": len(chunks),
+        "all_cores": all_cores,
     }
 
 
@@ -264,6 +290,7 @@ def main():
     step()
     torch.cuda.synchronize()
     prof0 = codec.prof_read()
+    kernel_slots = [s for s in kernel_slots if s in prof0]  # (a library built before a slot existed reports fewer)
     dominant = max(kernel_slots, key=lambda s: prof0[s][0])
     stage_slots = [s for s in codec.SLOTS if s.startswith("stage.")]
     timed_slots = enc_slots if args.profile_all else (dominant, *stage_slots)

@@ -999,16 +999,12 @@ __global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks
 //   k_hd_tail2   per block: the reference's end-of-stream walk (:455-498) on the intervals.
 // Any block that is not clean sends the batch to the tree-walking path above.
 // ------------------------------------------------------------------------------------------------
-#ifndef HD2_PAIRS
-#define HD2_PAIRS 1  // k_hd_trans walks the entries > 0 two at a time (3 or 4 in lockstep measured slower: occupancy)
-#endif
+// k_hd_trans walks the entries > 0 two at a time (one at a time, or 3 or 4 in lockstep, measured slower)
 constexpr uint32_t HD2_SEG   = 2048;  // bits per segment
 constexpr uint32_t HD2_LMAX  = 30;
 constexpr uint32_t HD2_TPB   = 256;
-#ifndef HD2_REFB_BITS
-#define HD2_REFB_BITS 512  // 64 / 128 / 256 / 512 / 1024: text decode 14.9 / 16.3 / 17.9 / 19.5 / 18.5 GB/s (registers)
-#endif
-constexpr uint32_t HD2_REFB  = HD2_REFB_BITS;  // boundary bitmap of the reference path (bits from the segment start)
+constexpr uint32_t HD2_REFB  = 512;   // boundary bitmap of the reference path (bits from the segment start;
+                                      // 64 / 128 / 256 / 512 / 1024: text decode 14.9 / 16.3 / 17.9 / 19.5 / 18.5 GB/s)
 constexpr uint32_t HD2_STRD  = 32;    // transfer words per segment
 constexpr uint32_t HD2_TAB   = 2304;  // u32 words per block table
 
@@ -1276,7 +1272,6 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
         }
         const uint32_t c0 = c, r0 = (bad << 31) | (((p - stop) & 31u) << 16);
         out[0]               = r0 | c0;
-#if HD2_PAIRS
         // the other entries two at a time in lockstep: both paths' window loads and LUT reads are
         // issued before either result is used (one path's step is a dependent load chain)
         for (uint32_t e = 1; e < nent; e += 2)
@@ -1344,50 +1339,6 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
             if (two)
                 out[e + 1] = rb;
         }
-#else
-        for (uint32_t e = 1; e < nent; ++e)
-        {
-            W.init(s + e);
-            p = s + e;
-            c = 0;
-            bad = 0;
-            bool merged = false;
-            while (p < stop)
-            {
-                const uint32_t d = p - s;
-                if (d < HD2_REFB)
-                {
-                    // hit test on the one bitmap word (a select chain), the rank only on a hit
-                    uint32_t wsel = 0;
-#pragma unroll
-                    for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
-                        wsel = (d >> 5) == (uint32_t) i ? bm[i] : wsel;
-                    if ((wsel >> (d & 31)) & 1u)
-                    {
-                        uint32_t rank = 0;
-#pragma unroll
-                        for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
-                        {
-                            const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
-                            rank += (uint32_t) __popc(bm[i] & m);
-                        }
-                        out[e] = r0 | (c + c0 - rank);
-                        merged = true;
-                        break;
-                    }
-                }
-                if (!hd2_dec(L, W.peek(p), len, sym) || len > nbits - p)
-                {
-                    bad = 1;
-                    break;
-                }
-                p += len;
-                ++c;
-            }
-            if (!merged)
-                out[e] = (bad << 31) | (((p - stop) & 31u) << 16) | c;
-        }
-#endif
     }
 }
 

@@ -430,6 +430,10 @@ struct WalkArgs
 };
 
 constexpr uint32_t IB_CHUNK = 256;
+#ifndef BRA_IB_WALK_WG
+#define BRA_IB_WALK_WG 2048
+#endif
+constexpr uint32_t IB_WALK_WG = BRA_IB_WALK_WG;  // persistent walk workgroups (EXPERIMENT: live splitters per XCD)
 
 __device__ __forceinline__ uint8_t* walk_dst(const WalkArgs& a, uint8_t* slot, uint32_t cap, uint32_t o, uint32_t& chunk, uint32_t g)
 {
@@ -917,7 +921,7 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
                 n += h_blocks[b].len;
             prof_bytes(P_DEC_IB_WALK, 5.0 * n);
         }
-        hipLaunchKernelGGL(k_ib_walk3, dim3(2048), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ib_walk3, dim3(IB_WALK_WG), dim3(256), 0, s, a);
     }
     hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
                        w.m_len, w.m_start, w.cyc, w.m_order, w.m_cnt);

@@ -434,10 +434,6 @@ __device__ __noinline__ uint32_t count_below(const uint32_t (&R)[NRD], uint32_t 
     return n;
 }
 
-#ifndef BRA_MTF_REG_FLAT
-#define BRA_MTF_REG_FLAT 1  // one branch-free path over the 8 table registers (0: 16-entry fast path + per-register branches)
-#endif
-#if BRA_MTF_REG_FLAT
 // One MTF step on the 32-entry register table: the symbol's position p = 4 k + b from the first
 // register holding a zero byte of R ^ c (k = 8: not among the first 32 entries -- a first
 // occurrence), then every register below k shifts up by one byte (v_alignbit) and register k
@@ -471,68 +467,6 @@ __device__ __forceinline__ uint32_t mtf_step_reg(uint32_t (&R)[NRD], uint32_t c)
     }
     return rank;
 }
-#else
-__device__ __forceinline__ uint32_t mtf_step_reg(uint32_t (&R)[NRD], uint32_t c)
-{
-    const uint32_t cc = c * 0x01010101u;
-    uint32_t       z[NRD];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        z[k] = haszero8(R[k] ^ cc);
-    const bool near = (z[0] | z[1] | z[2] | z[3]) != 0;
-    if (__builtin_amdgcn_ballot_w64(!near) == 0)
-    {
-        // every lane finds its symbol among the first 16 entries: shift only those
-        const uint32_t k = z[0] ? 0 : z[1] ? 1 : z[2] ? 2 : 3;
-        const uint32_t zz = z[0] ? z[0] : z[1] ? z[1] : z[2] ? z[2] : z[3];
-        const uint32_t b = (uint32_t) __builtin_ctz(zz) >> 3;
-        uint32_t       top = c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-        {
-            const uint32_t cur = R[q], ntop = cur >> 24;
-            if ((uint32_t) q < k)
-                R[q] = shift1(cur, top);
-            else if ((uint32_t) q == k)
-                R[q] = shift_upto(cur, top, b);
-            top = ntop;
-        }
-        return k * 4 + b;
-    }
-#pragma unroll
-    for (int k = 4; k < NRD; ++k)
-        z[k] = haszero8(R[k] ^ cc);
-    uint32_t k = NRD, zz = 0;
-#pragma unroll
-    for (int q = NRD - 1; q >= 0; --q)
-        if (z[q])
-        {
-            k  = (uint32_t) q;
-            zz = z[q];
-        }
-    uint32_t rank;
-    uint32_t b = 3;
-    if (k < (uint32_t) NRD)
-    {
-        b    = (uint32_t) __builtin_ctz(zz) >> 3;
-        rank = k * 4 + b;
-    }
-    else
-        rank = MTF_REG + c - count_below(R, c);  // first occurrence: an unseen value from behind the registers
-    uint32_t top = c;
-#pragma unroll
-    for (int q = 0; q < NRD; ++q)
-    {
-        const uint32_t cur = R[q], ntop = cur >> 24;
-        if ((uint32_t) q < k)
-            R[q] = shift1(cur, top);
-        else if ((uint32_t) q == k)
-            R[q] = shift_upto(cur, top, b);
-        top = ntop;
-    }
-    return rank;
-}
-#endif
 
 // The first MTF_REG entries of a segment's start table for a block of <= MTF_REG distinct symbols,
 // built by one wave: the seen symbols (last occurrence >= 0, at most MTF_REG of them) ordered by
@@ -929,9 +863,7 @@ __device__ __forceinline__ uint32_t count_less(uint32_t key, uint32_t q, uint64_
     return (uint32_t) __popc(ll) + (uint32_t) __popc(lh);
 }
 
-#ifndef BRA_MTF_REP_LOOP
-#define BRA_MTF_REP_LOOP 4  // repeats in a 64-symbol chunk counted one ballot each up to this many (random data: 0/4/8/16 -> 2.05/2.04/2.05/2.20 ms)
-#endif
+constexpr int MTF_REP_LOOP = 4;  // repeats in a 64-symbol chunk counted one ballot each up to this many (random data: 0/4/8/16 -> 2.05/2.04/2.05/2.20 ms)
 static_assert(MTF_SEG_ENC == 1024, "k_mtf_encode_wave stages a segment as 64 lanes x 16 bytes");
 
 __global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, const Piece* __restrict__ segs,
@@ -999,7 +931,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restri
                 const uint64_t fb = Fm & below;
                 rank              = p0 + (uint32_t) __popcll(fb) - count_less<8>(p0, p0, fb);
             }
-            if (__popcll(Am) > BRA_MTF_REP_LOOP)
+            if (__popcll(Am) > MTF_REP_LOOP)
             {
                 // many repeats: #{k in (j, i): nxt_k < i}, nxt in [1, 64] -> 7 bits
                 const uint64_t in_ji = below & (rep ? ~((2ull << j) - 1ull) : 0ull);

@@ -240,9 +240,6 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             __syncthreads();
 
             // ---- 3. walk the chain through this sub-window, compact it, write the output ----
-#ifdef RD_EXP_NOWALK
-            continue;  // measurement variant: phases 1 and 2 only (results are wrong)
-#endif
             const uint32_t ent = sub_entry[k];
             const uint32_t tot = sub_tot[k];
             const uint32_t ob0 = sub_out[k];
@@ -274,9 +271,6 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                 wave_lds_sync();
             }
             // output bytes [ob0, ob0 + tot) of the block: 16 per lane per round
-#ifdef RD_EXP_NOOUT
-            continue;  // measurement variant: no output (results are wrong)
-#endif
             for (uint32_t r0 = 0; r0 < tot; r0 += 64 * 16)
             {
                 const uint32_t o0 = r0 + lane * 16;  // relative to ob0

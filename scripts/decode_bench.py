@@ -29,5 +29,12 @@ for _ in range(args.reps):
     codec.decode(hdr, off, pay, args.total, args.block_size, out=out)
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / args.reps
+# one more decode with the decode slots timed
+codec.prof_enable(codec.slot_mask("dec.huffman", "dec.rle", "dec.mtf", "dec.ibwt", *codec.DECODE_KERNELS))
+codec.prof_reset()
+codec.decode(hdr, off, pay, args.total, args.block_size, out=out)
+torch.cuda.synchronize()
+prof = {k: round(v[0], 3) for k, v in codec.prof_read().items() if v[1]}
+codec.prof_enable(0)
 print(json.dumps({"kind": args.kind, "block_size": args.block_size, "decode_GBps": round(args.total / dt / 1e9, 4), "ms": round(dt * 1e3, 3),
-                  "roundtrip": ok}))
+                  "roundtrip": ok, "lib": os.path.basename(os.path.dirname(bra.LIB_PATH)), "slots_ms": prof}))

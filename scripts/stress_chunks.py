@@ -43,7 +43,8 @@ def one(codec, orc, D, name):
     st = stream.cpu().numpy().tobytes()
     bad = chunkdiag.records_vs_reference(st, w)
     if bad:
-        return f"ENCODE {len(bad)} records differ, first {bad[:8]}"
+        return f"ENCODE {len(bad)} records differ, first {bad[:8]}; " + "; ".join(
+            chunkdiag.encode_diagnosis(codec, orc, data, b, bs, total, st) for b in bad[:3])
     want = orc.chunks_crc32c(chunkdiag.headers_in_memory(st), data.tobytes(), CS)
     if crc != want:
         return f"ENCODE crc {crc:#x} != {want:#x}"
@@ -61,13 +62,14 @@ def one(codec, orc, D, name):
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    pre = int(sys.argv[2]) if len(sys.argv) > 2 else -1  # fixed prelude (-1: rotate through them)
     codec = bra.BlockCodec(0)
     orc = Oracle()
     D = chunkdiag.load_digests()
     fails = 0
     for r in range(rounds):
         t0 = time.time()
-        prelude(codec, r)
+        prelude(codec, r if pre < 0 else pre)
         res = {n: one(codec, orc, D, n) for n in ("text_256KiB_x1024", "sym16_256KiB_x1024")}
         fails += sum(not v.startswith("ok") for v in res.values())
         print(f"round {r}: {time.time() - t0:.1f} s {res}", flush=True)

@@ -89,3 +89,27 @@ def decode_diagnosis(codec, orc, data: np.ndarray, b: int, bs: int, total: int) 
     if d.size:
         return f"chunk {b}: MTF decode output differs at {d.size} bytes (first {d[:4].tolist()})"
     return f"chunk {b}: Huffman, RLE and MTF decode ok; inverse BWT output differs"
+
+
+def encode_diagnosis(codec, orc, data: np.ndarray, b: int, bs: int, total: int, stream: bytes) -> str:
+    """First encode stage of chunk b (of the codec's last encode, blocks at b * bs) whose output
+    differs from the oracle: BWT last column and primary index, MTF of the device's own BWT output,
+    then the record (RLE / Huffman)."""
+    lo, hi = b * bs, min(total, (b + 1) * bs)
+    blk = data[lo:hi].tobytes()
+    ref_L, ref_pi = orc.bwt_encode(blk)
+    recs = split_records(stream)
+    pi = recs[b][0] if b < len(recs) else -1
+    L = codec.stage_copy(0, total)[lo:hi]
+    d = np.flatnonzero(L != np.frombuffer(ref_L, np.uint8))
+    if d.size or pi != ref_pi:
+        return (f"chunk {b}: BWT differs (L at {d.size} bytes, first {d[:4].tolist()}; pi {pi} vs {ref_pi})")
+    M = codec.stage_copy(1, total)[lo:hi]
+    d = np.flatnonzero(M != np.frombuffer(orc.mtf_encode(L.tobytes()), np.uint8))
+    if d.size:
+        return f"chunk {b}: BWT ok; MTF differs at {d.size} bytes (first {d[:4].tolist()})"
+    ref = orc.encode_block(blk)
+    _, meta, pay = recs[b]
+    return (f"chunk {b}: BWT and MTF ok; record differs: lengths {'ok' if meta[:256] == ref.lengths else 'differ'}, "
+            f"sizes {int.from_bytes(meta[256:260], 'little'), int.from_bytes(meta[260:264], 'little')} vs {ref.orig_size, ref.encoded_size}, "
+            f"payload {'ok' if pay == ref.payload else 'differs'}")

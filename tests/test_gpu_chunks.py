@@ -235,7 +235,8 @@ def _chunk_stream_check(bra, codec, orc, name):
     stream, crc, compressed = codec.compress_chunks(d, CS)
     st = stream.cpu().numpy().tobytes()
     bad = chunkdiag.records_vs_reference(st, w)
-    assert not bad, f"encode: {len(bad)} of {nb} chunk records differ from the reference, first {bad[:8]}"
+    assert not bad, (f"encode: {len(bad)} of {nb} chunk records differ from the reference, first {bad[:8]}; "
+                     + "; ".join(chunkdiag.encode_diagnosis(codec, orc, data, b, bs, total, st) for b in bad[:3]))
     assert compressed == (len(st) < total)
     assert crc == orc.chunks_crc32c(chunkdiag.headers_in_memory(st), data.tobytes(), CS), "encode: chunk-stream CRC"
     if not compressed:
