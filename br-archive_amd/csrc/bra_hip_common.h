@@ -277,6 +277,11 @@ __device__ __forceinline__ uint32_t xlane(uint32_t x)
     }
 }
 
+// Every compare-exchange string writes VCC and, through its s_xnor_b64, SCC: both are declared
+// clobbered.  (Without "scc" the compiler kept a lane-mask select's SCC live across the string and
+// the s_cselect after it picked the mask from the xnor's result instead -- a network stage with the
+// inverted direction whenever the xnor came out zero, i.e. for some key sets only: the intermittent
+// wrong BWT blocks, found by replaying a failing job sort phase by phase, scripts/rerun_jobs.py.)
 // 128-bit keys as four dwords (k0 lowest).  k > o is the borrow out of the 128-bit subtraction
 // o - k: four chained VALU subtractions into VCC, so a compare-exchange is 4 subtractions, one SALU
 // xnor with a lane mask and 4 selects (the C++ form compiles to three 64-bit compares, SALU
@@ -299,7 +304,7 @@ __device__ __forceinline__ void cx128(uint32_t& k0, uint32_t& k1, uint32_t& k2, 
         "v_cndmask_b32 %[k3], %[k3], %[o3], vcc"
         : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1), [k2] "+v"(k2), [k3] "+v"(k3)
         : [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2), [o3] "v"(o3), [km] "s"(keep_min)
-        : "vcc");
+        : "vcc", "scc");
 }
 
 // In-lane compare-exchange of keys a and b: afterwards a < b in the lanes set in `asc`, a > b in
@@ -325,7 +330,7 @@ __device__ __forceinline__ void cx128_pair(uint32_t& a0, uint32_t& a1, uint32_t&
         : [t] "=&v"(t), [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [n3] "=&v"(n3), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2),
           [m3] "=&v"(m3)
         : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [a3] "v"(a3), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [b3] "v"(b3), [asc] "s"(asc)
-        : "vcc");
+        : "vcc", "scc");
     a0 = n0, a1 = n1, a2 = n2, a3 = n3;
     b0 = m0, b1 = m1, b2 = m2, b3 = m3;
 }
@@ -345,7 +350,7 @@ __device__ __forceinline__ void cx96(uint32_t& k0, uint32_t& k1, uint32_t& k2, u
         "v_cndmask_b32 %[k2], %[k2], %[o2], vcc"
         : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1), [k2] "+v"(k2)
         : [o0] "v"(o0), [o1] "v"(o1), [o2] "v"(o2), [km] "s"(keep_min)
-        : "vcc");
+        : "vcc", "scc");
 }
 
 __device__ __forceinline__ void cx96_pair(uint32_t& a0, uint32_t& a1, uint32_t& a2, uint32_t& b0, uint32_t& b1, uint32_t& b2, uint64_t asc)
@@ -364,7 +369,7 @@ __device__ __forceinline__ void cx96_pair(uint32_t& a0, uint32_t& a1, uint32_t& 
         "v_cndmask_b32 %[m2], %[b2], %[a2], vcc"
         : [t] "=&v"(t), [n0] "=&v"(n0), [n1] "=&v"(n1), [n2] "=&v"(n2), [m0] "=&v"(m0), [m1] "=&v"(m1), [m2] "=&v"(m2)
         : [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2), [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [asc] "s"(asc)
-        : "vcc");
+        : "vcc", "scc");
     a0 = n0, a1 = n1, a2 = n2;
     b0 = m0, b1 = m1, b2 = m2;
 }
@@ -382,7 +387,7 @@ __device__ __forceinline__ void cx64(uint32_t& k0, uint32_t& k1, uint32_t o0, ui
         "v_cndmask_b32 %[k1], %[k1], %[o1], vcc"
         : [t] "=&v"(t), [k0] "+v"(k0), [k1] "+v"(k1)
         : [o0] "v"(o0), [o1] "v"(o1), [km] "s"(keep_min)
-        : "vcc");
+        : "vcc", "scc");
 }
 
 __device__ __forceinline__ void cx64_pair(uint32_t& a0, uint32_t& a1, uint32_t& b0, uint32_t& b1, uint64_t asc)
@@ -398,15 +403,14 @@ __device__ __forceinline__ void cx64_pair(uint32_t& a0, uint32_t& a1, uint32_t& 
         "v_cndmask_b32 %[m1], %[b1], %[a1], vcc"
         : [t] "=&v"(t), [n0] "=&v"(n0), [n1] "=&v"(n1), [m0] "=&v"(m0), [m1] "=&v"(m1)
         : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1), [asc] "s"(asc)
-        : "vcc");
+        : "vcc", "scc");
     a0 = n0, a1 = n1;
     b0 = m0, b1 = m1;
 }
 
 // (Folding the lane exchange into the compare-exchange as DPP source operands -- v_sub_co / v_subb_co /
-// v_cndmask with a DPP src0, 4 VALU instead of 6 -- sorted wrongly now and then: one 8 MiB sym16
-// block of 32 differed from the reference in 4 of 6 identical runs, with s_nops around the block
-// or not; the separate DPP moves stay.)
+// v_cndmask with a DPP src0, 4 VALU instead of 6 -- sorted wrongly now and then in round 3; that was
+// most likely the missing scc clobber above, not the DPP form.)
 template <int LM>
 __device__ __forceinline__ uint64_t xlane64(uint64_t x)
 {

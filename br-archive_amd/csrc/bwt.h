@@ -12,6 +12,10 @@ void          bwt_workspace_destroy(BwtWorkspace* w);
 // Per block (after bwt_encode_device): 256-bit presence mask of its byte values, 8 dwords each (the
 // BWT output has the same bytes, so the MTF stage takes its alphabets from here).
 const uint32_t* bwt_alpha_masks(const BwtWorkspace* w);
+// The suffix-array slots of the last encode (u32 per element at the block offsets; diagnostics).
+const uint32_t* bwt_sa(const BwtWorkspace* w);
+// Diagnostics (BRA_JOB_AUDIT builds, else -1): re-run and audit the last encode's job phase.
+int bwt_debug_rerun_jobs(BwtWorkspace* w, int reps, hipStream_t s, uint32_t shuffle_seed);
 
 // BWT of every block: d_L[off..off+len) = last column, d_pi[b] = primary index (block-local).
 bool bwt_encode_device(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,

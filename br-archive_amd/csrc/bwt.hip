@@ -2221,6 +2221,16 @@ __device__ __forceinline__ void net_stage_lanes(uint32_t (&k)[KD][4], uint64_t k
 // pair in the lower rows, r1's in the upper rows, the lower slot in the first register), an
 // in-lane compare-exchange orders it, and the same swap puts the elements back: 7.5 VALU per
 // element instead of 18 with per-dword partner fetches.
+// Rows of x and y exchanged as the permlane swap does (LM 16: x's odd rows <-> y's even rows; 32: x's
+// upper half <-> y's lower half).
+template <int LM>
+__device__ __forceinline__ void swap_rows(uint32_t& x, uint32_t& y)
+{
+    const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(x, y, false, false) : __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = t[0];
+    y = t[1];
+}
+
 template <int LM, int KD>
 __device__ __forceinline__ void net_stage_swap(uint32_t (&k)[KD][4], uint64_t asc)
 {
@@ -2231,19 +2241,17 @@ __device__ __forceinline__ void net_stage_swap(uint32_t (&k)[KD][4], uint64_t as
 #pragma unroll
         for (int i = 0; i < KD; ++i)
         {
-            const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(k[i][q], k[i][q + 1], false, false)
-                                      : __builtin_amdgcn_permlane32_swap(k[i][q], k[i][q + 1], false, false);
-            a[i] = t[0];
-            b[i] = t[1];
+            a[i] = k[i][q];
+            b[i] = k[i][q + 1];
+            swap_rows<LM>(a[i], b[i]);
         }
         cxk_pair<KD>(a, b, asc);
 #pragma unroll
         for (int i = 0; i < KD; ++i)
         {
-            const auto t = (LM == 16) ? __builtin_amdgcn_permlane16_swap(a[i], b[i], false, false)
-                                      : __builtin_amdgcn_permlane32_swap(a[i], b[i], false, false);
-            k[i][q]     = t[0];
-            k[i][q + 1] = t[1];
+            swap_rows<LM>(a[i], b[i]);
+            k[i][q]     = a[i];
+            k[i][q + 1] = b[i];
         }
     }
 }
@@ -2390,11 +2398,22 @@ __device__ __forceinline__ void merge_level(uint32_t (&k)[2][4], JobLds<W>& S, u
 // permlane partners), then (W > 1, P > 256) merge-path levels across the waves.  Keys are unique
 // (the slot is in the low bits).  The network runs on dwords (no 64-bit register pairs to keep
 // together).
+#ifdef BRA_JOB_AUDIT
+__device__ uint32_t g_sort_fail;           // job sorts whose output was not strictly ascending (padding aside)
+__device__ uint32_t g_sort_owner = ~0u;     // workgroup that dumped the first one
+__device__ uint64_t g_sort_dump[2][1024];   // its input and output keys (slot order)
+__device__ uint32_t g_sort_meta[4];         // W, P, the wave's xcc, the sort's index in its job
+__device__ uint64_t g_sort_phase[10][1024];  // the failing sort re-run: keys after each phase
+#endif
+
 template <int W>
 __device__ __forceinline__ void job_sort(uint64_t (&key)[4], int P, JobLds<W>& S, int wj)
 {
     const int      lane = lane_id();
     const uint32_t e0   = wj * 256 + lane * 4;
+#ifdef BRA_JOB_AUDIT
+    const uint64_t kin[4] = {key[0], key[1], key[2], key[3]};
+#endif
     uint32_t       k[2][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -2437,6 +2456,82 @@ __device__ __forceinline__ void job_sort(uint64_t (&key)[4], int P, JobLds<W>& S
     for (int r = 0; r < 4; ++r)
         key[r] = ((uint64_t) k[1][r] << 32) | k[0][r];
     job_sync<W>();
+#ifdef BRA_JOB_AUDIT
+    {
+        // strictly ascending real keys over the first P slots (real keys carry their slot: unique)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            S.kh[e0 + r] = key[r];
+        job_sync<W>();
+        bool bad = false;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = e0 + r;
+            if (c + 1 < (uint32_t) P && key[r] != ~0ull && !(S.kh[c + 1] > key[r]))
+                bad = true;
+        }
+        bad = job_any<W>(bad);
+        if (bad)
+        {
+            if (threadIdx.x == 0)
+            {
+                atomicAdd(&g_sort_fail, 1u);
+                S.agg[0] = atomicCAS(&g_sort_owner, ~0u, blockIdx.x) == ~0u ? 1u : 0u;
+            }
+            job_sync<W>();
+            if (S.agg[0])
+            {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    g_sort_dump[0][e0 + r] = kin[r];
+                    g_sort_dump[1][e0 + r] = key[r];
+                }
+                // the same sort again from kin, with the keys after every phase
+                uint32_t kk[2][4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    kk[0][r] = (uint32_t) kin[r];
+                    kk[1][r] = (uint32_t) (kin[r] >> 32);
+                }
+                int ph = 0;
+                for (int size = 2; size <= P; size <<= 1, ++ph)
+                {
+                    if (!(dead && size <= 256))
+                    {
+                        if constexpr (W > 1)
+                            if (size > 256)
+                                merge_level<W>(kk, S, e0, (uint32_t) size / 2);
+                        if (size <= 256)
+                            switch (size)
+                            {
+                            case 2: net_phase<W, 2, 2>(kk, S, el); break;
+                            case 4: net_phase<W, 2, 4>(kk, S, el); break;
+                            case 8: net_phase<W, 2, 8>(kk, S, el); break;
+                            case 16: net_phase<W, 2, 16>(kk, S, el); break;
+                            case 32: net_phase<W, 2, 32>(kk, S, el); break;
+                            case 64: net_phase<W, 2, 64>(kk, S, el); break;
+                            case 128: net_phase<W, 2, 128>(kk, S, el); break;
+                            default: net_phase<W, 2, 256>(kk, S, el); break;
+                            }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        g_sort_phase[ph][e0 + r] = ((uint64_t) kk[1][r] << 32) | kk[0][r];
+                }
+                if (threadIdx.x == 0)
+                {
+                    g_sort_meta[0] = W;
+                    g_sort_meta[1] = (uint32_t) P;
+                    g_sort_meta[2] = xcc_id();
+                }
+            }
+        }
+        job_sync<W>();
+    }
+#endif
 }
 
 // Group heads, group starts (g: max-scan of the head positions) and ties over the T active slots
@@ -2953,6 +3048,175 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
     if (wj == 0)
         JT_FLUSH(1);
 }
+
+// ---- diagnostics: the job sort (network + merge levels) alone, on random keys ----
+// Every workgroup sorts `iters` random key sets of T in [1, 256 W] elements (the job kernels' key
+// layout: rotation bits above LOGS slot bits, padding all ones, a small key range so that keys
+// share their high bits as tied rotations do) and checks that the T real slots come out ascending
+// and as a permutation.  err[0] counts failing sorts.
+__device__ __forceinline__ uint32_t sn_hash(uint32_t x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+template <int W>
+__global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_sortnet_test(uint32_t seed, uint32_t iters, uint32_t* __restrict__ err,
+                                                                        const uint64_t* __restrict__ kfix, uint32_t tfix)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    JobLds<W>&     S    = *reinterpret_cast<JobLds<W>*>(smem);
+    using G             = JobGeom<W>;
+    const int      wj   = threadIdx.x >> 6, lane = lane_id();
+    uint32_t       bad  = 0;
+    for (uint32_t it = 0; it < iters; ++it)
+    {
+        const uint32_t h  = sn_hash(seed ^ (blockIdx.x * 7919u) ^ (it * 104729u));
+        const uint32_t T  = kfix ? tfix : 1 + h % (256u * W);
+        const uint32_t hb = 1u + (h >> 20) % 40u;  // key bits above the slot that vary
+        int            P  = 4;
+        while ((uint32_t) P < T)
+            P <<= 1;
+        uint64_t key[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            const uint64_t x = ((uint64_t) sn_hash(h + 2 * c + 1) << 32 | sn_hash(h ^ (3 * c + 7))) & ((1ull << hb) - 1);
+            key[r]           = kfix ? kfix[c] : c < T ? ((x << (64 - hb)) & ~G::SMASK) | c : ~0ull;
+            S.v[c]           = 0;
+        }
+        job_sort<W>(key, P, S, wj);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            S.kh[c]          = key[r];
+            if (c < T)
+                atomicAdd(&S.v[(uint32_t) (key[r] & G::SMASK) & (256u * W - 1)], 1u);
+        }
+        __syncthreads();
+        uint32_t b = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const uint32_t c = wj * 256 + lane * 4 + r;
+            if (c < T)
+                b |= (S.v[c] != 1u) || (c + 1 < T && S.kh[c] >= S.kh[c + 1]) || (c + 1 == T && T < 256u * W && S.kh[c + 1] != ~0ull);
+        }
+        bad += __syncthreads_or(b) ? 1u : 0u;
+    }
+    if (threadIdx.x == 0 && bad)
+        atomicAdd(err, bad);
+}
+
+#ifdef BRA_JOB_AUDIT
+// ---- diagnostics (make EXTRA=-DBRA_JOB_AUDIT): after the STRING jobs, every job's slots are
+// counted (a slot two jobs cover is a race between them) and every job's output rotations are
+// checked against its input payloads (sum and xor of the rotation indices); violations are
+// printed, at most 32 per call. ----
+__device__ uint32_t g_audit_prints;
+__device__ uint32_t g_audit_fail;
+__global__ void k_audit_cover(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t* __restrict__ cnt)
+{
+    const uint32_t n = dev_count(pn);
+    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x)
+    {
+        const Job J = jobs[j];
+        for (uint32_t c = threadIdx.x; c < J.len; c += blockDim.x)
+            atomicAdd(&cnt[J.start + c], 1u);
+    }
+}
+__global__ void k_audit_check(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t kind, const uint64_t* __restrict__ key0,
+                              const uint64_t* __restrict__ key1, const uint32_t* __restrict__ fsa, const uint32_t* __restrict__ cnt,
+                              const BlockDesc* __restrict__ blocks)
+{
+    __shared__ uint32_t s_in, s_out, x_in, x_out, over;
+    const uint32_t n = dev_count(pn);
+    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x)
+    {
+        if (threadIdx.x == 0)
+            s_in = s_out = x_in = x_out = over = 0;
+        __syncthreads();
+        const Job       J = jobs[j];
+        const uint64_t* K = J.buf ? key1 : key0;
+        for (uint32_t c = threadIdx.x; c < J.len; c += blockDim.x)
+        {
+            const uint32_t a = (uint32_t) K[J.start + c] & 0xFFFFFFu, b = fsa[J.start + c];
+            atomicAdd(&s_in, a);
+            atomicAdd(&s_out, b);
+            atomicXor(&x_in, a);
+            atomicXor(&x_out, b);
+            if (cnt[J.start + c] != 1u)
+                atomicAdd(&over, 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && (s_in != s_out || x_in != x_out || over))
+        {
+            atomicAdd(&g_audit_fail, 1u);
+            const uint32_t p = atomicAdd(&g_audit_prints, 1u);
+            if (p < 32)
+                printf("[bwt audit] %s job %u block %u (off %llu): start %u len %u kd %u buf %u d %u gdepth %u: in sum/xor %u/%u out %u/%u, %u slots shared\n",
+                       kind ? "wg" : "wave", j, J.block, (unsigned long long) blocks[J.block].off, J.start, J.len, J.kd, J.buf, J.d, J.gdepth, s_in,
+                       x_in, s_out, x_out, over);
+        }
+        __syncthreads();
+    }
+}
+
+// Re-runs with another input order: the payloads of every job are put in ascending rotation order
+// and then permuted by the ranks of h(seed ^ start * 2654435761, i) (ties by i), so the host can
+// rebuild the exact order a failing job saw.  One workgroup (1024 threads) per job.
+__device__ __forceinline__ uint32_t au_hash(uint32_t x)
+{
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+__global__ void __launch_bounds__(1024) k_audit_shuffle(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint64_t* __restrict__ key0,
+                                                        uint64_t* __restrict__ key1, uint32_t seed)
+{
+    __shared__ uint64_t pl[1024];
+    __shared__ uint32_t hk[1024];
+    const uint32_t n = dev_count(pn);
+    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x)
+    {
+        const Job J   = jobs[j];
+        uint64_t* K   = J.buf ? key1 : key0;
+        const uint32_t len = min(J.len, 1024u), t = threadIdx.x;
+        if (t < len)
+        {
+            pl[t] = K[J.start + t];
+            hk[t] = au_hash(seed ^ (J.start * 2654435761u) ^ au_hash(t + 1));
+        }
+        __syncthreads();
+        uint32_t dst = 0;
+        if (t < len)
+        {
+            // canonical rank of element t (ascending rotation index), then the slot the permutation gives that rank
+            uint32_t cr = 0;
+            const uint32_t me = (uint32_t) pl[t] & 0xFFFFFFu;
+            for (uint32_t i = 0; i < len; ++i)
+                cr += ((uint32_t) pl[i] & 0xFFFFFFu) < me;
+            const uint32_t hc = hk[cr];
+            for (uint32_t i = 0; i < len; ++i)
+                dst += hk[i] < hc || (hk[i] == hc && i < cr);
+        }
+        const uint64_t mine = t < len ? pl[t] : 0;
+        __syncthreads();
+        if (t < len)
+            K[J.start + dst] = mine;
+        __syncthreads();
+    }
+}
+#endif
 
 // Workgroup-job size classes: a job of (256, 512] elements runs on 2 waves, (512, 1024] on 4 (never
 // more waves than the job's network needs).
@@ -3574,6 +3838,7 @@ static void ws_free(BwtWorkspace& w)
 
 BwtWorkspace* bwt_workspace_create() { return new BwtWorkspace(); }
 const uint32_t* bwt_alpha_masks(const BwtWorkspace* w) { return w ? w->amask : nullptr; }
+const uint32_t* bwt_sa(const BwtWorkspace* w) { return w ? w->fsa : nullptr; }
 void          bwt_workspace_destroy(BwtWorkspace* w)
 {
     if (w)
@@ -3793,6 +4058,100 @@ static bool account_levels(BwtWorkspace& w, hipStream_t s)
     return true;
 }
 
+#ifdef BRA_JOB_AUDIT
+static JobPhase g_last_ph;
+static uint64_t g_last_n = 0;
+
+// The job audit (k_audit_cover / k_audit_check) of the jobs in the lists; returns the number of
+// failing jobs (-1 on a HIP error).
+static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hipStream_t s)
+{
+    static uint32_t* cnt = nullptr;
+    static uint64_t  cap = 0;
+    if (N > cap)
+    {
+        (void) hipFree(cnt);
+        if (hipMalloc(&cnt, N * 4) != hipSuccess)
+            return -1;
+        cap = N;
+    }
+    static const uint32_t zero = 0;
+    uint32_t              fails = 0;
+    if (hipMemsetAsync(cnt, 0, N * 4, s) != hipSuccess ||
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(g_audit_prints), &zero, 4, 0, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(g_audit_fail), &zero, 4, 0, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_audit_cover, dim3(4096), dim3(256), 0, s, w.jobs, &w.ctr[0].n_jobs, cnt);
+    hipLaunchKernelGGL(k_audit_cover, dim3(4096), dim3(256), 0, s, w.mjobs, &w.ctr[0].n_mjobs, cnt);
+    hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.jobs, &w.ctr[0].n_jobs, 0u, w.key[0], w.key[1], w.fsa, cnt, d_blocks);
+    hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.mjobs, &w.ctr[0].n_mjobs, 1u, w.key[0], w.key[1], w.fsa, cnt, d_blocks);
+    if (hipStreamSynchronize(s) != hipSuccess || hipMemcpyFromSymbol(&fails, HIP_SYMBOL(g_audit_fail), 4) != hipSuccess)
+        return -1;
+    uint32_t sf = 0;
+    if (hipMemcpyFromSymbol(&sf, HIP_SYMBOL(g_sort_fail), 4) != hipSuccess)
+        return -1;
+    if (sf)
+    {
+        static bool dumped = false;
+        fprintf(stderr, "[bwt audit] %u job sorts not ascending\n", sf);
+        if (!dumped)
+        {
+            dumped = true;
+            static uint64_t dump[2][1024];
+            uint32_t        meta[4];
+            if (hipMemcpyFromSymbol(dump, HIP_SYMBOL(g_sort_dump), sizeof dump) == hipSuccess &&
+                hipMemcpyFromSymbol(meta, HIP_SYMBOL(g_sort_meta), sizeof meta) == hipSuccess)
+            {
+                const char* dir = getenv("BRA_DIAG_DIR");
+                char        path[512];
+                snprintf(path, sizeof path, "%s/sort_dump.bin", dir ? dir : ".");
+                static uint64_t phases[10][1024];
+                if (hipMemcpyFromSymbol(phases, HIP_SYMBOL(g_sort_phase), sizeof phases) != hipSuccess)
+                    return -1;
+                if (FILE* f = fopen(path, "wb"))
+                {
+                    fwrite(meta, 4, 4, f);
+                    fwrite(dump, 8, 2 * 1024, f);
+                    fwrite(phases, 8, 10 * 1024, f);
+                    fclose(f);
+                    fprintf(stderr, "[bwt audit] first failing sort (W %u, P %u, xcc %u) dumped to %s\n", meta[0], meta[1], meta[2], path);
+                }
+            }
+        }
+        const uint32_t z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sort_fail), &z, 4) != hipSuccess)
+            return -1;
+    }
+    return (int) fails;
+}
+
+// Re-runs the job phase of the last STRING encode `reps` times on the unchanged lists and payloads
+// (the jobs only read them) and audits every run; returns the failing jobs summed over the runs.
+int bwt_debug_rerun_jobs(BwtWorkspace* wp, int reps, hipStream_t s, uint32_t seed)
+{
+    if (!g_last_n)
+        return -1;
+    int total = 0;
+    for (int r = 0; r < reps; ++r)
+    {
+        if (seed)
+        {
+            hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->jobs, &wp->ctr[0].n_jobs, wp->key[0], wp->key[1], seed + (uint32_t) r);
+            hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->mjobs, &wp->ctr[0].n_mjobs, wp->key[0], wp->key[1], seed + (uint32_t) r);
+        }
+        if (!run_jobs(*wp, g_last_ph, s))
+            return -1;
+        const int f = audit_jobs(*wp, g_last_n, g_last_ph.ja.blocks, s);
+        if (f < 0)
+            return -1;
+        total += f;
+    }
+    return total;
+}
+#else
+int bwt_debug_rerun_jobs(BwtWorkspace*, int, hipStream_t, uint32_t) { return -1; }
+#endif
+
 bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s)
 {
@@ -3935,6 +4294,12 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     if (!run_jobs(w, ph, s))
         return false;
     BRA_HIP_CHECK(hipGetLastError());
+#ifdef BRA_JOB_AUDIT
+    g_last_ph = ph;
+    g_last_n  = N;
+    if (audit_jobs(w, N, d_blocks, s) < 0)
+        return false;
+#endif
     if (!account_levels<MODE_STRING>(w, s))
         return false;
     static const bool level_stats = getenv("BRA_LEVEL_STATS") != nullptr;  // diagnostic: per-level counts to stderr
@@ -4093,3 +4458,38 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
 }
 
 }  // namespace bra
+
+// Diagnostics: run the job sort of W waves (1, 2 or 4) on `groups` workgroups x `iters` random key
+// sets (k_sortnet_test); returns the number of failing sorts, or -1 on a launch error.
+// With keys (host array of 256 * waves keys in slot order, padding = all ones), every sort uses them.
+extern "C" int bra_gpu_sortnet_selftest(int waves, unsigned groups, unsigned iters, unsigned seed, const unsigned long long* keys)
+{
+    using namespace bra;
+    uint32_t* d = nullptr;
+    uint64_t* dk = nullptr;
+    uint32_t  h = 0, tfix = 0;
+    if (hipMalloc(&d, 4) != hipSuccess)
+        return -1;
+    if (keys)
+    {
+        for (int c = 0; c < 256 * waves; ++c)
+            tfix += keys[c] != ~0ull;
+        if (hipMalloc(&dk, 256 * 4 * 8) != hipSuccess || hipMemcpy(dk, keys, 256 * waves * 8, hipMemcpyHostToDevice) != hipSuccess)
+            return -1;
+    }
+    int rc = -1;
+    if (hipMemset(d, 0, 4) == hipSuccess)
+    {
+        if (waves == 1)
+            hipLaunchKernelGGL(k_sortnet_test<1>, dim3(groups), dim3(64), sizeof(JobLds<1>), 0, seed, iters, d, dk, tfix);
+        else if (waves == 2)
+            hipLaunchKernelGGL(k_sortnet_test<2>, dim3(groups), dim3(128), sizeof(JobLds<2>), 0, seed, iters, d, dk, tfix);
+        else
+            hipLaunchKernelGGL(k_sortnet_test<4>, dim3(groups), dim3(256), sizeof(JobLds<4>), 0, seed, iters, d, dk, tfix);
+        if (hipGetLastError() == hipSuccess && hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost) == hipSuccess)
+            rc = (int) std::min<uint32_t>(h, 0x7FFFFFFF);
+    }
+    (void) hipFree(d);
+    (void) hipFree(dk);
+    return rc;
+}

@@ -995,8 +995,20 @@ const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)
     case 2: return c->d_rle;
     case 3: return c->d_enc_rle_base;  // RLE output bases of the last batch encode
     case 4: return c->d_rle_size;
+    case 5: return bwt_sa(c->bwt);  // BWT suffix-array slots of the last batch encode (diagnostics)
     default: return nullptr;
     }
+}
+
+// Diagnostics: re-run the job phase of the last batch encode `reps` times (each time with the jobs'
+// inputs in another order when shuffle_seed != 0) and audit it (builds with
+// -DBRA_JOB_AUDIT; -1 otherwise).  Returns the failing jobs summed over the runs.
+int bra_gpu_debug_rerun_jobs(bra_gpu_ctx_t* c, int reps, unsigned shuffle_seed)
+{
+    if (!c)
+        return -1;
+    DevGuard dg(c->device);
+    return bwt_debug_rerun_jobs(c->bwt, reps, c->stream, shuffle_seed);
 }
 
 const char* bra_gpu_version(void) { return "bra_hip 0.1.0 (gfx950)"; }

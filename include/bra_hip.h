@@ -240,7 +240,9 @@ int bra_gpu_assemble_shards(bra_gpu_ctx_t* ctx, uint32_t nparts, const bra_io_ch
 /*
  * Device pointers to the intermediate stage outputs of the last bra_gpu_encode_blocks call (for
  * parity tests): 0 = BWT last column (total bytes), 1 = MTF (total bytes), 2 = RLE output (block b
- * at byte offset rle_base[b]), 3 = rle_base (uint64_t[nblocks]), 4 = RLE sizes (uint32_t[nblocks]).
+ * at byte offset rle_base[b]), 3 = rle_base (uint64_t[nblocks]), 4 = RLE sizes (uint32_t[nblocks]),
+ * 5 = BWT suffix-array slots (uint32_t per input byte, block-local rotation indices at the block
+ * offsets).
  */
 const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* ctx, int stage);
 

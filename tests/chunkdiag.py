@@ -91,6 +91,69 @@ def decode_diagnosis(codec, orc, data: np.ndarray, b: int, bs: int, total: int) 
     return f"chunk {b}: Huffman, RLE and MTF decode ok; inverse BWT output differs"
 
 
+def cyclic_sa(blk: np.ndarray) -> np.ndarray:
+    """Sorted cyclic rotations of blk (ties by index, as the reference's stable qsort_r): prefix
+    doubling over ranks with numpy (a 256 KiB block takes well under a second)."""
+    n = blk.size
+    rank = blk.astype(np.int64)
+    sa = np.argsort(rank, kind="stable")
+    k = 1
+    while k < n:
+        key2 = rank[(np.arange(n) + k) % n]
+        sa = np.lexsort((np.arange(n), key2, rank))
+        r1, r2 = rank[sa], key2[sa]
+        head = np.empty(n, bool)
+        head[0] = True
+        head[1:] = (r1[1:] != r1[:-1]) | (r2[1:] != r2[:-1])
+        new = np.empty(n, np.int64)
+        new[sa] = np.cumsum(head) - 1
+        rank = new
+        if head.all():
+            break
+        k *= 2
+    return sa
+
+
+def _lcp(blk: np.ndarray, i: int, j: int, cap: int = 4096) -> int:
+    n = blk.size
+    for t in range(min(cap, n)):
+        if blk[(i + t) % n] != blk[(j + t) % n]:
+            return t
+    return cap
+
+
+def sa_diagnosis(codec, blk: np.ndarray, lo: int, total: int, save: str | None = None) -> str:
+    """Where the device's suffix array of a block (stage 5, u32 per element at the block offset)
+    departs from the reference order: whether it is still a permutation (a data-movement error
+    loses or duplicates rotations; a sort error only misorders them), the span of the differing
+    slots and the common-prefix depths there (which MSD level / job size the span belongs to)."""
+    n = blk.size
+    sa_dev = codec.stage_copy(5, 4 * total).view(np.uint32)[lo:lo + n].astype(np.int64)
+    sa_ref = cyclic_sa(blk)
+    d = np.flatnonzero(sa_dev != sa_ref)
+    if not d.size:
+        return "SA equal (L / pi written wrongly after the sort)"
+    perm = np.array_equal(np.sort(sa_dev), np.arange(n))
+    a, z = int(d[0]), int(d[-1])
+    # the group of slots sharing the span's common prefix in the reference order: its size tells
+    # the job class (<= 256 wave job, <= 1024 workgroup job) that sorted it
+    dep = min(_lcp(blk, int(sa_ref[a]), int(sa_ref[z])), 4096)
+    g0, g1 = a, z
+    while g0 > 0 and _lcp(blk, int(sa_ref[g0 - 1]), int(sa_ref[a])) >= dep:
+        g0 -= 1
+    while g1 + 1 < n and _lcp(blk, int(sa_ref[g1 + 1]), int(sa_ref[a])) >= dep:
+        g1 += 1
+    inner = [_lcp(blk, int(sa_ref[i]), int(sa_ref[i + 1])) for i in range(a, min(z, a + 64))]
+    msg = (f"SA {d.size} slots differ in [{a}, {z}] ({'permutation' if perm else 'NOT a permutation'}); "
+           f"common prefix of the span {dep} bytes, group of that prefix [{g0}, {g1}] ({g1 - g0 + 1} slots); "
+           f"adjacent lcps in span min {min(inner) if inner else -1} max {max(inner) if inner else -1}; "
+           f"dev slots {sa_dev[a:a + 6].tolist()} ref {sa_ref[a:a + 6].tolist()}")
+    save = save or (os.path.join(os.environ["BRA_DIAG_DIR"], f"sa_{lo}.npz") if os.environ.get("BRA_DIAG_DIR") else None)
+    if save:
+        np.savez_compressed(save, blk=blk, sa_dev=sa_dev, sa_ref=sa_ref)
+    return msg
+
+
 def encode_diagnosis(codec, orc, data: np.ndarray, b: int, bs: int, total: int, stream: bytes) -> str:
     """First encode stage of chunk b (of the codec's last encode, blocks at b * bs) whose output
     differs from the oracle: BWT last column and primary index, MTF of the device's own BWT output,
@@ -103,7 +166,8 @@ def encode_diagnosis(codec, orc, data: np.ndarray, b: int, bs: int, total: int, 
     L = codec.stage_copy(0, total)[lo:hi]
     d = np.flatnonzero(L != np.frombuffer(ref_L, np.uint8))
     if d.size or pi != ref_pi:
-        return (f"chunk {b}: BWT differs (L at {d.size} bytes, first {d[:4].tolist()}; pi {pi} vs {ref_pi})")
+        return (f"chunk {b}: BWT differs (L at {d.size} bytes, first {d[:4].tolist()}; pi {pi} vs {ref_pi}); "
+                + sa_diagnosis(codec, data[lo:hi], lo, total))
     M = codec.stage_copy(1, total)[lo:hi]
     d = np.flatnonzero(M != np.frombuffer(orc.mtf_encode(L.tobytes()), np.uint8))
     if d.size:
