@@ -40,6 +40,7 @@ ABI_SYMBOLS = (
     "bra_gpu_frame_chunks", "bra_gpu_unframe_chunks", "bra_gpu_compress_chunks", "bra_gpu_decompress_chunks",
     "bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host",
     "bra_gpu_chunks_crc32c_shard", "bra_gpu_assemble_shards",
+    "bra_gpu_debug_rerun_jobs", "bra_gpu_sortnet_selftest",
 )
 MAX_CHUNK_SIZE = 256 * 1024  # BRA_MAX_CHUNK_SIZE (src/lib_bra_defs.h:93): the .BRa chunk size
 
@@ -499,6 +500,16 @@ class BlockCodec:
             m |= 1 << cls.SLOTS.index(n)
         return m
 
+    def debug_rerun_jobs(self, reps: int, shuffle_seed: int = 0) -> int:
+        """Re-run the last encode's BWT job phase `reps` times (job inputs reordered when
+        shuffle_seed != 0), auditing each run: the failing jobs summed over the runs."""
+        f = lib.bra_gpu_debug_rerun_jobs
+        f.argtypes, f.restype = [C.c_void_p, C.c_int, C.c_uint], C.c_int
+        r = f(self.ctx, reps, shuffle_seed)
+        if r < 0:
+            raise RuntimeError("bra_gpu_debug_rerun_jobs failed")
+        return r
+
     def stage_ptr(self, stage: int) -> int:
         return lib.bra_gpu_stage_ptr(self.ctx, stage) or 0
 
@@ -514,6 +525,16 @@ class BlockCodec:
         if rc != 0:
             raise RuntimeError(f"hipMemcpy failed ({rc})")
         return out
+
+
+def sortnet_selftest(waves: int, groups: int = 4096, iters: int = 64, seed: int = 1) -> int:
+    """Failing sorts of the BWT job sort (bra_gpu_sortnet_selftest) on random key sets."""
+    f = lib.bra_gpu_sortnet_selftest
+    f.argtypes, f.restype = [C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_void_p], C.c_int
+    r = f(waves, groups, iters, seed, None)
+    if r < 0:
+        raise RuntimeError("bra_gpu_sortnet_selftest failed")
+    return r
 
 
 def _stream_handle(stream):

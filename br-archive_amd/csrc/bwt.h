@@ -14,7 +14,8 @@ void          bwt_workspace_destroy(BwtWorkspace* w);
 const uint32_t* bwt_alpha_masks(const BwtWorkspace* w);
 // The suffix-array slots of the last encode (u32 per element at the block offsets; diagnostics).
 const uint32_t* bwt_sa(const BwtWorkspace* w);
-// Diagnostics (BRA_JOB_AUDIT builds, else -1): re-run and audit the last encode's job phase.
+// Diagnostics: re-run the last STRING encode's job phase `reps` times (inputs reordered when
+// shuffle_seed != 0) and audit every run; returns the failing jobs summed over the runs (-1: error).
 int bwt_debug_rerun_jobs(BwtWorkspace* w, int reps, hipStream_t s, uint32_t shuffle_seed);
 
 // BWT of every block: d_L[off..off+len) = last column, d_pi[b] = primary index (block-local).

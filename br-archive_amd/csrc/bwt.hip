@@ -3114,11 +3114,10 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_sortnet_test(uint32_
         atomicAdd(err, bad);
 }
 
-#ifdef BRA_JOB_AUDIT
-// ---- diagnostics (make EXTRA=-DBRA_JOB_AUDIT): after the STRING jobs, every job's slots are
-// counted (a slot two jobs cover is a race between them) and every job's output rotations are
-// checked against its input payloads (sum and xor of the rotation indices); violations are
-// printed, at most 32 per call. ----
+// ---- job audit (diagnostics: bra_gpu_debug_rerun_jobs, and after every encode in -DBRA_JOB_AUDIT
+// builds): every job's slots are counted (a slot two jobs cover is a race between them) and every
+// job's output rotations are checked against its input payloads (sum and xor of the rotation
+// indices); violations are printed, at most 32 per call. ----
 __device__ uint32_t g_audit_prints;
 __device__ uint32_t g_audit_fail;
 __global__ void k_audit_cover(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t* __restrict__ cnt)
@@ -3216,7 +3215,6 @@ __global__ void __launch_bounds__(1024) k_audit_shuffle(const Job* __restrict__ 
         __syncthreads();
     }
 }
-#endif
 
 // Workgroup-job size classes: a job of (256, 512] elements runs on 2 waves, (512, 1024] on 4 (never
 // more waves than the job's network needs).
@@ -3630,6 +3628,13 @@ __global__ void k_pi_from_isa(const BlockDesc* __restrict__ blocks, const uint8_
 // =================================================================================================
 // host driver
 // =================================================================================================
+// The job launches of a STRING encode (kept for the job-phase re-runs of bra_gpu_debug_rerun_jobs).
+struct JobPhase
+{
+    JobArgs  ja, jm;
+    uint32_t nblocks;
+};
+
 struct BwtWorkspace
 {
     uint64_t  cap_n          = 0;
@@ -3683,6 +3688,8 @@ struct BwtWorkspace
     uint32_t  cap_loc    = 0;
     uint32_t  local_max  = BRA_LOCAL_ON ? LOCAL_MAX : 0u;  // 0: no local stage (every large bucket takes the global levels)
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
+    JobPhase  last_ph{};                // job launches and batch size of the last STRING encode (diagnostics)
+    uint64_t  last_n     = 0;
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -3906,11 +3913,6 @@ static size_t tile_stage_bytes() { return sizeof(TileStage); }
 // The STRING jobs of a call, after the last MSD level: order the jobs block-major per XCD, then
 // the wave-job launch and one workgroup-job launch per size class.  Jobs are final when emitted:
 // no later level touches their slots.
-struct JobPhase
-{
-    JobArgs  ja, jm;
-    uint32_t nblocks;
-};
 
 static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
 {
@@ -4058,10 +4060,6 @@ static bool account_levels(BwtWorkspace& w, hipStream_t s)
     return true;
 }
 
-#ifdef BRA_JOB_AUDIT
-static JobPhase g_last_ph;
-static uint64_t g_last_n = 0;
-
 // The job audit (k_audit_cover / k_audit_check) of the jobs in the lists; returns the number of
 // failing jobs (-1 on a HIP error).
 static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hipStream_t s)
@@ -4087,6 +4085,7 @@ static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hi
     hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.mjobs, &w.ctr[0].n_mjobs, 1u, w.key[0], w.key[1], w.fsa, cnt, d_blocks);
     if (hipStreamSynchronize(s) != hipSuccess || hipMemcpyFromSymbol(&fails, HIP_SYMBOL(g_audit_fail), 4) != hipSuccess)
         return -1;
+#ifdef BRA_JOB_AUDIT
     uint32_t sf = 0;
     if (hipMemcpyFromSymbol(&sf, HIP_SYMBOL(g_sort_fail), 4) != hipSuccess)
         return -1;
@@ -4122,6 +4121,7 @@ static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hi
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_sort_fail), &z, 4) != hipSuccess)
             return -1;
     }
+#endif
     return (int) fails;
 }
 
@@ -4129,7 +4129,7 @@ static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hi
 // (the jobs only read them) and audits every run; returns the failing jobs summed over the runs.
 int bwt_debug_rerun_jobs(BwtWorkspace* wp, int reps, hipStream_t s, uint32_t seed)
 {
-    if (!g_last_n)
+    if (!wp->last_n)
         return -1;
     int total = 0;
     for (int r = 0; r < reps; ++r)
@@ -4139,18 +4139,15 @@ int bwt_debug_rerun_jobs(BwtWorkspace* wp, int reps, hipStream_t s, uint32_t see
             hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->jobs, &wp->ctr[0].n_jobs, wp->key[0], wp->key[1], seed + (uint32_t) r);
             hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->mjobs, &wp->ctr[0].n_mjobs, wp->key[0], wp->key[1], seed + (uint32_t) r);
         }
-        if (!run_jobs(*wp, g_last_ph, s))
+        if (!run_jobs(*wp, wp->last_ph, s))
             return -1;
-        const int f = audit_jobs(*wp, g_last_n, g_last_ph.ja.blocks, s);
+        const int f = audit_jobs(*wp, wp->last_n, wp->last_ph.ja.blocks, s);
         if (f < 0)
             return -1;
         total += f;
     }
     return total;
 }
-#else
-int bwt_debug_rerun_jobs(BwtWorkspace*, int, hipStream_t, uint32_t) { return -1; }
-#endif
 
 bool bwt_encode_device(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s)
@@ -4294,9 +4291,9 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     if (!run_jobs(w, ph, s))
         return false;
     BRA_HIP_CHECK(hipGetLastError());
+    w.last_ph = ph;
+    w.last_n  = N;
 #ifdef BRA_JOB_AUDIT
-    g_last_ph = ph;
-    g_last_n  = N;
     if (audit_jobs(w, N, d_blocks, s) < 0)
         return false;
 #endif

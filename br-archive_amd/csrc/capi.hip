@@ -1001,8 +1001,8 @@ const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* c, int stage)
 }
 
 // Diagnostics: re-run the job phase of the last batch encode `reps` times (each time with the jobs'
-// inputs in another order when shuffle_seed != 0) and audit it (builds with
-// -DBRA_JOB_AUDIT; -1 otherwise).  Returns the failing jobs summed over the runs.
+// inputs in another order when shuffle_seed != 0) and audit it.  Returns the failing jobs summed
+// over the runs, -1 on an error.
 int bra_gpu_debug_rerun_jobs(bra_gpu_ctx_t* c, int reps, unsigned shuffle_seed)
 {
     if (!c)

@@ -247,6 +247,18 @@ int bra_gpu_assemble_shards(bra_gpu_ctx_t* ctx, uint32_t nparts, const bra_io_ch
 const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* ctx, int stage);
 
 /*
+ * Diagnostics of the BWT job kernels (no reference equivalent; tests/test_gpu_jobs.py).
+ * bra_gpu_debug_rerun_jobs re-runs the job phase of the last batch encode `reps` times on its
+ * unchanged job lists -- with every job's input payloads put in another order first when
+ * shuffle_seed != 0 -- and checks each run (no slot covered by two jobs, every job's output
+ * rotations = its input rotations); returns the failing jobs summed over the runs, -1 on an error.
+ * bra_gpu_sortnet_selftest sorts groups x iters random key sets (or the 256 * waves given keys,
+ * slot order, padding all ones) with the job sort of `waves` waves and returns the failing sorts.
+ */
+int bra_gpu_debug_rerun_jobs(bra_gpu_ctx_t* ctx, int reps, unsigned shuffle_seed);
+int bra_gpu_sortnet_selftest(int waves, unsigned groups, unsigned iters, unsigned seed, const unsigned long long* keys);
+
+/*
  * Kernel timing with HIP events on the launching stream (used by bench.py): `mask` selects the
  * timing slots (bit i = slot i; 0 = off).  bra_gpu_prof_read waits for the recorded events and
  * returns the number of slots; for a valid `slot` it reports the slot's name, the summed device
