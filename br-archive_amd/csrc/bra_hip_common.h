@@ -409,8 +409,9 @@ __device__ __forceinline__ void cx64_pair(uint32_t& a0, uint32_t& a1, uint32_t& 
 }
 
 // (Folding the lane exchange into the compare-exchange as DPP source operands -- v_sub_co / v_subb_co /
-// v_cndmask with a DPP src0, 4 VALU instead of 6 -- sorted wrongly now and then in round 3; that was
-// most likely the missing scc clobber above, not the DPP form.)
+// v_cndmask with a DPP src0, 4 VALU instead of 6 -- is correct with the scc clobber (round 3's wrong
+// sorts with it were the missing clobber) but measured equal in round 4: 1.889 vs 1.893 ms wave
+// jobs, 3.25 ms workgroup jobs either way; the separate DPP moves stay.)
 template <int LM>
 __device__ __forceinline__ uint64_t xlane64(uint64_t x)
 {

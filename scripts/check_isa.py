@@ -1,7 +1,7 @@
 """Static checks of the gfx950 machine code of the block codec (CPU-only; tests/test_isa.py runs it).
 
 1. SCC across the compare-exchange strings.  The sort networks' inline asm (bra_hip_common.h cx*)
-   computes its lane mask with `s_xnor_b64 vcc, vcc, ...`, which also writes SCC.  If the compiler
+   computes its lane mask with `s_xnor_b64` / `s_xor_b64 vcc, vcc, ...`, which also write SCC.  If the compiler
    believes SCC survives the string (a missing "scc" clobber), a later s_cselect / s_cbranch_scc
    reads the xnor's result instead of the compiler's own compare: a network stage silently takes
    the wrong direction for some key sets.  Flagged: an SCC reader whose nearest preceding SCC writer
@@ -90,7 +90,7 @@ def check(path: str):
         if SCC_READ.match(op):
             for prev in reversed(recent):
                 if SCC_WRITE.match(prev.split(None, 1)[0]):
-                    if prev.startswith("s_xnor_b64 vcc, vcc"):
+                    if re.match(r"s_xn?or_b64 vcc, vcc", prev):
                         findings.append(f"{os.path.basename(path)} [{fn}] `{ins}` reads SCC written by `{prev}` (inline asm without an scc clobber)")
                     break
         # 2. VALU write -> DPP / permlane swap read
@@ -100,7 +100,14 @@ def check(path: str):
             continue
         if op.startswith("v_") and (DPP.search(ins) or op.startswith("v_permlane")):
             ops = [a.strip() for a in args.split(",")]
-            srcs = _regs(ops[0]) + _regs(ops[1]) if op.startswith("v_permlane") and len(ops) > 1 else [r for a in ops for r in _regs(a.split()[0] if a else "")]
+            if op.startswith("v_permlane"):
+                srcs = _regs(ops[0]) + (_regs(ops[1]) if len(ops) > 1 else [])
+            else:
+                # sources; the destination too when its old value can be kept (a partial row / bank
+                # mask, or a shift without bound_ctrl that leaves lanes without a source)
+                partial = "row_mask:0xf" not in ins or "bank_mask:0xf" not in ins or (
+                    re.search(r"\brow_(shl|shr)|\bwave_", ins) and "bound_ctrl" not in ins)
+                srcs = [r for a in (ops if partial else ops[1:]) for r in _regs(a.split()[0] if a else "")]
             for r in srcs:
                 if r in last_write and t - last_write[r] < 2:
                     findings.append(f"{os.path.basename(path)} [{fn}] `{ins}` reads v{r} {t - last_write[r]} wait state(s) after a VALU write")
