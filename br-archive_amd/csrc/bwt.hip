@@ -57,10 +57,7 @@ constexpr int      TILE         = 4096;  // elements per MSD tile (256 threads x
 constexpr int      TPB          = 256;
 constexpr int      PER_THREAD   = TILE / TPB;
 constexpr uint32_t JOB_MAX      = 256;  // elements one wave sorts in registers
-#ifndef BRA_MJ_WAVES
-#define BRA_MJ_WAVES 4  // EXPERIMENT (0: no workgroup jobs, the local stage splits down to wave jobs)
-#endif
-constexpr int      MJ_WAVES_DEF = BRA_MJ_WAVES;    // waves of the largest workgroup job (2 or 4; 8 / 16 -- jobs of up to 4096 -- measured slower, removed)
+constexpr int      MJ_WAVES_DEF = 4;    // waves of the largest workgroup job (2 or 4; 8 / 16 -- jobs of up to 4096 -- measured slower, removed)
 constexpr uint32_t DCAP_BIG     = 64;   // MSD depth after which a big bucket goes to the fallback
 constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied group goes to the fallback
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
@@ -111,8 +108,6 @@ struct Counters
     alignas(128) uint32_t n_moved;       // elements the level's scatter moves (byte accounting)
     alignas(128) uint32_t n_elems_next;
     alignas(128) uint32_t n_melems;      // elements in workgroup jobs (byte accounting)
-    alignas(128) uint32_t n_loc;         // local buckets (finished in LDS by k_local)
-    uint32_t n_loc_elems;                // their elements (byte accounting)
 };
 
 // A STRING-mode MSD tile as the hist and scatter kernels need it (built with the tile order, so a
@@ -732,9 +727,6 @@ struct ScanArgs
     const PackDesc* pk;        // STRING: packed key strings per block
     const uint32_t* btot;      // level 0: per-bucket digit totals (k_l0_colscan) instead of the tile rows
     uint32_t*       bbase;     // level 0: per-bucket sub-bucket starts (| NEXT_FLAG), added to the tiles' running counts by the scatter
-    Bucket*         loc;       // STRING: local buckets (mjob_max < size <= local_max), finished by k_local
-    uint32_t        cap_loc;
-    uint32_t        local_max; // 0: no local buckets (RANK mode)
 };
 
 // One wave per bucket (SCAN_WAVES buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
@@ -746,7 +738,7 @@ constexpr int SCAN_WAVES = 4;  // buckets (waves) per scan workgroup: 16 and 8 m
 
 struct ScanWaveCounts
 {
-    uint32_t jobs, mjobs, big, tiles, groups, moved, melems, elems_next, gmembers, hmin, loc, lelems;
+    uint32_t jobs, mjobs, big, tiles, groups, moved, melems, elems_next, gmembers, hmin;
 };
 
 template <uint32_t MODE>
@@ -756,7 +748,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
     __shared__ uint32_t       jlen_s[SCAN_WAVES][256];
     __shared__ uint8_t        nx_s[SCAN_WAVES][256];
     __shared__ ScanWaveCounts cnt_s[SCAN_WAVES];
-    __shared__ uint32_t       base_s[SCAN_WAVES][6];  // jobs, mjobs, big, tiles, groups, local buckets
+    __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
     const int                 lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t            nbuckets = a.lin ? dev_count(&a.lin->n_big) : a.nbuckets;
     const uint32_t            bstride  = gridDim.x * SCAN_WAVES;
@@ -818,7 +810,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
             {
-                const bool nb = (MODE == MODE_STRING) && tot[r] > max(a.mjob_max, a.local_max) && B.d + 1 < a.dcap;
+                const bool nb = (MODE == MODE_STRING) && tot[r] > a.mjob_max && B.d + 1 < a.dcap;
                 flag[r]       = nb ? 0x80000000u : 0u;
             }
             uint4*   to     = reinterpret_cast<uint4*>(a.tile_off + (size_t) B.tile0 * 256) + lane;
@@ -847,25 +839,21 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                nm_next |= (tot[r] == B.len) && tot[r] > max(a.mjob_max, a.local_max) && B.d + 1 < a.dcap;
+                nm_next |= (tot[r] == B.len) && tot[r] > a.mjob_max && B.d + 1 < a.dcap;
             nm_next = __any(nm_next);
         }
         const uint32_t nd     = B.d + 1;
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
         if (active && lane == 0)
             a.nomove[bi] = nomove ? (nm_next ? 2 : 1) : 0;
-        // the payload carry base of elements that are not re-gathered by this level's scatter (local
-        // buckets): level 0 writes digits [1, 1 + CARRY), a moving or staying bucket keeps its own
-        const uint32_t lkd = (B.buf == 2u) ? 1u : B.kd;
-        bool big[4], med[4], fin[4], nbn[4], lcl[4];
+        bool big[4], med[4], fin[4], nbn[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
             big[r] = tot[r] > a.mjob_max;
             med[r] = tot[r] > JOB_MAX && !big[r];
             fin[r] = big[r] && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
-            lcl[r] = big[r] && !fin[r] && tot[r] <= a.local_max;
-            nbn[r] = big[r] && !fin[r] && !lcl[r];
+            nbn[r] = big[r] && !fin[r];
         }
         // ---- wave jobs: greedy packing of consecutive sub-buckets of <= JOB_MAX elements ----
         // The non-empty sub-buckets form a list in digit order; a wave-job sub-bucket weighs its
@@ -951,8 +939,8 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         for (int r = 0; r < 4; ++r)
             jidx[r] = jex[r];
         // ---- workgroup jobs, next-level buckets, fallback groups ----
-        uint32_t cm[4], cb[4], ct[4], cg[4], cl[4], mex[4], bex[4], tex[4], gex[4], lex[4], ntl[4];
-        uint32_t melems = 0, enext = 0, gmem = 0, gmin = 0xFFFFFFFFu, lelems = 0;
+        uint32_t cm[4], cb[4], ct[4], cg[4], mex[4], bex[4], tex[4], gex[4], ntl[4];
+        uint32_t melems = 0, enext = 0, gmem = 0, gmin = 0xFFFFFFFFu;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -961,8 +949,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
             cb[r]  = nbn[r] ? 1u : 0u;
             ct[r]  = ntl[r];
             cg[r]  = fin[r] ? 1u : 0u;
-            cl[r]  = lcl[r] ? 1u : 0u;
-            lelems += lcl[r] ? tot[r] : 0;
             melems += med[r] ? tot[r] : 0;
             enext += nbn[r] ? tot[r] : 0;
             gmem += fin[r] ? tot[r] : 0;
@@ -972,16 +958,9 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         wave_excl_sum4(cb, bex, &C.big);
         wave_excl_sum4(ct, tex, &C.tiles);
         wave_excl_sum4(cg, gex, &C.groups);
-        wave_excl_sum4(cl, lex, &C.loc);
         C.jobs = active ? jtot : 0;
         if (!active)
-            C.mjobs = C.big = C.tiles = C.groups = C.loc = 0;
-        if (C.loc)
-        {
-            for (int d = 32; d >= 1; d >>= 1)
-                lelems += __shfl_xor(lelems, d, WAVE);
-            C.lelems = lelems;
-        }
+            C.mjobs = C.big = C.tiles = C.groups = 0;
         if (a.account || C.groups)
         {
             for (int d = 32; d >= 1; d >>= 1)
@@ -1002,7 +981,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         __syncthreads();
         if (threadIdx.x == 0)
         {
-            uint32_t pre[6] = {0, 0, 0, 0, 0, 0}, tj = 0, tm = 0, tb = 0, tt = 0, tg = 0, tl = 0, tle = 0;
+            uint32_t pre[5] = {0, 0, 0, 0, 0}, tj = 0, tm = 0, tb = 0, tt = 0, tg = 0;
             ScanWaveCounts T{};
             T.hmin = 0xFFFFFFFFu;
             for (int v = 0; v < SCAN_WAVES; ++v)
@@ -1013,9 +992,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                 base_s[v][2] = tb;
                 base_s[v][3] = tt;
                 base_s[v][4] = tg;
-                base_s[v][5] = tl;
-                tl += c.loc;
-                tle += c.lelems;
                 tj += c.jobs;
                 tm += c.mjobs;
                 tb += c.big;
@@ -1047,12 +1023,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                 atomicAdd(&a.ctr->g_members, T.gmembers);
                 atomicMin(&a.ctr->hmin, T.hmin);
             }
-            if (tl)
-            {
-                const unsigned long long old =
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_loc), ((unsigned long long) tle << 32) | tl);
-                pre[5] = (uint32_t) old;
-            }
             if (a.account)
             {
                 if (T.moved)
@@ -1063,7 +1033,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                     atomicAdd(&a.lout->n_elems_next, T.elems_next);
             }
             for (int v = 0; v < SCAN_WAVES; ++v)
-                for (int q = 0; q < 6; ++q)
+                for (int q = 0; q < 5; ++q)
                     base_s[v][q] += pre[q];
         }
         __syncthreads();
@@ -1111,14 +1081,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                     else
                         atomicExch(&a.ctr->overflow, 1u);
                 }
-                if (lcl[r])
-                {
-                    const uint32_t slot = base_s[w][5] + lex[r];
-                    if (slot < a.cap_loc)
-                        a.loc[slot] = Bucket{s0, tot[r], nd, lkd, B.block, obuf, B.gdepth, 0};
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
                 if (fin[r])
                 {
                     const uint32_t gdep = (MODE == MODE_STRING) ? nd : B.gdepth;
@@ -1134,393 +1096,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
     }
 }
 
-// -------------------------------------------------------------------------------------------------
-// Local MSD (STRING mode).  A sub-bucket of mjob_max < size <= LOCAL_MAX elements does not go through
-// further global MSD levels: one workgroup loads its payloads into LDS and splits it there, digit by
-// digit (re-gathering the carried digits every CARRY levels), until every part is a job, then writes
-// the payloads back in place and appends the jobs -- exactly the sub-buckets, jobs, workgroup jobs and
-// fallback groups the global levels would have produced (the order of the elements inside a
-// sub-bucket is free: every job sorts its elements completely and ties are identical rotations).
-// Text (1 MiB blocks): after two virtual bytes 48 % of the elements sit in buckets of 1025-8192
-// elements, which the global levels 2..8 moved again and again (HBM: 18 B per element per level).
-// -------------------------------------------------------------------------------------------------
-#ifndef BRA_LOCAL_MAX
-#define BRA_LOCAL_MAX 8192  // EXPERIMENT (16384: 1 workgroup of 1024 threads per CU)
-#endif
-#ifndef BRA_LOCAL_ON
-#define BRA_LOCAL_ON 0      // EXPERIMENT: the local stage is off by default (slower as measured so far)
-#endif
-constexpr uint32_t LOCAL_MAX = BRA_LOCAL_MAX;     // largest local bucket (64 KiB of payloads in LDS)
-constexpr int      LTPB      = LOCAL_MAX / 16;    // threads of a local workgroup
-constexpr int      LPT       = LOCAL_MAX / LTPB;  // payloads per thread
-constexpr int      LNC       = 4;                 // digit-counter copies (lane & 3), CSTRIDE apart
-constexpr uint32_t LSTACK    = 64;                // segments waiting to be split
-
-struct LocalSeg
-{
-    uint32_t s, len, d, kd;  // bucket-relative start, length, depth (digit d splits it), payload carry base
-};
-
-struct LocalArgs
-{
-    const Bucket*   loc;
-    uint64_t*       pay0;
-    uint64_t*       pay1;
-    const uint8_t*  packed;
-    const PackDesc* pk;
-    Job*            jobs;
-    uint32_t        cap_jobs;
-    Job*            mjobs;
-    uint32_t        cap_mjobs;
-    Group*          groups;
-    uint32_t        cap_groups;
-    Counters*       ctr;
-    uint32_t        dcap;
-    uint32_t        mjob_max;
-};
-
-constexpr uint32_t LJOBS = 128, LMJOBS = 32, LGROUPS = 16;  // records kept in LDS until the bucket is done
-
-struct LocalLds
-{
-    uint64_t pay[LOCAL_MAX];
-    Job      jrec[LJOBS];    // the bucket's wave jobs, workgroup jobs and fallback groups, appended to the
-    Job      mrec[LMJOBS];   // call-wide lists with one atomic per list when the bucket is done (an atomic
-    Group    grec[LGROUPS];  // per split kept the workgroup waiting on its return at every split)
-    uint32_t nj, nm, ng, gmem, gmin, melems;
-    uint32_t cnt[LNC * CSTRIDE];  // per copy: counts, then the copy's first slot per digit
-    uint32_t Ew[256];             // wave-job packing (as in k_scan)
-    uint32_t Sw[256];
-    uint8_t  nx[256];
-    LocalSeg stk[LSTACK];
-    uint32_t nstk;
-};
-
-// Wave 0: sub-buckets of segment G (digit t = 4 lane + r has tot[t] elements at base[t]): jobs,
-// workgroup jobs and fallback groups are appended to the call-wide lists, parts still larger than a
-// workgroup job replace G on the stack.
-__device__ __forceinline__ void local_classify(const LocalArgs& a, const Bucket& B, const LocalSeg& G, uint32_t kd, LocalLds& S, uint32_t ns,
-                                               const uint32_t (&tot)[4], const uint32_t (&base)[4])
-{
-    const int      lane = lane_id();
-    const uint32_t nd   = G.d + 1;
-    bool           big[4], med[4], fin[4];
-    uint32_t       cm[4], cg[4], cp[4], mex[4], gex[4], pex[4], nm, ng, np;
-    uint32_t       melems = 0, gmem = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        big[r] = tot[r] > a.mjob_max;
-        med[r] = tot[r] > JOB_MAX && !big[r];
-        fin[r] = big[r] && nd >= a.dcap;
-        cm[r]  = med[r] ? 1u : 0u;
-        cg[r]  = fin[r] ? 1u : 0u;
-        cp[r]  = (big[r] && !fin[r]) ? 1u : 0u;
-        melems += med[r] ? tot[r] : 0u;
-        gmem += fin[r] ? tot[r] : 0u;
-    }
-    wave_excl_sum4(cm, mex, &nm);
-    wave_excl_sum4(cg, gex, &ng);
-    wave_excl_sum4(cp, pex, &np);
-    // wave jobs: greedy packing of consecutive sub-buckets of <= JOB_MAX elements (k_scan)
-    uint32_t li[4], wt[4], wx[4], nlist;
-    {
-        uint32_t ne[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            ne[r] = tot[r] ? 1u : 0u;
-            wt[r] = tot[r] == 0 ? 0u : (tot[r] <= JOB_MAX ? tot[r] : JOB_MAX + 1u);
-        }
-        wave_excl_sum4(ne, li, &nlist);
-        wave_excl_sum4(wt, wx);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (tot[r])
-        {
-            S.Ew[li[r]] = wx[r] + wt[r];
-            S.Sw[li[r]] = base[r];
-            S.nx[li[r]] = 0;
-        }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t nxt[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        nxt[r] = li[r] + 1;
-        if (tot[r] && tot[r] <= JOB_MAX)
-        {
-            const uint32_t lim = wx[r] + JOB_MAX;
-            uint32_t       lo = li[r] + 1, hi = nlist;
-            while (lo < hi)
-            {
-                const uint32_t m = (lo + hi) >> 1;
-                if (S.Ew[m] > lim)
-                    hi = m;
-                else
-                    lo = m + 1;
-            }
-            nxt[r] = lo;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (tot[r])
-            S.Ew[li[r]] = nxt[r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0)
-        for (uint32_t c = 0; c < nlist; c = S.Ew[c])
-            S.nx[c] = 1;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    bool     jstart[4];
-    uint32_t js[4], jex[4], jlen[4], nj;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        jstart[r] = tot[r] && tot[r] <= JOB_MAX && S.nx[li[r]];
-        js[r]     = jstart[r] ? 1u : 0u;
-        jlen[r]   = jstart[r] ? (nxt[r] < nlist ? S.Sw[nxt[r]] : G.len) - base[r] : 0u;
-    }
-    wave_excl_sum4(js, jex, &nj);
-    for (int d = 32; d >= 1; d >>= 1)
-    {
-        melems += __shfl_xor(melems, d, WAVE);
-        gmem += __shfl_xor(gmem, d, WAVE);
-    }
-    // LDS record slots (lists full: this split's records go to the device lists directly)
-    const uint32_t jb0 = S.nj, mb0 = S.nm, gb0 = S.ng;
-    const bool     jl = jb0 + nj <= LJOBS, ml = mb0 + nm <= LMJOBS, gl = gb0 + ng <= LGROUPS;
-    uint32_t       jb = jb0, mb = mb0, gb = gb0;
-    if (lane == 0)
-    {
-        if ((nj && !jl) || (nm && !ml))
-        {
-            const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs),
-                                                     ((unsigned long long) (ml ? 0u : nm) << 32) | (jl ? 0u : nj));
-            if (!jl)
-                jb = (uint32_t) old;
-            if (!ml)
-                mb = (uint32_t) (old >> 32);
-        }
-        if (ng && !gl)
-            gb = atomicAdd(&a.ctr->n_groups, ng);
-        S.nj = jb0 + (jl ? nj : 0u);
-        S.nm = mb0 + (ml ? nm : 0u);
-        S.ng = gb0 + (gl ? ng : 0u);
-        S.melems += melems;
-        S.gmem += gmem;
-        if (ng)
-            S.gmin = min(S.gmin, nd);
-    }
-    jb = __builtin_amdgcn_readfirstlane(jb);
-    mb = __builtin_amdgcn_readfirstlane(mb);
-    gb = __builtin_amdgcn_readfirstlane(gb);
-    Job* const   jdst = jl ? S.jrec : a.jobs;
-    Job* const   mdst = ml ? S.mrec : a.mjobs;
-    Group* const gdst = gl ? S.grec : a.groups;
-    const uint32_t jcap = jl ? LJOBS : a.cap_jobs, mcap = ml ? LMJOBS : a.cap_mjobs, gcap = gl ? LGROUPS : a.cap_groups;
-    const uint32_t top = ns - 1;  // G's entry is replaced by its children
-    if (top + np > LSTACK)
-    {
-        if (lane == 0)
-            atomicExch(&a.ctr->overflow, 1u);
-        np = 0;  // (the call fails: the overflow is reported)
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        const uint32_t s0 = B.start + G.s + base[r];
-        if (jstart[r])
-        {
-            const uint32_t slot = jb + jex[r];
-            if (slot < jcap)
-                jdst[slot] = Job{s0, jlen[r], nxt[r] == li[r] + 1 ? 1u : 0u, B.buf, B.block, B.gdepth, nd};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (med[r])
-        {
-            const uint32_t slot = mb + mex[r];
-            if (slot < mcap)
-                mdst[slot] = Job{s0, tot[r], kd, B.buf, B.block, B.gdepth, nd};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (fin[r])
-        {
-            const uint32_t slot = gb + gex[r];
-            if (slot < gcap)
-                gdst[slot] = Group{s0, tot[r], nd, B.block | (B.buf << 31)};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (cp[r] && top + pex[r] < LSTACK)
-            S.stk[top + pex[r]] = LocalSeg{G.s + base[r], tot[r], nd, kd};
-    }
-    if (lane == 0)
-        S.nstk = top + np;
-}
-
-__global__ void __launch_bounds__(LTPB, 4) k_local(LocalArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    LocalLds&      S    = *reinterpret_cast<LocalLds*>(smem);
-    const uint32_t nloc = dev_count(&a.ctr->n_loc);
-    const int      lane = lane_id();
-    const uint32_t cp   = (uint32_t) (lane & (LNC - 1)) * CSTRIDE;
-    for (uint32_t bi = blockIdx.x; bi < nloc; bi += gridDim.x)
-    {
-        const Bucket   B  = a.loc[bi];
-        const PackDesc P  = a.pk[B.block];
-        const uint8_t* pk = a.packed + P.poff;
-        uint64_t*      gp = (B.buf ? a.pay1 : a.pay0) + B.start;
-        const uint32_t n  = min(B.len, LOCAL_MAX);  // (the scan emits none larger)
-        for (uint32_t i = threadIdx.x; i < n; i += LTPB)
-            S.pay[i] = gp[i];
-        for (uint32_t c = threadIdx.x; c < LNC * CSTRIDE; c += LTPB)
-            S.cnt[c] = 0;
-        if (threadIdx.x == 0)
-        {
-            S.stk[0] = LocalSeg{0, n, B.d, B.kd};
-            S.nstk   = 1;
-            S.nj = S.nm = S.ng = S.gmem = S.melems = 0;
-            S.gmin = 0xFFFFFFFFu;
-        }
-        __syncthreads();
-        while (true)
-        {
-            const uint32_t ns = S.nstk;
-            if (ns == 0)
-                break;  // uniform
-            const LocalSeg G  = S.stk[ns - 1];
-            const bool     rg = G.d - G.kd >= CARRY;  // the carried digits are used up: re-gather them
-            const uint32_t kd = rg ? G.d : G.kd, j = G.d - kd;
-            if (rg)
-            {
-                for (uint32_t e = threadIdx.x; e < G.len; e += LTPB)
-                    S.pay[G.s + e] = p_make(pk, P.b, P.nbits, G.d, S.pay[G.s + e]);
-                __syncthreads();
-            }
-            uint64_t       v[LPT];
-            uint32_t       dr[LPT];  // digit << 16 | rank among the digit's elements of this lane's counter copy
-#pragma unroll
-            for (int r = 0; r < LPT; ++r)
-            {
-                const uint32_t e = threadIdx.x + r * LTPB;
-                if (e < G.len)
-                {
-                    const uint64_t q  = S.pay[G.s + e];
-                    v[r]              = q;
-                    const uint32_t dg = p_digit(q, j);
-                    dr[r]             = dg << 16 | atomicAdd(&S.cnt[cp + dg], 1u);
-                }
-            }
-            __syncthreads();  // counts complete; every thread has read G and its payloads
-            uint32_t tot[4], base[4];  // wave 0: digits 4 lane + r
-            if (threadIdx.x < WAVE)
-            {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const uint32_t d = 4 * lane + r;
-                    tot[r]           = 0;
-#pragma unroll
-                    for (int k = 0; k < LNC; ++k)
-                        tot[r] += S.cnt[k * CSTRIDE + d];
-                }
-                wave_excl_sum4(tot, base);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const uint32_t d   = 4 * lane + r;
-                    uint32_t       run = G.s + base[r];
-#pragma unroll
-                    for (int k = 0; k < LNC; ++k)
-                    {
-                        const uint32_t c       = S.cnt[k * CSTRIDE + d];
-                        S.cnt[k * CSTRIDE + d] = run;
-                        run += c;
-                    }
-                }
-            }
-            __syncthreads();  // slots per digit and copy
-#pragma unroll
-            for (int r = 0; r < LPT; ++r)
-            {
-                const uint32_t e = threadIdx.x + r * LTPB;
-                if (e < G.len)
-                    S.pay[S.cnt[cp + (dr[r] >> 16)] + (dr[r] & 0xFFFFu)] = v[r];
-            }
-            if (threadIdx.x < WAVE)  // (G's stack entry was read by everyone before the barrier above)
-                local_classify(a, B, G, kd, S, ns, tot, base);
-            __syncthreads();  // the segment is in digit order, the new stack; the counters are free
-            for (uint32_t c = threadIdx.x; c < LNC * CSTRIDE; c += LTPB)
-                S.cnt[c] = 0;
-            __syncthreads();
-        }
-        for (uint32_t i = threadIdx.x; i < n; i += LTPB)
-            gp[i] = S.pay[i];
-        // the bucket's records into the call-wide lists: one atomic per list
-        __shared__ uint32_t base_s[3];
-        if (threadIdx.x == 0)
-        {
-            base_s[0] = base_s[1] = base_s[2] = 0;
-            if (S.nj || S.nm)
-            {
-                const unsigned long long old =
-                    atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) S.nm << 32) | S.nj);
-                base_s[0] = (uint32_t) old;
-                base_s[1] = (uint32_t) (old >> 32);
-            }
-            if (S.ng)
-                base_s[2] = atomicAdd(&a.ctr->n_groups, S.ng);
-            if (S.gmin != 0xFFFFFFFFu)
-            {
-                atomicAdd(&a.ctr->g_members, S.gmem);
-                atomicMin(&a.ctr->hmin, S.gmin);
-            }
-            if (S.melems)
-                atomicAdd(&a.ctr->n_melems, S.melems);
-        }
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < S.nj; i += LTPB)
-        {
-            if (base_s[0] + i < a.cap_jobs)
-                a.jobs[base_s[0] + i] = S.jrec[i];
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        for (uint32_t i = threadIdx.x; i < S.nm; i += LTPB)
-        {
-            if (base_s[1] + i < a.cap_mjobs)
-                a.mjobs[base_s[1] + i] = S.mrec[i];
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        for (uint32_t i = threadIdx.x; i < S.ng; i += LTPB)
-        {
-            if (base_s[2] + i < a.cap_groups)
-                a.groups[base_s[2] + i] = S.grec[i];
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        __syncthreads();
-    }
-}
-
-// -------------------------------------------------------------------------------------------------
-// LDS-staged scatter of one tile into its sub-buckets
-// -------------------------------------------------------------------------------------------------
 struct TileStage
 {
     uint64_t key[TILE];
@@ -3684,9 +3259,6 @@ struct BwtWorkspace
     uint32_t* jobq       = nullptr;   // per-XCD claim counters of the job launches ((1 + MJ_CLASSES) x 8 x 32 dwords)
     uint32_t  jobq_chunk = JQ_CHUNK;  // wave jobs claimed at once
     uint32_t  nblocks    = 0;         // blocks of the current call
-    Bucket*   loc        = nullptr;   // local buckets of the STRING levels (k_local)
-    uint32_t  cap_loc    = 0;
-    uint32_t  local_max  = BRA_LOCAL_ON ? LOCAL_MAX : 0u;  // 0: no local stage (every large bucket takes the global levels)
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
     JobPhase  last_ph{};                // job launches and batch size of the last STRING encode (diagnostics)
     uint64_t  last_n     = 0;
@@ -3827,7 +3399,7 @@ static void ws_free(BwtWorkspace& w)
     }
     void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
                    w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask, w.l0tot, w.l0base,
-                   w.loc};
+};
     for (void* p : dev)
         (void) hipFree(p);
     if (w.h_ctr)
@@ -3873,7 +3445,6 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     w.cap_jobs   = (uint32_t) (N / 2 + B + 1024);
     w.cap_groups = (uint32_t) (N / 2 + B + 64);
     w.cap_mjobs  = (uint32_t) (N / JOB_MAX + B + 64);
-    w.cap_loc    = (uint32_t) (N / JOB_MAX + B + 64);  // local buckets hold > mjob_max >= JOB_MAX elements
     const uint32_t cap_sorted = (uint32_t) (N / 8 + B + 1024);
     bool ok = true;
     for (int i = 0; i < 2 && ok; ++i)
@@ -3888,7 +3459,7 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
          dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
          dev_alloc(w.jobq, (1 + MJ_CLASSES) * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
          dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B) &&
-         dev_alloc(w.tmask, 8ull * w.cap_l0) && dev_alloc(w.l0tot, 256ull * B) && dev_alloc(w.l0base, 256ull * B) && dev_alloc(w.loc, w.cap_loc);
+         dev_alloc(w.tmask, 8ull * w.cap_l0) && dev_alloc(w.l0tot, 256ull * B) && dev_alloc(w.l0base, 256ull * B);
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -4001,7 +3572,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                        w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
                        w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
                        (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout, w.pkd, nullptr, nullptr,
-                       w.loc, w.cap_loc, MODE == MODE_STRING ? w.local_max : 0u};
+};
             {
                 BRA_PROF(P_BWT_SCAN, s);
                 hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
@@ -4207,7 +3778,6 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         const size_t lds = tile_stage_bytes();
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
         BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_l0_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int) (sizeof(TileStageL0) + TILE + 64)));
-        BRA_HIP_CHECK(hipFuncSetAttribute((const void*) k_local, hipFuncAttributeMaxDynamicSharedMemorySize, (int) sizeof(LocalLds)));
         attr_set.fetch_or(dev_bit);
     }
     const int grid = w.grid;
@@ -4251,7 +3821,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     ScanArgs a0{d_blocks, w.l0b,     nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1, w.pkd,
-                w.l0tot,          w.l0base,    w.loc,      w.cap_loc,  w.local_max};
+                w.l0tot,          w.l0base};
     {
         BRA_PROF(P_BWT_SCAN, s);
         hipLaunchKernelGGL(k_l0_colscan, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(256 * L0CS_GROUPS), 0, s, w.l0b, nblocks, w.tile_hist,
@@ -4279,15 +3849,6 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     ph.nblocks = nblocks;
     if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s)))
         return false;
-    if (w.local_max)
-    {
-        // the local buckets of every level (their slots are final: no later level touches them)
-        BRA_PROF(P_BWT_LOCAL, s);
-        const LocalArgs la{w.loc, w.key[0], w.key[1], w.packed, w.pkd, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs, w.groups[0], w.cap_groups,
-                           w.ctr, DCAP_BIG, w.mjob_max()};
-        hipLaunchKernelGGL(k_local, dim3((160u * 1024u / (uint32_t) sizeof(LocalLds)) * 256u), dim3(LTPB), sizeof(LocalLds), s, la);
-        BRA_DSYNC(s);
-    }
     if (!run_jobs(w, ph, s))
         return false;
     BRA_HIP_CHECK(hipGetLastError());
@@ -4306,8 +3867,8 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, ns * sizeof(Counters), hipMemcpyDeviceToHost, s));
         BRA_HIP_CHECK(hipStreamSynchronize(s));
         const Counters& c0 = w.h_ctr[0];
-        fprintf(stderr, "[bwt levels] N %llu jobs %u mjobs %u melems %u groups %u local %u (%u elements)\n", (unsigned long long) N, c0.n_jobs,
-                c0.n_mjobs, c0.n_melems, c0.n_groups, c0.n_loc, c0.n_loc_elems);
+        fprintf(stderr, "[bwt levels] N %llu jobs %u mjobs %u melems %u groups %u\n", (unsigned long long) N, c0.n_jobs,
+                c0.n_mjobs, c0.n_melems, c0.n_groups);
         for (uint32_t k = 1; k < ns; ++k)
             fprintf(stderr, "[bwt levels] slot %u: buckets %u tiles %u elems %u moved(into) %u\n", k, w.h_ctr[k].n_big, w.h_ctr[k].n_tiles_next,
                     w.h_ctr[k].n_elems_next, w.h_ctr[k].n_moved);
@@ -4340,13 +3901,12 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
 #endif
     // SURVEY 8.1(d) BWT model: 11 algorithmic bytes per element (input read, SA written and
     // re-read, L gathered and written), charged to the job kernels by the elements each kind covers
-    if (g_prof && (g_prof->mask >> P_BWT_JOBS & 1 || g_prof->mask >> P_BWT_MJOBS & 1 || g_prof->mask >> P_BWT_LOCAL & 1))
+    if (g_prof && (g_prof->mask >> P_BWT_JOBS & 1 || g_prof->mask >> P_BWT_MJOBS & 1))
     {
         BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
         BRA_HIP_CHECK(hipStreamSynchronize(s));
         prof_bytes(P_BWT_JOBS, 11.0 * ((double) N - (double) w.h_ctr->n_melems));
         prof_bytes(P_BWT_MJOBS, 11.0 * (double) w.h_ctr->n_melems);
-        prof_bytes(P_BWT_LOCAL, 16.0 * (double) w.h_ctr->n_loc_elems);  // payloads read and written once
     }
 
     // ---- fallback: prefix doubling on the groups still tied ----

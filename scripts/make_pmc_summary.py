@@ -19,7 +19,7 @@ SLOTS = {
     "bwt.pack": ["k_alpha", "k_pack_desc", "k_pack"],
     "bwt.l0_hist": ["k_l0_hist"], "bwt.l0_scatter": ["k_l0_scatter"], "bwt.hist": ["k_hist<0u>"], "bwt.scan": ["k_scan<0u>"],
     "bwt.scatter": ["k_scatter", "k_scatter_p"], "bwt.jobs": ["k_jobs<0u>"],
-    "bwt.mjobs": ["k_mjobs<0u, 2>", "k_mjobs<0u, 4>", "k_mjobs<0u, 8>", "k_mjobs<0u, 16>"], "bwt.local": ["k_local"],
+    "bwt.mjobs": ["k_mjobs<0u, 2>", "k_mjobs<0u, 4>", "k_mjobs<0u, 8>", "k_mjobs<0u, 16>"],
     "mtf.lastocc": ["k_mtf_lastocc"], "mtf.scan": ["k_mtf_scan"], "mtf.encode": ["k_mtf_encode_pos", "k_mtf_encode_reg", "k_mtf_encode_wave"],
     "rle.runs": ["k_rle_runs"], "rle.link": ["k_rle_link"], "rle.sizes": ["k_rle_sizes"], "rle.offsets": ["k_rle_offsets"],
     "rle.write": ["k_rle_write"], "huf.build": ["k_huff_build"], "huf.offsets": ["k_huff_offsets"], "huf.tilebits": ["k_huff_tilebits"],
