@@ -65,9 +65,6 @@ constexpr uint32_t CSTRIDE    = 256 + 16;  // digit-counter copies (TileStagePN,
 constexpr int      SCATTER_NC = 4;  // digit-counter copies of the MSD scatter
 constexpr int      HIST_NC    = 4;  // counter copies of the MSD histogram (copy = lane & (NC - 1))
 constexpr uint32_t JQ_CHUNK   = 2;  // wave jobs a wave claims with one atomic (8: equal)
-#ifndef BRA_JOB_VEC_OUT
-#define BRA_JOB_VEC_OUT 1  // job outputs as 16-byte / 4-byte stores where 4 consecutive aligned slots resolve together
-#endif
 #define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
 #define JOB_MIN_WAVES 5   // min waves per SIMD of the wave-job kernel (6 spills)
 
@@ -2448,18 +2445,6 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
             }
         }
         // ---- outputs of the resolved slots (all slots when finishing) ----
-        // A lane whose 4 elements all resolve into 4 consecutive slots (every lane of a job's first
-        // round, most of the later ones) writes them with one 16-byte and one 4-byte store when the
-        // slots are 4-aligned, instead of 4 dword and 4 byte stores.
-        const uint32_t c0   = wj * 256 + lane * 4;
-        const bool     vec4 = BRA_JOB_VEC_OUT && c0 + 3 < T && (finish || !(tied[0] || tied[1] || tied[2] || tied[3])) &&
-                          pos[1] == pos[0] + 1 && pos[2] == pos[0] + 2 && pos[3] == pos[0] + 3 && ((J.start + pos[0]) & 3u) == 0;
-        if (vec4)
-        {
-            const uint32_t slot = J.start + pos[0];
-            *reinterpret_cast<uint4*>(a.fsa + slot) = make_uint4(v[0] & 0xFFFFFFu, v[1] & 0xFFFFFFu, v[2] & 0xFFFFFFu, v[3] & 0xFFFFFFu);
-            *reinterpret_cast<uint32_t*>(a.L + slot) = (v[0] >> 24) | ((v[1] >> 24) << 8) | ((v[2] >> 24) << 16) | ((v[3] >> 24) << 24);
-        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -2468,11 +2453,8 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
                 continue;
             const uint32_t slot = J.start + pos[r];
             const uint32_t idx  = v[r] & 0xFFFFFFu;
-            if (!vec4)
-            {
-                a.fsa[slot] = idx;
-                a.L[slot]   = (uint8_t) (v[r] >> 24);
-            }
+            a.fsa[slot]         = idx;
+            a.L[slot]           = (uint8_t) (v[r] >> 24);
             if (MODE == MODE_RANK)
                 a.isa[BD.off + idx] = J.start + S.pos[g[r]] - boff;  // block-local start of the group
             if (idx == 0)

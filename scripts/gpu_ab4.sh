@@ -4,6 +4,7 @@
 # usage: O=gpurun_out/<tag> bash scripts/gpu_ab4.sh variant [variant ...]
 set -o pipefail
 O=${O:-gpurun_out/ab4}; mkdir -p $O
+timeout -k 10 120 python -u scripts/exp_pipeline.py 1 2 3 > $O/pipeline.log 2>&1; echo "pipeline rc $?"; cat $O/pipeline.log
 timeout -k 10 500 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_chunks.py tests/test_gpu_jobs.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc $rc: $(tail -1 $O/pytest.log)"; [ $rc -le 1 ] || exit $rc
 for rep in 1 2; do
