@@ -1968,6 +1968,119 @@ __device__ __forceinline__ void merge_level(uint32_t (&k)[2][4], JobLds<W>& S, u
     }
 }
 
+// Small sorts (16 <= P <= 128 slots: the later rounds' tied elements, small jobs).  In the 4-per-lane
+// layout a stage costs 4 registers' compare-exchanges whatever P is; here the keys of slots < P move
+// through LDS to R = 1 (P <= 64) or 2 (P = 128) registers per lane, slot s = R * lane + r, so a
+// stage costs R.  Network cost (VALU per lane): P = 16 70 + ~25 for the moves against 154, P = 64
+// 147 against 390, P = 128 329 against 552 (below 16 slots the moves cost more than they save).
+template <int R, uint32_t X, uint32_t Y>
+constexpr uint64_t lanes_where_r()
+{
+    uint64_t m = 0;
+    for (uint32_t l = 0; l < 64; ++l)
+    {
+        const bool a = ((R * l) & X) == 0, b = Y ? ((R * l) & Y) == 0 : true;
+        if (a == b)
+            m |= 1ull << l;
+    }
+    return m;
+}
+
+template <int R, int SIZE, int J>
+__device__ __forceinline__ void snet_stage(uint32_t (&k)[2][4])
+{
+    if constexpr (J >= R)
+    {
+        // partner J / R lanes away; the lower slot keeps the minimum where (slot & SIZE) == 0
+        constexpr uint64_t keep_min = lanes_where_r<R, SIZE, J>();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+        {
+            const uint32_t o[2] = {xlane<J / R>(k[0][r]), xlane<J / R>(k[1][r])};
+            cxk<2>(k, r, o, keep_min);
+        }
+    }
+    else
+    {
+        // R = 2, J = 1: the lane's own two slots, ascending where (2 lane & SIZE) == 0
+        uint32_t a[2] = {k[0][0], k[1][0]}, b[2] = {k[0][1], k[1][1]};
+        cxk_pair<2>(a, b, lanes_where_r<R, SIZE, 0>());
+        k[0][0] = a[0];
+        k[1][0] = a[1];
+        k[0][1] = b[0];
+        k[1][1] = b[1];
+    }
+    if constexpr (J > 1)
+        snet_stage<R, SIZE, J / 2>(k);
+}
+
+template <int R>
+__device__ __forceinline__ void snet_sort(uint32_t (&k)[2][4], int P)
+{
+    for (int size = 2; size <= P; size <<= 1)
+        switch (size)
+        {
+        case 2: snet_stage<R, 2, 1>(k); break;
+        case 4: snet_stage<R, 4, 2>(k); break;
+        case 8: snet_stage<R, 8, 4>(k); break;
+        case 16: snet_stage<R, 16, 8>(k); break;
+        case 32: snet_stage<R, 32, 16>(k); break;
+        case 64: snet_stage<R, 64, 32>(k); break;
+        default:
+            if constexpr (R == 2)
+                snet_stage<R, 128, 64>(k);
+            break;
+        }
+}
+
+// One wave's small sort.  S.kh is free during a sort (its last readers precede the caller's barrier).
+template <int W>
+__device__ __forceinline__ void job_sort_small(uint32_t (&k)[2][4], int P, JobLds<W>& S)
+{
+    const uint32_t lane = (uint32_t) lane_id();
+    uint64_t*      X    = S.kh;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (lane * 4 + r < (uint32_t) P)
+            X[lane * 4 + r] = ((uint64_t) k[1][r] << 32) | k[0][r];
+    job_sync<1>();
+    uint32_t q[2][4];
+    if (P <= 64)
+    {
+        const uint64_t x = lane < (uint32_t) P ? X[lane] : ~0ull;
+        q[0][0]          = (uint32_t) x;
+        q[1][0]          = (uint32_t) (x >> 32);
+        snet_sort<1>(q, P);
+        job_sync<1>();
+        if (lane < (uint32_t) P)
+            X[lane] = ((uint64_t) q[1][0] << 32) | q[0][0];
+    }
+    else
+    {
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+        {
+            const uint64_t x = X[2 * lane + r];
+            q[0][r]          = (uint32_t) x;
+            q[1][r]          = (uint32_t) (x >> 32);
+        }
+        snet_sort<2>(q, P);
+        job_sync<1>();
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+            X[2 * lane + r] = ((uint64_t) q[1][r] << 32) | q[0][r];
+    }
+    job_sync<1>();
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (lane * 4 + r < (uint32_t) P)
+        {
+            const uint64_t x = X[lane * 4 + r];
+            k[0][r]          = (uint32_t) x;
+            k[1][r]          = (uint32_t) (x >> 32);
+        }
+}
+
 // Sort of the job's 256*W 64-bit keys (4 consecutive per lane, slot e = wj*256 + lane*4 + r) over
 // the first P (power of two) slots: each wave's 256 slots by the in-wave bitonic phases (DPP /
 // permlane partners), then (W > 1, P > 256) merge-path levels across the waves.  Keys are unique
@@ -2005,7 +2118,11 @@ __device__ __forceinline__ void job_sort(uint64_t (&key)[4], int P, JobLds<W>& S
         dead = __builtin_amdgcn_ballot_w64((k[0][0] & k[1][0] & k[0][1] & k[1][1] & k[0][2] & k[1][2] & k[0][3] & k[1][3]) != ~0u) == 0;
     // the in-wave phases sort each wave's slots ascending (directions from the wave-local slot)
     const uint32_t el = (W > 1 && P > 256) ? (uint32_t) lane * 4 : e0;
-    for (int size = 2; size <= P; size <<= 1)
+    // wave jobs only: in the workgroup jobs the extra code cost a wave per SIMD (88 VGPRs)
+    const bool small = W == 1 && P >= 16 && P <= 128;
+    if (small)
+        job_sort_small<W>(k, P, S);
+    for (int size = 2; !small && size <= P; size <<= 1)
     {
         if (dead && size <= 256)
             continue;
@@ -2204,10 +2321,10 @@ __device__ __forceinline__ uint64_t make_key(uint32_t grp, uint32_t slot, uint64
 // rounds, rounds, jobs}; printed to stderr after each STRING encode.
 // Accumulated per wave in LDS and added to the device totals once, when the wave leaves the kernel
 // (per-phase device atomics queued behind each other and slowed the job kernels 20x).
-__device__ unsigned long long g_jt[2][10];
+__device__ unsigned long long g_jt[2][32];  // [10 + lg P]: round-1 sorts by log2 P, [21 + lg P]: later sorts
 __device__ __forceinline__ unsigned long long* jt_slots()
 {
-    __shared__ unsigned long long jt_s[16][10];
+    __shared__ unsigned long long jt_s[16][32];
     return jt_s[threadIdx.x >> 6];
 }
 #define JT_NOW() (wj == 0 ? (unsigned long long) clock64() : 0ull)
@@ -2220,13 +2337,13 @@ __device__ __forceinline__ unsigned long long* jt_slots()
 #define JT_INIT()                                  \
     do                                             \
     {                                              \
-        if (lane_id() < 10)                        \
+        if (lane_id() < 32)                        \
             jt_slots()[lane_id()] = 0;             \
     } while (0)
 #define JT_FLUSH(w2)                               \
     do                                             \
     {                                              \
-        if (lane_id() < 10)                        \
+        if (lane_id() < 32)                        \
             atomicAdd(&g_jt[w2][lane_id()], jt_slots()[lane_id()]); \
     } while (0)
 #else
@@ -2366,6 +2483,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
         JT_ADD(1, t1 - jt);
         jt = t1;
     }
+    JT_ADD(10 + __builtin_ctz((unsigned) P), 1);
     job_sort<W>(key, P, S, wj);
     {
         // payloads and round-2 key bits into sorted order
@@ -2516,6 +2634,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
             JT_ADD(4, t1 - jt);
             jt = t1;
         }
+        JT_ADD(21 + __builtin_ctz((unsigned) P), 1);
         job_sort<W>(key, P, S, wj);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -3890,11 +4009,17 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return false;
 #ifdef BRA_JOB_TIMING
     {
-        unsigned long long jt[2][10];
+        unsigned long long jt[2][32];
         BRA_HIP_CHECK(hipMemcpyFromSymbol(jt, HIP_SYMBOL(g_jt), sizeof jt));
         for (int k = 0; k < 2; ++k)
+        {
             fprintf(stderr, "[job timing %s] claim %llu gather1 %llu sort1 %llu groups+out %llu regather %llu sortN %llu | sorts %llu jobs %llu | between jobs %llu\n",
                     k ? "wg" : "wave", jt[k][0], jt[k][1], jt[k][2], jt[k][3], jt[k][4], jt[k][5], jt[k][6], jt[k][7], jt[k][8]);
+            fprintf(stderr, "[job sorts %s] P:", k ? "wg" : "wave");
+            for (int lg = 2; lg <= 10; ++lg)
+                fprintf(stderr, " %d:%llu/%llu", 1 << lg, jt[k][10 + lg], jt[k][21 + lg]);
+            fprintf(stderr, "\n");
+        }
         std::memset(jt, 0, sizeof jt);
         BRA_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_jt), jt, sizeof jt));
     }

@@ -430,10 +430,11 @@ struct WalkArgs
 };
 
 constexpr uint32_t IB_CHUNK = 256;
-#ifndef BRA_IB_WALK_WG
-#define BRA_IB_WALK_WG 2048
-#endif
-constexpr uint32_t IB_WALK_WG = BRA_IB_WALK_WG;  // persistent walk workgroups (EXPERIMENT: live splitters per XCD)
+// Persistent walk workgroups.  The grid sets how many blocks an XCD walks at once (lanes per XCD /
+// splitters per block): their TL arrays are what the random loads hit, so fewer live blocks keep
+// them in L2 / MALL.  Walk time for 256 x 1 MiB text (scripts/gpu_r4v.sh): 256 WGs 3.55 ms, 384
+// 3.07, 512 3.18, 768 3.59, 1024 3.88, 2048 4.29, 4096 4.31.
+constexpr uint32_t IB_WALK_WG = 384;
 
 __device__ __forceinline__ uint8_t* walk_dst(const WalkArgs& a, uint8_t* slot, uint32_t cap, uint32_t o, uint32_t& chunk, uint32_t g)
 {
