@@ -298,63 +298,45 @@ struct L0Tile
 
 // ---- packing (see "Packed key strings") ----
 // Presence mask of the byte values of every level-0 tile: tmask[8 * tile + w] bit v = value 32 w + v
-// occurs.  Each thread ORs its 16 bytes into 8 registers, DPP scans OR them over the wave, LDS over
-// the workgroup; plain stores, no atomics (same-address device atomics from every tile of a block
-// serialised this pass to half a millisecond).
+// occurs.  Each thread marks its 16 bytes in a 256-byte LDS table (plain byte stores of 1: any
+// order of same-address writes gives the same table; the OR-into-8-registers form cost 12 VALU per
+// byte, 116 µs per 256 MiB), then 8 threads fold 32 entries each into a mask word; plain stores,
+// no atomics (same-address device atomics from every tile of a block serialised this pass to half
+// a millisecond).
 __global__ void __launch_bounds__(TPB) k_alpha(const uint8_t* __restrict__ in, const BlockDesc* __restrict__ blocks,
                                                const L0Tile* __restrict__ tiles, uint32_t ntiles, uint32_t* __restrict__ tmask)
 {
-    __shared__ uint32_t part[TPB / WAVE][8];
+    __shared__ __attribute__((aligned(16))) uint8_t seen[256];
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
         const L0Tile    T   = tiles[t];
         const BlockDesc B   = blocks[T.block];
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
         const uint8_t*  p   = in + B.off + T.start;
-        uint32_t        m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        const auto      add  = [&](uint32_t v) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                m[k] |= ((v >> 5) == (uint32_t) k) ? (1u << (v & 31)) : 0u;
-        };
+        seen[threadIdx.x]   = 0;
+        __syncthreads();
         if (cnt == TILE && (((uintptr_t) p) & 15) == 0)
         {
             const uint4    q    = reinterpret_cast<const uint4*>(p)[threadIdx.x];
             const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-            if (!__builtin_amdgcn_ballot_w64(((q.x | q.y | q.z | q.w) & 0x80808080u) != 0))
-            {
-                // the whole wave's bytes are < 128 (text): 4 mask words, half the selects
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                {
-                    const uint32_t v = (w[i >> 2] >> (8 * (i & 3))) & 0x7Fu;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        m[k] |= ((v >> 5) == (uint32_t) k) ? (1u << (v & 31)) : 0u;
-                }
-            }
-            else
-#pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    add((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+            for (int i = 0; i < 16; ++i)
+                seen[(w[i >> 2] >> (8 * (i & 3))) & 0xFFu] = 1;
         }
         else
             for (uint32_t i = threadIdx.x; i < cnt; i += TPB)
-                add(p[i]);
-        const uint32_t wv = threadIdx.x / WAVE;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-        {
-            const uint32_t x = wave_scan<true>(m[k], 0u, OpOr());
-            if (lane_id() == WAVE - 1)
-                part[wv][k] = x;
-        }
+                seen[p[i]] = 1;
         __syncthreads();
         if (threadIdx.x < 8)
         {
-            uint32_t x = 0;
-            for (uint32_t v = 0; v < TPB / WAVE; ++v)
-                x |= part[v][threadIdx.x];
+            // entries 32 k .. 32 k + 31 (0 / 1 bytes) -> bits of mask word k
+            const uint4* s = reinterpret_cast<const uint4*>(seen) + 2 * threadIdx.x;
+            const uint4  a = s[0], b = s[1];
+            const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            uint32_t       x    = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                x |= (((d[j] * 0x01020408u) >> 24) & 0xFu) << (4 * j);  // bytes 0..3 (each 0 / 1) -> bits 0..3
             tmask[8 * (size_t) t + threadIdx.x] = x;
         }
         __syncthreads();

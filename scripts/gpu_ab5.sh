@@ -12,6 +12,6 @@ for rep in ${REPS:-1 2}; do
     BRA_HIP_LIB=$L timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-check --profile-all > $O/bench_${v}_$rep.json 2>> $O/bench.err
     rc=$?; [ $rc -eq 0 ] || { echo "bench $v rc $rc"; exit $rc; }
     python3 scripts/show_bench.py $O/bench_${v}_$rep.json | python3 -c "
-import sys; L=sys.stdin.read().splitlines(); print('$v', L[0][:60]); [print('  ', l) for l in L[1:] if any(k in l for k in ('jobs','scatter','scan','hist','level0'))]"
+import sys,os; L=sys.stdin.read().splitlines(); print('$v', L[0][:60]); [print('  ', l) for l in L[1:] if any(k in l for k in (os.environ.get('SHOW','jobs,scatter,scan,hist').split(',')))]"
   done
 done
