@@ -229,6 +229,10 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if args.backend != "nccl":
+        # rehearsal of the N > 1 path on fewer devices (gloo: ranks may share a GPU); counting the
+        # devices does not initialise the GPU
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         if args.backend == "nccl":
@@ -408,7 +412,9 @@ def main():
                 "global_bytes": global_total,
                 "batches_per_rank": len(batches),
                 "parallelism": f"dp{world}: block b on GPU b mod {world} (round robin)"
-                               + (", RCCL gather of compressed chunks + CRC shares to rank 0" if world > 1 else ""),
+                               + ((", RCCL gather of compressed chunks + CRC shares to rank 0" if args.backend == "nccl" else
+                                  f", {args.backend} gather through host copies (ranks sharing a GPU: rehearsal, not a scaling number)")
+                                 if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",

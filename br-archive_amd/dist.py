@@ -15,7 +15,9 @@ rank 0:
 
 With the "nccl" backend (RCCL on ROCm) the tensors are device tensors and the copies run over
 xGMI; the same gather runs with "gloo" on CPU tensors (tests/test_dist.py), where
-`assemble_host` is the host-side interleave used to check it.
+`assemble_host` is the host-side interleave used to check it, and with "gloo" on device tensors
+through host copies (`bench.py --gpus 2 --backend gloo`: ranks sharing one GPU rehearse the N > 1
+bench path end to end).
 """
 from __future__ import annotations
 
@@ -56,6 +58,12 @@ class ChunkGather:
         import torch
 
         dist, rank, world = self.dist, self.rank, self.world
+        # gloo with device tensors (the one-GPU rehearsal of the N > 1 path): the exchange goes
+        # through host copies; RCCL moves the device tensors themselves
+        host = hdr.is_cuda and dist.get_backend() == "gloo"
+        dev = hdr.device
+        if host:
+            hdr, off, pay, crc = hdr.cpu(), off.cpu(), pay[: int(off[-1].item())].cpu(), crc.cpu()
         # (payload bytes, block count) of every rank in one small all_gather
         meta = torch.cat([off[-1:], torch.full((1,), hdr.shape[0], dtype=torch.int64, device=off.device)])
         metas = [torch.empty_like(meta) for _ in range(world)]
@@ -93,6 +101,8 @@ class ChunkGather:
         for r in range(1, world):
             b = self.bufs[r]
             parts.append((b[0], b[1], b[2][: sizes[r]], b[3]))
+        if host:
+            parts = [tuple(t.to(dev) for t in p) for p in parts]
         return parts
 
 
