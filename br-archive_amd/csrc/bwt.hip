@@ -2100,9 +2100,11 @@ __device__ __forceinline__ void job_sort(uint64_t (&key)[4], int P, JobLds<W>& S
         dead = __builtin_amdgcn_ballot_w64((k[0][0] & k[1][0] & k[0][1] & k[1][1] & k[0][2] & k[1][2] & k[0][3] & k[1][3]) != ~0u) == 0;
     // the in-wave phases sort each wave's slots ascending (directions from the wave-local slot)
     const uint32_t el = (W > 1 && P > 256) ? (uint32_t) lane * 4 : e0;
-    // wave jobs only: in the workgroup jobs the extra code cost a wave per SIMD (88 VGPRs)
-    const bool small = W == 1 && P >= 16 && P <= 128;
-    if (small)
+    // Workgroup jobs (their wave 0; the other waves hold padding only): up to 64 slots -- the
+    // 128-slot form raised the 4-wave kernel to 88 allocated VGPRs (a wave per SIMD less, 6 %
+    // slower); up to 64 it stays at 80 (mjobs 3.20 vs 3.23 ms).
+    const bool small = P >= 16 && P <= (W == 1 ? 128 : 64);
+    if (small && wj == 0)
         job_sort_small<W>(k, P, S);
     for (int size = 2; !small && size <= P; size <<= 1)
     {
