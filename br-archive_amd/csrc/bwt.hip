@@ -273,17 +273,17 @@ __device__ __forceinline__ uint32_t dev_count(const uint32_t* p)
 // can follow the level loop without a copy or a stream synchronisation.  `seq` is stored last.
 struct Mail
 {
-    uint32_t n_big, n_tiles, overflow, n_groups, hmin, n_jobs, n_mjobs, seq;
+    uint32_t n_big, n_tiles, overflow, n_groups, hmin, n_jobs, n_mjobs, n_melems, seq;
 };
 
 __global__ void k_publish(const Counters* __restrict__ g, const Counters* __restrict__ lv, Mail* __restrict__ mail, uint32_t seq)
 {
     if (threadIdx.x != 0)
         return;
-    const uint32_t v[7] = {lv ? dev_count(&lv->n_big) : 0u, lv ? dev_count(&lv->n_tiles_next) : 0u, dev_count(&g->overflow), dev_count(&g->n_groups),
-                           dev_count(&g->hmin),  dev_count(&g->n_jobs),  dev_count(&g->n_mjobs)};
+    const uint32_t v[8] = {lv ? dev_count(&lv->n_big) : 0u, lv ? dev_count(&lv->n_tiles_next) : 0u, dev_count(&g->overflow), dev_count(&g->n_groups),
+                           dev_count(&g->hmin),  dev_count(&g->n_jobs),  dev_count(&g->n_mjobs), dev_count(&g->n_melems)};
     uint32_t* m = reinterpret_cast<uint32_t*>(mail);
-    for (int i = 0; i < 7; ++i)
+    for (int i = 0; i < 8; ++i)
         __hip_atomic_store(m + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&mail->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3343,6 +3343,7 @@ struct BwtWorkspace
     Counters* h_ctr          = nullptr;  // pinned copy (byte accounting when profiling)
     Mail*     h_mail         = nullptr;  // pinned, device-written mailbox records (one per level slot)
     uint32_t  mail_seq       = 0;
+    uint32_t  jobs_seq       = 0;        // the mailbox record posted right after an encode's jobs (bwt_encode_finish waits for it)
     L0Tile*   l0tiles        = nullptr;
     uint8_t*  packed         = nullptr;  // packed key strings (PackDesc.poff), N + PACK_PAD per block
     PackDesc* pkd            = nullptr;  // per block
@@ -3395,6 +3396,7 @@ static bool wait_mail(BwtWorkspace& w, uint32_t slot, uint32_t seq, hipStream_t 
             out.hmin     = __atomic_load_n(&m->hmin, __ATOMIC_RELAXED);
             out.n_jobs   = __atomic_load_n(&m->n_jobs, __ATOMIC_RELAXED);
             out.n_mjobs  = __atomic_load_n(&m->n_mjobs, __ATOMIC_RELAXED);
+            out.n_melems = __atomic_load_n(&m->n_melems, __ATOMIC_RELAXED);
             out.seq      = seq;
             if (out.overflow)
             {
@@ -3954,6 +3956,11 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         return false;
     if (!run_jobs(w, ph, s))
         return false;
+    // posted here, waited for in bwt_encode_finish after the caller has queued its later stages:
+    // the host resumes when the jobs are done, with the rest of the step still queued ahead of the
+    // device (posted at the end of the chain, the host waited for the whole step and the device
+    // idled while the next one was queued)
+    w.jobs_seq = post(w, 0, s);
     BRA_HIP_CHECK(hipGetLastError());
     w.last_ph = ph;
     w.last_n  = N;
@@ -3989,7 +3996,7 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     if (fallback_ran)
         *fallback_ran = false;
     Mail mc{};
-    if (!post_wait(w, 0, s, mc))
+    if (!wait_mail(w, 0, w.jobs_seq, s, mc))
         return false;
 #ifdef BRA_JOB_TIMING
     {
@@ -4010,13 +4017,8 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
 #endif
     // SURVEY 8.1(d) BWT model: 11 algorithmic bytes per element (input read, SA written and
     // re-read, L gathered and written), charged to the job kernels by the elements each kind covers
-    if (g_prof && (g_prof->mask >> P_BWT_JOBS & 1 || g_prof->mask >> P_BWT_MJOBS & 1))
-    {
-        BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-        BRA_HIP_CHECK(hipStreamSynchronize(s));
-        prof_bytes(P_BWT_JOBS, 11.0 * ((double) N - (double) w.h_ctr->n_melems));
-        prof_bytes(P_BWT_MJOBS, 11.0 * (double) w.h_ctr->n_melems);
-    }
+    prof_bytes(P_BWT_JOBS, 11.0 * ((double) N - (double) mc.n_melems));
+    prof_bytes(P_BWT_MJOBS, 11.0 * (double) mc.n_melems);
 
     // ---- fallback: prefix doubling on the groups still tied ----
     uint32_t ng = mc.n_groups;

@@ -387,9 +387,12 @@ static int encode_impl(bra_gpu_ctx_s* c, const uint8_t* d_in, const std::vector<
         rc = later_stages();  // L changed
     if (rc != 0)
         return rc;
-    if (g_prof && g_prof->mask)
+    constexpr uint64_t SIZE_SLOTS = 1ull << P_RLE_WRITE | 1ull << P_HUF_BUILD | 1ull << P_HUF_TILEBITS | 1ull << P_HUF_TILESCAN | 1ull << P_HUF_ZERO |
+                                    1ull << P_HUF_PACK | 1ull << P_HUF_OFFSETS;
+    if (g_prof && (g_prof->mask & SIZE_SLOTS))
     {
-        // sizes of the RLE outputs for the byte accounting of rle.write / huf.* (profiling only)
+        // sizes of the RLE outputs for the byte accounting of rle.write / huf.* (profiling those
+        // slots only: the copy waits for the step)
         std::vector<uint32_t> rs(nb);
         if (hipMemcpyAsync(rs.data(), c->d_rle_size, nb * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipMemcpyAsync(&total, d_payload_off + nb, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)

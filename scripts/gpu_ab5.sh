@@ -9,7 +9,7 @@ rc=$?; echo "pytest rc $rc: $(tail -1 $O/pytest.log)"; [ $rc -eq 0 ] || { tail -
 for rep in ${REPS:-1 2}; do
   for v in default "$@"; do
     L=$PWD/br-archive_amd/libbra_hip.so; [ $v = default ] || L=$PWD/br-archive_amd/build/variants/$v/libbra_hip.so
-    BRA_HIP_LIB=$L timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-check --profile-all > $O/bench_${v}_$rep.json 2>> $O/bench.err
+    BRA_HIP_LIB=$L timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-check ${BENCH_ARGS---profile-all} > $O/bench_${v}_$rep.json 2>> $O/bench.err
     rc=$?; [ $rc -eq 0 ] || { echo "bench $v rc $rc"; exit $rc; }
     python3 scripts/show_bench.py $O/bench_${v}_$rep.json | python3 -c "
 import sys,os; L=sys.stdin.read().splitlines(); print('$v', L[0][:60]); [print('  ', l) for l in L[1:] if any(k in l for k in (os.environ.get('SHOW','jobs,scatter,scan,hist').split(',')))]"
