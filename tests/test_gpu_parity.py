@@ -515,3 +515,23 @@ def test_single_block_small_and_full_alphabet(bra, orc):
         assert (bytes(h.lengths), h.orig_size, h.encoded_size, h.data) == orc.huffman_encode(r)
         assert bra.huffman_decode(h.lengths, h.orig_size, h.encoded_size, h.data) == r
         assert bra.rle_decode(r) == m and bra.mtf_decode(m) == L and bra.bwt_decode(L, pi) == x
+
+
+@pytest.mark.gpu
+def test_huffman_tied_frequencies(bra, orc):
+    """Code lengths where the reference's list order decides (bra_huffman.c:90-175): histograms
+    with many equal frequencies, smaller ones arriving before / after each group in symbol order,
+    against the oracle's restatement of the inserts."""
+    rng = np.random.default_rng(90175)
+    for case in range(300):
+        nsym = int(rng.integers(1, 257))
+        syms = rng.choice(256, size=nsym, replace=False)
+        top = int(rng.choice([1, 2, 3, 4, 8, 50]))
+        freq = rng.integers(1, top + 1, size=nsym)
+        if case % 3 == 0:  # a run of equal frequencies behind a smaller one, and one before it
+            freq[: nsym // 2] = top
+        data = np.repeat(syms.astype(np.uint8), freq)
+        rng.shuffle(data)
+        r = data.tobytes()
+        h = bra.huffman_encode(r)
+        assert (bytes(h.lengths), h.orig_size, h.encoded_size, h.data) == orc.huffman_encode(r), (case, nsym, top)
