@@ -23,7 +23,7 @@ struct IbwtWorkspace
     uint32_t *             m_next = nullptr, *m_len = nullptr, *m_ovf = nullptr, *m_start = nullptr, *ovl_next = nullptr;
     uint32_t *             m_order = nullptr, *m_cnt = nullptr;  // hops in output order, chain hops per block
     uint8_t *              slot = nullptr, *pool = nullptr;
-    uint32_t               cap_mb = 0, cap_ms = 0, pool_cap = 0, G = 0;
+    uint32_t               cap_mb = 0, cap_ms = 0, pool_cap = 0, G = 0, walk_wg = 384;
     uint64_t               cap_slot = 0;
     std::vector<uint64_t>  h_blk;
     std::vector<uint32_t>  h_ctl;

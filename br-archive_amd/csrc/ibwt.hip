@@ -430,11 +430,13 @@ struct WalkArgs
 };
 
 constexpr uint32_t IB_CHUNK = 256;
-// Persistent walk workgroups.  The grid sets how many blocks an XCD walks at once (lanes per XCD /
-// splitters per block): their TL arrays are what the random loads hit, so fewer live blocks keep
-// them in L2 / MALL.  Walk time for 256 x 1 MiB text (scripts/gpu_r4v.sh): 256 WGs 3.55 ms, 384
-// 3.07, 512 3.18, 768 3.59, 1024 3.88, 2048 4.29, 4096 4.31.
-constexpr uint32_t IB_WALK_WG = 384;
+// Persistent walk workgroups.  The grid sets how much of the TL arrays an XCD's lanes walk at once
+// (each live lane works one splitter hop of S entries): the random loads hit those bytes, so the
+// grid is sized to keep them near the XCD's 4 MB L2, with enough lanes left to hide the load
+// latency.  256 x 1 MiB text (S = 64, scripts/gpu_r4v.sh): 256 WGs 3.55 ms, 384 3.07 (12 K lanes
+// per XCD: 3 MB of TL), 512 3.18, 768 3.59, 1024 3.88, 2048 4.29, 4096 4.31; 32 x 8 MiB 16-symbol
+// blocks (S = 512, scripts/gpu_r4aq.sh): 128 WGs 7.95 ms, 192 6.66, 256 6.49, 384 6.74.
+__host__ inline uint32_t walk_grid(uint32_t max_shift) { return max_shift <= 6 ? 384u : 256u; }
 
 __device__ __forceinline__ uint8_t* walk_dst(const WalkArgs& a, uint8_t* slot, uint32_t cap, uint32_t o, uint32_t& chunk, uint32_t g)
 {
@@ -878,13 +880,14 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
         w.h_blk.assign(nblocks * 4, 0);
         std::vector<uint32_t> cum(nblocks + 1), ctl(512, 0);
         uint64_t              slot = 0;
-        uint32_t              G    = 0;
+        uint32_t              G = 0, max_shift = 6;
         for (uint32_t b = 0; b < nblocks; ++b)
         {
             const uint32_t n     = h_blocks[b].len;
             uint32_t       shift = 6;
             while (((uint64_t) n + (1u << shift) - 1) >> shift > IB_MAXS - 1)
                 ++shift;
+            max_shift = std::max(max_shift, shift);
             const uint32_t ns = (uint32_t) (((uint64_t) n + (1u << shift) - 1) >> shift);
             IbBlk          B{h_blocks[b].off, slot, n, shift, ns, 0};
             std::memcpy(&w.h_blk[(size_t) b * 4], &B, sizeof B);
@@ -893,6 +896,7 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
             slot += (uint64_t) (ns + 1) * (4u << shift);
         }
         cum[nblocks] = G;
+        w.walk_wg    = walk_grid(max_shift);
         // XCD x serves blocks [xr[x], xr[x+1]): contiguous eighths of the batch
         for (uint32_t x = 0; x <= 8; ++x)
             ctl[256 + x] = (uint32_t) ((uint64_t) nblocks * x / 8);
@@ -922,7 +926,7 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
                 n += h_blocks[b].len;
             prof_bytes(P_DEC_IB_WALK, 5.0 * n);
         }
-        hipLaunchKernelGGL(k_ib_walk3, dim3(IB_WALK_WG), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ib_walk3, dim3(w.walk_wg), dim3(256), 0, s, a);
     }
     hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
                        w.m_len, w.m_start, w.cyc, w.m_order, w.m_cnt);
