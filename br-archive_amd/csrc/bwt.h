@@ -16,7 +16,9 @@ const uint32_t* bwt_alpha_masks(const BwtWorkspace* w);
 const uint32_t* bwt_sa(const BwtWorkspace* w);
 // Diagnostics: re-run the last STRING encode's job phase `reps` times (inputs reordered when
 // shuffle_seed != 0) and audit every run; returns the failing jobs summed over the runs (-1: error).
-int bwt_debug_rerun_jobs(BwtWorkspace* w, int reps, hipStream_t s, uint32_t shuffle_seed);
+// Valid only right after an encode whose input the caller still holds; -1 otherwise.
+int  bwt_debug_rerun_jobs(BwtWorkspace* w, int reps, hipStream_t s, uint32_t shuffle_seed);
+void bwt_forget_jobs(BwtWorkspace* w);  // any other call on the context invalidates the re-run state
 
 // BWT of every block: d_L[off..off+len) = last column, d_pi[b] = primary index (block-local).
 bool bwt_encode_device(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,

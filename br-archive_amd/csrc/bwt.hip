@@ -65,6 +65,12 @@ constexpr uint32_t CSTRIDE    = 256 + 16;  // digit-counter copies (TileStagePN,
 constexpr int      SCATTER_NC = 4;  // digit-counter copies of the MSD scatter
 constexpr int      HIST_NC    = 4;  // counter copies of the MSD histogram (copy = lane & (NC - 1))
 constexpr uint32_t JQ_CHUNK   = 2;  // wave jobs a wave claims with one atomic (8: equal)
+// Former compile-time tuning knobs are constants now: a build that still passes one fails here
+// instead of measuring the default under another label.
+#if defined(JOB_MIN_WAVES) || defined(MJOB_MIN_WAVES) || defined(BRA_SCATTER_NC) || defined(BRA_TILE) || defined(HD2_REFB_BITS) || \
+    defined(BRA_SCAN_MIN_WAVES) || defined(BRA_HIST_NC)
+#error "removed tuning macro: these values are constants in bwt.hip"
+#endif
 #define MJOB_MIN_WAVES 5  // min waves per SIMD of the workgroup-job kernels (merge levels are LDS-latency bound: 4 -> 5 waves 4.37 -> 4.06 ms; 6 spills)
 #define JOB_MIN_WAVES 5   // min waves per SIMD of the wave-job kernel (6 spills)
 
@@ -3365,7 +3371,9 @@ struct BwtWorkspace
     uint32_t  nblocks    = 0;         // blocks of the current call
     uint32_t  levels     = 0;         // MSD levels enqueued by the last STRING level loop
     JobPhase  last_ph{};                // job launches and batch size of the last STRING encode (diagnostics)
-    uint64_t  last_n     = 0;
+    uint64_t  last_n     = 0;         // 0: no job phase to re-run (none yet, a fallback rewrote the lists, or another call ran since)
+    uint32_t* audit_cnt  = nullptr;   // slot-cover counts of the job audit (allocated on first use)
+    uint64_t  audit_cap  = 0;
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
@@ -3504,7 +3512,7 @@ static void ws_free(BwtWorkspace& w)
     }
     void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
                    w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask, w.l0tot, w.l0base,
-};
+                   w.audit_cnt};
     for (void* p : dev)
         (void) hipFree(p);
     if (w.h_ctr)
@@ -3523,6 +3531,11 @@ static void ws_free(BwtWorkspace& w)
 BwtWorkspace* bwt_workspace_create() { return new BwtWorkspace(); }
 const uint32_t* bwt_alpha_masks(const BwtWorkspace* w) { return w ? w->amask : nullptr; }
 const uint32_t* bwt_sa(const BwtWorkspace* w) { return w ? w->fsa : nullptr; }
+void            bwt_forget_jobs(BwtWorkspace* w)
+{
+    if (w)
+        w->last_n = 0;
+}
 void          bwt_workspace_destroy(BwtWorkspace* w)
 {
     if (w)
@@ -3740,15 +3753,16 @@ static bool account_levels(BwtWorkspace& w, hipStream_t s)
 // failing jobs (-1 on a HIP error).
 static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hipStream_t s)
 {
-    static uint32_t* cnt = nullptr;
-    static uint64_t  cap = 0;
-    if (N > cap)
+    if (N > w.audit_cap)
     {
-        (void) hipFree(cnt);
-        if (hipMalloc(&cnt, N * 4) != hipSuccess)
+        (void) hipFree(w.audit_cnt);
+        w.audit_cnt = nullptr;
+        w.audit_cap = 0;
+        if (hipMalloc(&w.audit_cnt, N * 4) != hipSuccess)
             return -1;
-        cap = N;
+        w.audit_cap = N;
     }
+    uint32_t* const cnt = w.audit_cnt;
     static const uint32_t zero = 0;
     uint32_t              fails = 0;
     if (hipMemsetAsync(cnt, 0, N * 4, s) != hipSuccess ||
@@ -3803,9 +3817,11 @@ static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hi
 
 // Re-runs the job phase of the last STRING encode `reps` times on the unchanged lists and payloads
 // (the jobs only read them) and audits every run; returns the failing jobs summed over the runs.
+// Valid only right after a STRING encode on this workspace whose input buffer the caller still
+// holds (the job launches read it); -1 when there is nothing to re-run.
 int bwt_debug_rerun_jobs(BwtWorkspace* wp, int reps, hipStream_t s, uint32_t seed)
 {
-    if (!wp->last_n)
+    if (!wp->last_n || reps < 0)
         return -1;
     int total = 0;
     for (int r = 0; r < reps; ++r)
@@ -3851,6 +3867,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         bra_hip_report("bwt: batch too large (%llu bytes)", (unsigned long long) N);
         return false;
     }
+    w.last_n = 0;  // the job phase of an earlier encode is no longer re-runnable
     if (!ws_reserve(w, N, nblocks))
         return false;
     w.nblocks = nblocks;
@@ -4029,6 +4046,7 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
         return true;
     if (fallback_ran)
         *fallback_ran = true;
+    w.last_n = 0;  // the fallback refills the job lists and counters with RANK-mode work
     BRA_PROF(P_BWT_FALLBACK, s);
     int gcur = 0;
     hipLaunchKernelGGL(k_group_depth_chars, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pkd);
@@ -4133,19 +4151,22 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
 extern "C" int bra_gpu_sortnet_selftest(int waves, unsigned groups, unsigned iters, unsigned seed, const unsigned long long* keys)
 {
     using namespace bra;
+    if ((waves != 1 && waves != 2 && waves != 4) || groups == 0)
+        return -1;
     uint32_t* d = nullptr;
     uint64_t* dk = nullptr;
     uint32_t  h = 0, tfix = 0;
+    int       rc = -1;
     if (hipMalloc(&d, 4) != hipSuccess)
         return -1;
     if (keys)
     {
-        for (int c = 0; c < 256 * waves; ++c)
+        const size_t nk = 256u * (unsigned) waves;
+        for (size_t c = 0; c < nk; ++c)
             tfix += keys[c] != ~0ull;
-        if (hipMalloc(&dk, 256 * 4 * 8) != hipSuccess || hipMemcpy(dk, keys, 256 * waves * 8, hipMemcpyHostToDevice) != hipSuccess)
-            return -1;
+        if (hipMalloc(&dk, nk * 8) != hipSuccess || hipMemcpy(dk, keys, nk * 8, hipMemcpyHostToDevice) != hipSuccess)
+            goto done;
     }
-    int rc = -1;
     if (hipMemset(d, 0, 4) == hipSuccess)
     {
         if (waves == 1)
@@ -4157,6 +4178,8 @@ extern "C" int bra_gpu_sortnet_selftest(int waves, unsigned groups, unsigned ite
         if (hipGetLastError() == hipSuccess && hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost) == hipSuccess)
             rc = (int) std::min<uint32_t>(h, 0x7FFFFFFF);
     }
+done:
+    (void) hipGetLastError();
     (void) hipFree(d);
     (void) hipFree(dk);
     return rc;

@@ -429,6 +429,7 @@ static int decode_impl(bra_gpu_ctx_s* c, const bra_io_chunk_header_t* d_headers,
                        const std::vector<BlockDesc>& hb, uint8_t* d_out, hipStream_t s, bool flex = false, uint64_t out_cap = 0,
                        uint64_t* out_size = nullptr, std::vector<uint32_t>* out_sizes = nullptr)
 {
+    bwt_forget_jobs(c->bwt);  // the job phase of the last encode is no longer re-runnable
     const uint32_t nb = (uint32_t) hb.size();
     if (nb == 0)
         return -1;

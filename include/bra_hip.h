@@ -251,7 +251,10 @@ const void* bra_gpu_stage_ptr(bra_gpu_ctx_t* ctx, int stage);
  * bra_gpu_debug_rerun_jobs re-runs the job phase of the last batch encode `reps` times on its
  * unchanged job lists -- with every job's input payloads put in another order first when
  * shuffle_seed != 0 -- and checks each run (no slot covered by two jobs, every job's output
- * rotations = its input rotations); returns the failing jobs summed over the runs, -1 on an error.
+ * rotations = its input rotations); returns the failing jobs summed over the runs, -1 on an error
+ * or when there is nothing to re-run: only right after a batch encode on the context (no decode or
+ * fallback since), with that encode's input buffer still allocated and unchanged.
+ * bra_gpu_sortnet_selftest: waves must be 1, 2 or 4 and groups >= 1 (else -1).
  * bra_gpu_sortnet_selftest sorts groups x iters random key sets (or the 256 * waves given keys,
  * slot order, padding all ones) with the job sort of `waves` waves and returns the failing sorts.
  */

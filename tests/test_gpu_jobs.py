@@ -37,3 +37,26 @@ def test_job_phase_any_input_order(kind, bs, nb):
         assert codec.debug_rerun_jobs(200, 1000) == 0
     finally:
         codec.close()
+
+
+def test_debug_entry_points_reject_stale_or_invalid_requests():
+    """the sort self-test takes 1, 2 or 4 waves only, and the job re-run refuses once a
+    decode (or a fallback) has run on the context since the encode."""
+    for w in (0, 3, 8, -1):
+        with pytest.raises(RuntimeError):
+            bra.sortnet_selftest(w, 1, 1, 1)
+    codec = bra.BlockCodec(0)
+    try:
+        bs = 65536
+        d = torch.from_numpy(bra.synth_fill(bra.SYNTH_TEXT, 4 * bs, bs)).cuda()
+        with pytest.raises(RuntimeError):
+            codec.debug_rerun_jobs(1)  # nothing encoded yet
+        hdr, off, pay = codec.encode(d, bs)
+        torch.cuda.synchronize()
+        assert codec.debug_rerun_jobs(2) == 0
+        out = codec.decode(hdr, off, pay, d.numel(), bs)
+        assert torch.equal(out, d)
+        with pytest.raises(RuntimeError):
+            codec.debug_rerun_jobs(1)
+    finally:
+        codec.close()
