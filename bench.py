@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--profile-all", action="store_true", help="time every kernel during the timed steps")
     ap.add_argument("--no-secondary", action="store_true", help="skip the decode and PCIe-inclusive measurements")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--pcie-batches", type=int, default=4, help="batches of the overlapped transfer-inclusive encode")
     return ap.parse_args()
 
 
@@ -142,6 +143,11 @@ def cpu_baseline(data_np, bs, threads, gpu_chunks, all_host_cores=True):
                      "affinity_cpus": na, "cgroup_cpu_max": cgroup_cpu_max(),
                      "sample": f"{na_blocks} x {bs} B blocks, one block per task on {min(na, na_blocks)} threads ({dta:.2f} s wall)",
                      "same_output_as_16_thread_run": bool(ok_all)}
+        quota = cgroup_cpu_max().split()
+        if len(quota) == 2 and quota[0].isdigit() and quota[1].isdigit() and int(quota[1]):
+            cpus = int(quota[0]) / int(quota[1])
+            all_cores["note"] = (f"the cgroup quota caps this process at {cpus:g} CPUs, so {min(na, na_blocks)} threads share {cpus:g} CPUs: "
+                                 f"the {threads}-thread figure above is this host's real ceiling for the reference encoder")
     return {
         "value": round(nm * bs / dtm / 1e9, 6),
         "unit": "GB/s",
@@ -217,6 +223,86 @@ def check_vs_reference(H, O, P, kind, bs, nbg, global_total, world, threads):
     return res
 
 
+def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work_stream, nbatch):
+    """Transfer-inclusive encode (SURVEY 8.1(d) secondary): pinned host input -> HBM, encode, chunk
+    headers + payload back to pinned host memory, timed from the first byte sent to the last byte
+    received.  Serial: one copy in, one encode, copies out, on one stream.  Overlapped: the input in
+    `nbatch` batches -- every host-to-device copy queued at once on a copy stream (batch k's encode
+    waits for its copy's event), each batch's payload copied back on a third stream as soon as the
+    host has read its size (the host reads it only after queueing the next batch's encode, so the
+    device never waits for the host) -- so the copies run under the kernels of other batches."""
+    import torch
+
+    total = data_np.size
+    h_in = torch.from_numpy(data_np).pin_memory()
+    h_hdr = torch.empty(hdr.shape, dtype=torch.uint8).pin_memory()
+    h_pay = torch.empty((payload_bytes + 4096 * (nbatch + 1),), dtype=torch.uint8).pin_memory()
+    res = {}
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(2):
+        with torch.cuda.stream(work_stream):
+            d.copy_(h_in, non_blocking=True)
+            codec.encode(d, bs, hdr, off, pay, stream=work_stream)
+            h_hdr.copy_(hdr, non_blocking=True)
+            h_pay[:payload_bytes].copy_(pay[:payload_bytes], non_blocking=True)
+    torch.cuda.synchronize()
+    res["encode_pcie_inclusive_serial_GBps"] = round(2 * total / (time.perf_counter() - t1) / 1e9, 4)
+    # overlapped: batches of whole blocks
+    per = max(1, -(-nb // nbatch))
+    parts = [(b0, min(nb, b0 + per)) for b0 in range(0, nb, per)]
+    h2d, d2h = torch.cuda.Stream(), torch.cuda.Stream()
+    offs = [torch.empty((b1 - b0 + 1,), dtype=torch.int64, device=d.device) for b0, b1 in parts]
+    cap = [int((b1 - b0) * bs * 1.25) + 64 * (b1 - b0) + 65536 for b0, b1 in parts]
+    pbase = [sum(cap[:k]) for k in range(len(parts))]
+    if pbase[-1] + cap[-1] > pay.numel():
+        return res
+    sizes = torch.empty((len(parts),), dtype=torch.int64).pin_memory()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        ev_in = []
+        with torch.cuda.stream(h2d):
+            for b0, b1 in parts:
+                lo, hi = b0 * bs, min(total, b1 * bs)
+                d[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
+                e = torch.cuda.Event()
+                e.record(h2d)
+                ev_in.append(e)
+        ev_enc, hbase = [], 0
+
+        def drain(k):
+            nonlocal hbase
+            ev_enc[k].synchronize()  # batch k's encode is done (the device is busy with the next one)
+            sz = int(sizes[k])
+            with torch.cuda.stream(d2h):
+                d2h.wait_event(ev_enc[k])
+                b0, b1 = parts[k]
+                h_hdr[b0:b1].copy_(hdr[b0:b1], non_blocking=True)
+                h_pay[hbase:hbase + sz].copy_(pay[pbase[k]:pbase[k] + sz], non_blocking=True)
+            hbase += sz
+
+        for k, (b0, b1) in enumerate(parts):
+            lo, hi = b0 * bs, min(total, b1 * bs)
+            work_stream.wait_event(ev_in[k])
+            with torch.cuda.stream(work_stream):
+                codec.encode(d[lo:hi], bs, hdr[b0:b1], offs[k], pay[pbase[k]:pbase[k] + cap[k]], stream=work_stream)
+                sizes[k:k + 1].copy_(offs[k][-1:], non_blocking=True)
+                e = torch.cuda.Event()
+                e.record(work_stream)
+                ev_enc.append(e)
+            if k > 0:
+                drain(k - 1)
+        drain(len(parts) - 1)
+        d2h.synchronize()
+    torch.cuda.synchronize()
+    res["encode_pcie_inclusive_GBps"] = round(reps * total / (time.perf_counter() - t1) / 1e9, 4)
+    res["encode_pcie_inclusive_batches"] = len(parts)
+    res["encode_pcie_inclusive_bytes_back"] = int(hbase + hdr.numel())
+    return res
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -253,19 +339,52 @@ def main():
     d = torch.from_numpy(data_np).cuda()
     codec = bra.BlockCodec(local)
     dev = d.device
-    hdr = torch.empty((nb, bra.HEADER_BYTES), dtype=torch.uint8, device=dev)
-    off = torch.empty((nb + 1,), dtype=torch.int64, device=dev)
-    pay = torch.empty((int(my_bytes * 1.25) + 64 * nb + 65536,), dtype=torch.uint8, device=dev)
-    crc_share = torch.zeros((1,), dtype=torch.int32, device=dev)
+    def outputs():
+        return (torch.empty((nb, bra.HEADER_BYTES), dtype=torch.uint8, device=dev), torch.empty((nb + 1,), dtype=torch.int64, device=dev),
+                torch.empty((int(my_bytes * 1.25) + 64 * nb + 65536,), dtype=torch.uint8, device=dev),
+                torch.zeros((1,), dtype=torch.int32, device=dev))
+
+    # world > 1: two output sets, so that step i + 1 encodes while step i's chunks are gathered
+    outs = [outputs() for _ in range(2 if world > 1 else 1)]
+    hdr, off, pay, crc_share = outs[0]
     per_batch = max(1, args.batch_bytes // bs)
     batches = [(b0, min(nb, b0 + per_batch)) for b0 in range(0, nb, per_batch)]
     off_b = torch.empty((per_batch + 1,), dtype=torch.int64, device=dev)
     gather = dmod.ChunkGather(dist, rank, world) if world > 1 else None
     work_stream = torch.cuda.Stream()
+    gather_stream = torch.cuda.Stream() if world > 1 else None
     result = {}
+    state = {"i": 0, "pending": None, "free": [None] * len(outs)}
+
+    def gather_assemble(k, ev):
+        """Gather output set k (its encode ended at event ev) to rank 0 and assemble it there, on the
+        gather stream: the collectives wait for that encode only, not for the one queued after it, so
+        the host's read of the gathered sizes (ChunkGather) finds them ready and the transfers run
+        under the next step's kernels."""
+        with torch.cuda.stream(gather_stream):
+            gather_stream.wait_event(ev)
+            parts = gather(*outs[k])
+            if rank == 0:
+                result["stream"] = dmod.assemble(codec, parts, round_robin=True, stream=gather_stream)
+                result["crc_t"] = dmod.merge_crc_device(parts)
+            e = torch.cuda.Event()
+            e.record(gather_stream)
+            state["free"][k] = e  # the set's sends are done: the next encode into it may start
+
+    def flush():
+        if state["pending"] is not None:
+            gather_assemble(*state["pending"])
+            state["pending"] = None
 
     def step():
-        """Encode this rank's blocks, CRC share, gather to rank 0, assemble there in global order."""
+        """Encode this rank's blocks and its CRC share; rank 0 assembles the chunks in global order.
+        World > 1: the gather of this step's output to rank 0 is issued after the next step's encode
+        has been queued (flush() issues the last one), so no rank waits on the host for the others."""
+        k = state["i"] % len(outs)
+        state["i"] += 1
+        hdr, off, pay, crc_share = outs[k]
+        if state["free"][k] is not None:
+            work_stream.wait_event(state["free"][k])
         with torch.cuda.stream(work_stream):
             if len(batches) == 1:
                 codec.encode(d, bs, hdr, off, pay, stream=work_stream)
@@ -277,21 +396,25 @@ def main():
                     off[b0:b1 + 1] = off_b[: b1 - b0 + 1] + base
                     base += int(off_b[b1 - b0].item())
             codec.chunks_crc32c_shard(d, hdr, bs, rank, world, global_total, rank == 0, out=crc_share, stream=work_stream)
-            if world > 1:
-                parts = gather(hdr, off, pay, crc_share)
-            else:
+            if world == 1:
+                # assembled on the stream and the CRC merged on the device: a step has no host wait of
+                # its own, so the host queues the next step while this one runs
                 parts = [(hdr, off, pay, crc_share)]  # the payload's capacity: no host read of its size
-            if rank == 0:
-                # assembled on the stream and the CRC shares merged on the device: a step has no host
-                # wait of its own (world 1), so the host queues the next step while this one runs
                 result["stream"] = dmod.assemble(codec, parts, round_robin=True)
                 result["crc_t"] = dmod.merge_crc_device(parts)
+                return
+            ev = torch.cuda.Event()
+            ev.record(work_stream)
+        prev, state["pending"] = state["pending"], (k, ev)
+        if prev is not None:
+            gather_assemble(*prev)
 
     # ---- find the dominant kernel (one untimed, fully profiled pass) ----
     kernel_slots = [s for s in codec.SLOTS if not s.startswith(("stage.", "dec."))]
     enc_slots = [s for s in codec.SLOTS if not s.startswith("dec.")]
     codec.prof_enable(codec.slot_mask(*enc_slots))
     step()
+    flush()
     torch.cuda.synchronize()
     prof0 = codec.prof_read()
     kernel_slots = [s for s in kernel_slots if s in prof0]  # (a library built before a slot existed reports fewer)
@@ -302,6 +425,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     codec.prof_reset()
 
@@ -312,6 +436,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    flush()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -375,20 +500,7 @@ def main():
                     "kernels_ms": {s: round(dp[s][0] / max(1, dp[s][1]), 4) for s in codec.DECODE_KERNELS}}
             del out
         if not args.no_secondary and world == 1 and len(batches) == 1:
-            # PCIe-inclusive encode: pinned host input -> HBM, encode, headers + payload back to pinned host
-            h_in = torch.from_numpy(data_np).pin_memory()
-            h_hdr = torch.empty(hdr.shape, dtype=torch.uint8).pin_memory()
-            h_pay = torch.empty((payload_bytes + 4096,), dtype=torch.uint8).pin_memory()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(2):
-                with torch.cuda.stream(work_stream):
-                    d.copy_(h_in, non_blocking=True)
-                    codec.encode(d, bs, hdr, off, pay, stream=work_stream)
-                    h_hdr.copy_(hdr, non_blocking=True)
-                    h_pay[: payload_bytes].copy_(pay[: payload_bytes], non_blocking=True)
-            torch.cuda.synchronize()
-            secondary["encode_pcie_inclusive_GBps"] = round(2 * global_total / (time.perf_counter() - t1) / 1e9, 4)
+            secondary.update(pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work_stream, args.pcie_batches))
 
         line = {
             "metric": METRIC,
