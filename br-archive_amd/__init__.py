@@ -41,6 +41,7 @@ ABI_SYMBOLS = (
     "bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host",
     "bra_gpu_chunks_crc32c_shard", "bra_gpu_assemble_shards",
     "bra_gpu_debug_rerun_jobs", "bra_gpu_sortnet_selftest",
+    "bra_gpu_host_alloc", "bra_gpu_host_free", "bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect",
 )
 MAX_CHUNK_SIZE = 256 * 1024  # BRA_MAX_CHUNK_SIZE (src/lib_bra_defs.h:93): the .BRa chunk size
 
@@ -148,6 +149,14 @@ def _load() -> C.CDLL:
     lib.bra_gpu_compress_chunks.restype = C.c_int
     lib.bra_gpu_decompress_chunks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, u64p, C.c_uint32, u32p, vp]
     lib.bra_gpu_decompress_chunks.restype = C.c_int
+    lib.bra_gpu_host_alloc.argtypes = [vp, C.c_uint64]
+    lib.bra_gpu_host_alloc.restype = vp
+    lib.bra_gpu_host_free.argtypes = [vp, vp]
+    lib.bra_gpu_host_free.restype = None
+    lib.bra_gpu_compress_chunks_submit.argtypes = [vp, C.c_int, vp, C.c_uint64, C.c_uint32]
+    lib.bra_gpu_compress_chunks_submit.restype = C.c_int
+    lib.bra_gpu_compress_chunks_collect.argtypes = [vp, C.c_int, vp, C.c_uint64, u64p, u32p]
+    lib.bra_gpu_compress_chunks_collect.restype = C.c_int
     lib.bra_gpu_chunks_crc32c_shard.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int,
                                                 vp, vp]
     lib.bra_gpu_chunks_crc32c_shard.restype = C.c_int
@@ -401,6 +410,41 @@ class BlockCodec:
         if rc < 0:
             raise RuntimeError(f"bra_gpu_compress_chunks failed ({rc})")
         return out[: size.value], crc.value, rc == 1
+
+    def compress_chunks_pipelined(self, data_np, batch_bytes: int, block_size: int = MAX_CHUNK_SIZE):
+        """Host-buffer compression in batches with two in flight (bra_gpu_compress_chunks_submit /
+        _collect, the front end's loop): [(records bytes, batch crc, compressed?)] per batch."""
+        import numpy as np
+
+        total = int(data_np.size)
+        bb = max(block_size, batch_bytes // block_size * block_size)
+        spans = [(o, min(total, o + bb)) for o in range(0, total, bb)]
+        cap = lib.bra_gpu_chunks_bound(bb, block_size)
+        hin = [lib.bra_gpu_host_alloc(self.ctx, bb) for _ in range(2)]
+        hout = lib.bra_gpu_host_alloc(self.ctx, cap)
+        if not all(hin) or not hout:
+            raise RuntimeError("bra_gpu_host_alloc failed")
+        res = []
+        try:
+            def submit(k):
+                lo, hi = spans[k]
+                C.memmove(hin[k % 2], data_np[lo:hi].ctypes.data, hi - lo)
+                if lib.bra_gpu_compress_chunks_submit(self.ctx, k % 2, hin[k % 2], hi - lo, block_size) != 0:
+                    raise RuntimeError("bra_gpu_compress_chunks_submit failed")
+
+            submit(0)
+            for k in range(len(spans)):
+                if k + 1 < len(spans):
+                    submit(k + 1)
+                size, crc = C.c_uint64(), C.c_uint32()
+                rc = lib.bra_gpu_compress_chunks_collect(self.ctx, k % 2, hout, cap, C.byref(size), C.byref(crc))
+                if rc < 0:
+                    raise RuntimeError(f"bra_gpu_compress_chunks_collect failed ({rc})")
+                res.append((C.string_at(hout, size.value), crc.value, rc == 1))
+        finally:
+            for p in (*hin, hout):
+                lib.bra_gpu_host_free(self.ctx, p)
+        return res
 
     def decompress_chunks(self, stream_t, block_size: int = MAX_CHUNK_SIZE, out_cap: int | None = None, prev_crc: int = 0, stream=None):
         """The reference decode loop on the device: (decoded tensor, crc chained from prev_crc)."""

@@ -220,6 +220,19 @@ struct bra_gpu_ctx_s
     uint64_t       cap_eb = 0, cap_erb = 0;
     hipEvent_t     null_ev = nullptr;  // CallStream: the null stream's position at a NULL-stream call
     Prof           prof;
+    // pipelined host-buffer chunk compression (bra_gpu_compress_chunks_submit / _collect)
+    struct PipeSlot
+    {
+        uint8_t*   d_in = nullptr;
+        uint8_t*   d_out = nullptr;
+        uint64_t   cap_in = 0, cap_out = 0;
+        hipEvent_t ev_in = nullptr, ev_done = nullptr;
+        uint64_t   data_size = 0;
+        uint32_t   nb = 0;
+        int        state = 0;  // 0 free, 1 submitted
+    } pipe[2];
+    hipStream_t    copy_in = nullptr, copy_out = nullptr;
+    uint64_t*      h_pipe_mail = nullptr;  // pinned: per slot {payload bytes, chunk-stream CRC}
 };
 
 static bool ctx_init(bra_gpu_ctx_s* c, int device)
@@ -248,6 +261,21 @@ static void ctx_free(bra_gpu_ctx_s* c)
                     c->d_word,    c->d_enc_blocks, c->d_enc_rle_base, c->d_hin, c->d_hout};
     for (void* p : ptrs)
         (void) hipFree(p);
+    for (auto& ps : c->pipe)
+    {
+        (void) hipFree(ps.d_in);
+        (void) hipFree(ps.d_out);
+        if (ps.ev_in)
+            (void) hipEventDestroy(ps.ev_in);
+        if (ps.ev_done)
+            (void) hipEventDestroy(ps.ev_done);
+    }
+    if (c->h_pipe_mail)
+        (void) hipHostFree(c->h_pipe_mail);
+    if (c->copy_in)
+        (void) hipStreamDestroy(c->copy_in);
+    if (c->copy_out)
+        (void) hipStreamDestroy(c->copy_out);
     if (c->stream)
         (void) hipStreamDestroy(c->stream);
     if (c->null_ev)
@@ -896,6 +924,116 @@ int bra_gpu_compress_chunks_host(bra_gpu_ctx_t* c, const uint8_t* h_in, uint64_t
     if (hipMemcpy(h_out, c->d_hout, osz, hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return rc;
+}
+
+// ---- pipelined host-buffer chunk compression (row f1 with the copies under the kernels) ----
+// Two slots: while slot k's encode runs on the context stream, the next batch's input copy runs on
+// copy_in and the previous batch's records come back on copy_out.  The chunk records of a slot are
+// framed into the slot's own device buffer, so a later encode never overwrites records not yet
+// copied back.  (An optimal prefix code over byte symbols is never longer than the 8-bit code, so a
+// block's payload is at most its RLE bytes + 1: the slot buffers use that bound.)
+static uint64_t pipe_records_bound(const std::vector<BlockDesc>& hb)
+{
+    uint64_t r = 64;
+    for (const BlockDesc& b : hb)
+        r += rle_capacity(b.len) + 16 + CHUNK_HDR_DISK;
+    return r;
+}
+
+void* bra_gpu_host_alloc(bra_gpu_ctx_t* c, uint64_t bytes)
+{
+    if (!c || !bytes)
+        return nullptr;
+    DevGuard dg(c->device);
+    void* p = nullptr;
+    if (!dg.ok || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess)
+    {
+        (void) hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void bra_gpu_host_free(bra_gpu_ctx_t* c, void* p)
+{
+    if (!c || !p)
+        return;
+    DevGuard dg(c->device);
+    (void) hipHostFree(p);
+}
+
+int bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* c, int slot, const uint8_t* h_in, uint64_t data_size, uint32_t block_size)
+{
+    if (!c || slot < 0 || slot > 1 || !h_in || !data_size || !block_size || block_size >= (1u << 24))
+        return -1;
+    auto& ps = c->pipe[slot];
+    if (ps.state != 0)
+        return -1;  // collect the slot first
+    DevGuard dg(c->device);
+    if (!dg.ok)
+        return -1;
+    if (!c->copy_in && (hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
+                        hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess))
+        return -1;
+    if (!c->h_pipe_mail && hipHostMalloc(&c->h_pipe_mail, 4 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+    {
+        c->h_pipe_mail = nullptr;
+        return -1;
+    }
+    if ((!ps.ev_in && hipEventCreateWithFlags(&ps.ev_in, hipEventDisableTiming) != hipSuccess) ||
+        (!ps.ev_done && hipEventCreateWithFlags(&ps.ev_done, hipEventDisableTiming) != hipSuccess))
+        return -1;
+    const auto     hb  = geometry(data_size, block_size);
+    const uint32_t nb  = (uint32_t) hb.size();
+    const uint64_t rb  = pipe_records_bound(hb);
+    hipStream_t    s   = c->stream;
+    if (!grow(ps.d_in, ps.cap_in, data_size + 16) || !grow(ps.d_out, ps.cap_out, rb + 16) || !grow(c->d_hdr, c->cap_hdr, nb) ||
+        !grow(c->d_off, c->cap_off, nb + 1) || !grow(c->d_pay, c->cap_pay, rb) || !grow(c->d_word, c->cap_word, 4))
+        return -1;
+    if (hipMemcpyAsync(ps.d_in, h_in, data_size, hipMemcpyHostToDevice, c->copy_in) != hipSuccess || hipEventRecord(ps.ev_in, c->copy_in) != hipSuccess ||
+        hipStreamWaitEvent(s, ps.ev_in, 0) != hipSuccess)
+        return -1;
+    g_prof = c->prof.mask ? &c->prof : nullptr;
+    int rc = encode_impl(c, ps.d_in, hb, c->d_hdr, c->d_off, c->d_pay, c->cap_pay, s, nullptr);
+    g_prof = nullptr;
+    uint64_t* mail = c->h_pipe_mail + 2 * slot;
+    if (rc == 0 &&
+        (!frame_chunks_device(reinterpret_cast<const uint8_t*>(c->d_hdr), c->d_off, c->d_pay, nb, ps.d_out, s) ||
+         !crc_stream_device(ps.d_in, data_size, block_size, reinterpret_cast<const uint8_t*>(c->d_hdr), 0, c->d_word, s) ||
+         hipMemcpyAsync(mail, c->d_off + nb, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+         hipMemcpyAsync(mail + 1, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipEventRecord(ps.ev_done, s) != hipSuccess))
+        rc = -1;
+    if (rc != 0)
+    {
+        (void) hipStreamSynchronize(s);
+        return -1;
+    }
+    ps.data_size = data_size;
+    ps.nb        = nb;
+    ps.state     = 1;
+    return 0;
+}
+
+int bra_gpu_compress_chunks_collect(bra_gpu_ctx_t* c, int slot, uint8_t* h_out, uint64_t out_cap, uint64_t* out_size, uint32_t* chunks_crc)
+{
+    if (!c || slot < 0 || slot > 1 || c->pipe[slot].state != 1)
+        return -1;
+    auto& ps = c->pipe[slot];
+    ps.state = 0;
+    DevGuard dg(c->device);
+    if (!dg.ok || hipEventSynchronize(ps.ev_done) != hipSuccess)
+        return -1;
+    const uint64_t* mail = c->h_pipe_mail + 2 * slot;
+    const uint64_t  need = mail[0] + (uint64_t) CHUNK_HDR_DISK * ps.nb;
+    if (out_size)
+        *out_size = need;
+    if (chunks_crc)
+        *chunks_crc = (uint32_t) mail[1];
+    if (need > out_cap || !h_out)
+        return need > out_cap ? -2 : -1;
+    if (hipMemcpyAsync(h_out, ps.d_out, need, hipMemcpyDeviceToHost, c->copy_out) != hipSuccess || hipStreamSynchronize(c->copy_out) != hipSuccess)
+        return -1;
+    return need < ps.data_size ? 1 : 0;  // 0: not smaller than the input -> STORED (lib_bra_io_file_chunks.c:274-278)
 }
 
 int bra_gpu_decompress_chunks_host(bra_gpu_ctx_t* c, const uint8_t* h_stream, uint64_t stream_size, uint32_t block_size, uint8_t* h_out,

@@ -153,6 +153,42 @@ bool bra_io_file_chunks_copy_file(bra_io_file_t* dst, bra_io_file_t* src, const 
 
 static uint64_t num_chunks(uint64_t n) { return (n + CHUNK_SIZE - 1) / CHUNK_SIZE; }
 
+/* A batch read from the source file on a helper thread, so that reading batch k + 2 overlaps the
+ * device work of batches k and k + 1 (the reference reads, encodes and writes one chunk after the
+ * other, lib_bra_io_file_chunks.c:199-266). */
+typedef struct
+{
+    bra_io_file_t* src;
+    uint8_t*       buf;
+    uint64_t       n;
+    bool           ok;
+    pthread_t      th;
+    bool           running;
+} batch_read_t;
+
+static void* batch_read_main(void* arg)
+{
+    batch_read_t* r = (batch_read_t*) arg;
+    r->ok           = bra_io_file_read(r->src, r->buf, r->n);
+    return NULL;
+}
+
+static void batch_read_start(batch_read_t* r, bra_io_file_t* src, uint8_t* buf, uint64_t n)
+{
+    r->src = src, r->buf = buf, r->n = n, r->ok = false;
+    r->running = pthread_create(&r->th, NULL, batch_read_main, r) == 0;
+    if (!r->running)
+        r->ok = bra_io_file_read(src, buf, n); /* no thread: read inline */
+}
+
+static bool batch_read_join(batch_read_t* r)
+{
+    if (r->running)
+        pthread_join(r->th, NULL);
+    r->running = false;
+    return r->ok;
+}
+
 bool bra_io_file_chunks_compress_file(bra_io_file_t* dst, bra_io_file_t* src, const uint64_t data_size, bra_meta_entry_t* me)
 {
     assert(dst != NULL && src != NULL && me != NULL);
@@ -167,41 +203,81 @@ bool bra_io_file_chunks_compress_file(bra_io_file_t* dst, bra_io_file_t* src, co
         bra_log_error("unable to compress file: %s", src->fn);
         return false;
     }
-    const uint64_t batch = _bra_min((uint64_t) BATCH_CHUNKS * CHUNK_SIZE, data_size);
-    const uint64_t cap   = bra_gpu_chunks_bound(batch, (uint32_t) CHUNK_SIZE);
-    uint8_t*       in    = (uint8_t*) malloc(batch ? batch : 1);
-    uint8_t*       out   = (uint8_t*) malloc(cap ? cap : 1);
-    uint32_t       crc32 = BRA_CRC32C_INIT; /* the running CRC of header + source chunk pairs (:214,248-249) */
-    bool           ok    = in != NULL && out != NULL;
-    for (uint64_t done = 0; ok && done < data_size;)
+    // Batches of BATCH_CHUNKS chunks, two in flight on the device (bra_gpu_compress_chunks_submit /
+    // _collect): batch k + 1's input copy and kernels are queued before batch k's records are
+    // copied back and written, and batch k + 2 is read from the file meanwhile.  Pinned host
+    // buffers make the copies asynchronous.
+    const uint64_t batch  = _bra_min((uint64_t) BATCH_CHUNKS * CHUNK_SIZE, data_size);
+    const uint64_t nbatch = batch ? (data_size + batch - 1) / batch : 0;
+    const uint64_t cap    = bra_gpu_chunks_bound(batch, (uint32_t) CHUNK_SIZE);
+    uint8_t*       in[2]  = {(uint8_t*) bra_gpu_host_alloc(ctx, batch ? batch : 1), (uint8_t*) bra_gpu_host_alloc(ctx, batch ? batch : 1)};
+    uint8_t*       out    = (uint8_t*) bra_gpu_host_alloc(ctx, cap ? cap : 1);
+    uint32_t       crc32  = BRA_CRC32C_INIT; /* the running CRC of header + source chunk pairs (:214,248-249) */
+    bool           ok     = in[0] != NULL && in[1] != NULL && out != NULL;
+    bool           read_failed = false, pending[2] = {false, false};
+    batch_read_t   rd;
+    memset(&rd, 0, sizeof rd);
+#define BATCH_LEN(k) _bra_min(batch, data_size - (uint64_t) (k) * batch)
+    if (ok && nbatch > 0)
     {
-        const uint64_t n = _bra_min(batch, data_size - done);
-        bra_log_printf("%3u%%", (unsigned int) (done * 100 / data_size));
+        read_failed = !bra_io_file_read(src, in[0], BATCH_LEN(0));
+        ok          = !read_failed && bra_gpu_compress_chunks_submit(ctx, 0, in[0], BATCH_LEN(0), (uint32_t) CHUNK_SIZE) == 0;
+        pending[0]  = ok;
+        if (ok && nbatch > 1)
+            batch_read_start(&rd, src, in[1], BATCH_LEN(1));
+    }
+    for (uint64_t k = 0; ok && k < nbatch; ++k)
+    {
+        bra_log_printf("%3u%%", (unsigned int) (k * batch * 100 / data_size));
         bra_log_printf("\b\b\b\b");
-        if (!bra_io_file_read(src, in, n))
+        if (k + 1 < nbatch)
         {
-            bra_io_file_close(&tmpfile);
-            bra_io_file_close(dst);
-            free(in);
-            free(out);
-            return false;
+            // batch k + 1 was read into in[(k + 1) % 2]; in[k % 2] is free (batch k's input copy ended
+            // before its jobs, which its submit waited for): batch k + 2 is read into it meanwhile
+            if (!batch_read_join(&rd))
+            {
+                read_failed = true;
+                break;
+            }
+            if (k + 2 < nbatch)
+                batch_read_start(&rd, src, in[k % 2], BATCH_LEN(k + 2));
+            if (bra_gpu_compress_chunks_submit(ctx, (int) ((k + 1) % 2), in[(k + 1) % 2], BATCH_LEN(k + 1), (uint32_t) CHUNK_SIZE) != 0)
+            {
+                bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, (k + 1) * batch);
+                ok = false;
+                break;
+            }
+            pending[(k + 1) % 2] = true;
         }
-        uint64_t osz = 0;
+        uint64_t osz  = 0;
         uint32_t bcrc = 0;
-        const int rc = bra_gpu_compress_chunks_host(ctx, in, n, (uint32_t) CHUNK_SIZE, out, cap, &osz, &bcrc);
-        if (rc < 0)
+        pending[k % 2] = false;
+        if (bra_gpu_compress_chunks_collect(ctx, (int) (k % 2), out, cap, &osz, &bcrc) < 0)
         {
-            bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, done);
+            bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, k * batch);
             ok = false;
             break;
         }
         // this batch's share of the running CRC: its headers and chunks follow the previous ones
+        const uint64_t n = BATCH_LEN(k);
         crc32 = bra_gpu_crc32c_combine(crc32, bcrc, n + num_chunks(n) * sizeof(bra_io_chunk_header_t));
         ok    = bra_io_file_write(&tmpfile, out, (size_t) osz);
-        done += n;
     }
-    free(in);
-    free(out);
+#undef BATCH_LEN
+    (void) batch_read_join(&rd);
+    for (int q = 0; q < 2; ++q)
+        if (pending[q])  // a batch still in flight after an error: drained, its records dropped
+            (void) bra_gpu_compress_chunks_collect(ctx, q, NULL, 0, NULL, NULL);
+    bra_gpu_host_free(ctx, in[0]);
+    bra_gpu_host_free(ctx, in[1]);
+    bra_gpu_host_free(ctx, out);
+    if (read_failed)
+    {
+        // the reference's read-error path (:203-210): tmpfile and dst closed, the caller closes src
+        bra_io_file_close(&tmpfile);
+        bra_io_file_close(dst);
+        return false;
+    }
     if (!ok)
     {
         bra_io_file_close(&tmpfile);

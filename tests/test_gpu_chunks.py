@@ -287,3 +287,40 @@ def test_round_robin_shards_assemble_and_crc(bra, codec, world, nblocks, tail):
     # too small a payload buffer is reported, not overrun
     with pytest.raises(RuntimeError):
         codec.assemble_shards([(h, o, p) for h, o, p, _ in parts], payload=torch.empty((16,), dtype=torch.uint8, device="cuda"))
+
+
+@pytest.mark.parametrize("name", [n for n, g in sorted(_golden().items()) if g["compressed"]])
+def test_pipelined_host_compression_vs_reference_golden(bra, name):
+    """bra_gpu_compress_chunks_submit / _collect (the front end's overlapped loop, two batches in
+    flight, batches of 2 chunks) give the reference's tmpfile bytes and, folded per batch the way
+    the front end folds them, its chunk-stream CRC."""
+    g = _golden()[name]
+    data = case_input(bra, g)
+    c = bra.BlockCodec(0)
+    try:
+        res = c.compress_chunks_pipelined(data, 2 * CS, CS)
+    finally:
+        c.close()
+    s = b"".join(r[0] for r in res)
+    assert len(s) == g["stream_size"]
+    assert hashlib.sha256(s).hexdigest() == g["stream_sha256"]
+    crc, done = 0, 0
+    for (_, bcrc, _), o in zip(res, range(0, data.size, 2 * CS)):
+        n = min(2 * CS, data.size - o)
+        crc = bra.crc32c_combine(crc, bcrc, n + (-(-n // CS)) * 268)
+    assert bra.entry_crc32c(g["entry_crc_before"], len(s), crc, g["total"]) == g["entry_crc"]
+
+
+def test_pipelined_host_compression_long_stream(bra, codec):
+    """Many batches through the two slots (text, 6 MiB + 100 B in 1 MiB batches) == the one-call device loop."""
+    import torch
+
+    data = bra.synth_fill(0, (6 << 20) + 100, CS)
+    want, wcrc, _ = codec.compress_chunks(torch.from_numpy(data).cuda(), CS)
+    res = codec.compress_chunks_pipelined(data, 1 << 20, CS)
+    assert b"".join(r[0] for r in res) == want.cpu().numpy().tobytes()
+    crc = 0
+    for (_, bcrc, _), o in zip(res, range(0, data.size, 1 << 20)):
+        n = min(1 << 20, data.size - o)
+        crc = bra.crc32c_combine(crc, bcrc, n + (-(-n // CS)) * 268)
+    assert crc == wcrc
