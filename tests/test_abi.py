@@ -90,4 +90,4 @@ def test_lib_bra_links_against_gpu_library(lib):
     if lib == "libbralib_hipenc.so":  # the reference's own chunk loop calls the drop-in encoders
         assert {"bra_bwt_encode2", "bra_mtf_encode2", "bra_rle_encode", "bra_huffman_encode", "bra_huffman_chunk_free"} <= need
     else:  # the batched front end calls the batch ABI
-        assert {"bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host"} <= need
+        assert {"bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect", "bra_gpu_decompress_chunks_host"} <= need
