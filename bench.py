@@ -253,7 +253,9 @@ def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work
     parts = [(b0, min(nb, b0 + per)) for b0 in range(0, nb, per)]
     h2d, d2h = torch.cuda.Stream(), torch.cuda.Stream()
     offs = [torch.empty((b1 - b0 + 1,), dtype=torch.int64, device=d.device) for b0, b1 in parts]
-    cap = [int((b1 - b0) * bs * 1.25) + 64 * (b1 - b0) + 65536 for b0, b1 in parts]
+    # payload room per batch: a block's payload never exceeds its RLE bytes + 1 (an optimal prefix
+    # code over byte symbols is never longer than the 8-bit code)
+    cap = [(b1 - b0) * (bs + bs // 128 + 64) + 4096 for b0, b1 in parts]
     pbase = [sum(cap[:k]) for k in range(len(parts))]
     if pbase[-1] + cap[-1] > pay.numel():
         return res

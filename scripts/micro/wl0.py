@@ -39,7 +39,7 @@ opay = torch.empty(n * nb, dtype=torch.int64, device="cuda")
 odig = torch.empty(n * nb, dtype=torch.uint8, device="cuda")
 lib.wl0_set_attr()
 s = torch.cuda.current_stream().cuda_stream
-for P in [int(a) for a in sys.argv[1:]] or [2, 4, 8]:
+for P in [int(a) for a in sys.argv[1:]] or [2, 4, 8, 16]:
     def run():
         assert lib.wl0_launch(d.data_ptr(), rk.data_ptr(), n, nb, starts.data_ptr(), opay.data_ptr(), odig.data_ptr(), P, s) == 0
     opay.fill_(-1)
