@@ -1508,8 +1508,8 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
 // so nothing needs a device-wide fence; the roots are claimed with one atomic each.
 // -------------------------------------------------------------------------------------------------
 constexpr uint32_t LOCAL_MAX   = 65536;  // default root size limit (BRA_LOCAL_MAX overrides; 0 = off)
-constexpr uint32_t LOCAL_STACK = 256;    // >= LOCAL_MAX_CAP / 257
-constexpr uint32_t LOCAL_MAX_CAP = LOCAL_STACK * (JOB_MAX + 1);  // the largest root the stack bound covers
+constexpr uint32_t LOCAL_STACK = 128;    // pending children: disjoint, each > mjob_max >= 256 elements
+constexpr uint32_t LOCAL_MAX_CAP = LOCAL_STACK * (256 * MJ_WAVES_DEF + 1);  // the largest root the stack bound covers (see local_limit)
 
 struct LocalArgs
 {
@@ -1539,18 +1539,128 @@ struct LocalLds
     uint32_t sp;
     uint32_t run[256];  // next free slot of each sub-bucket (absolute)
     uint32_t tot[256];
-    uint8_t  nxt[256];  // sub-bucket continues (its elements get the next digit byte; regathered payloads)
+    uint8_t  nxt[256];  // 1: the sub-bucket continues (regathered payloads); 2: and it is split in passes (it needs its digit bytes)
     uint32_t Ew[256], Sw[256];  // wave_job_pack scratch
     uint8_t  nxs[256];
     uint32_t nomove;    // 1: one sub-bucket holds the whole bucket (nothing moves)
 };
 
+// Wave 0 of k_msd_local: the bucket's sub-buckets from L.tot (the rules of k_scan): cursors and
+// continue flags into L, wave jobs / workgroup jobs / fallback groups into the call's lists,
+// continuing children onto the stack.
+__device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, const Bucket& B)
+{
+    const int lane = lane_id();
+    uint32_t  tot[4], base[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        tot[r] = L.tot[lane * 4 + r];
+    wave_excl_sum4(tot, base);
+    const bool     nomove   = __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
+    const bool     regather = B.d + 1 - B.kd >= CARRY;
+    const uint32_t kd       = regather ? B.d + 1 : B.kd;
+    const uint32_t nd       = B.d + 1;
+    const uint32_t obuf     = nomove ? B.buf : 1u - B.buf;
+    bool           med[4], fin[4], nbn[4];
+    uint32_t       cm[4], cg[4], cb[4], mex[4], gex[4], bex[4], nm = 0, ng = 0, nb = 0, gmem = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const bool big = tot[r] > a.mjob_max;
+        med[r]         = tot[r] > JOB_MAX && !big;
+        fin[r]         = big && nd >= a.dcap;
+        nbn[r]         = big && !fin[r];
+        cm[r]          = med[r] ? 1u : 0u;
+        cg[r]          = fin[r] ? 1u : 0u;
+        cb[r]          = nbn[r] ? 1u : 0u;
+        gmem += fin[r] ? tot[r] : 0u;
+        L.run[lane * 4 + r] = B.start + base[r];
+        L.nxt[lane * 4 + r] = nbn[r] ? (tot[r] > (uint32_t) TILE ? 2 : 1) : 0;
+    }
+    WaveJobs wj;
+    wave_job_pack(tot, base, B.len, L.Ew, L.Sw, L.nxs, wj);
+    wave_excl_sum4(cm, mex, &nm);
+    wave_excl_sum4(cg, gex, &ng);
+    wave_excl_sum4(cb, bex, &nb);
+    for (int d = 32; d >= 1; d >>= 1)
+        gmem += __shfl_xor(gmem, d, WAVE);
+    uint32_t pj = 0, pm = 0, pg = 0;
+    if (lane == 0)
+    {
+        if (wj.jtot || nm)
+        {
+            const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) nm << 32) | wj.jtot);
+            pj = (uint32_t) old;
+            pm = (uint32_t) (old >> 32);
+        }
+        if (ng)
+        {
+            pg = atomicAdd(&a.ctr->n_groups, ng);
+            atomicAdd(&a.ctr->g_members, gmem);
+            atomicMin(&a.ctr->hmin, nd);
+        }
+        if (a.account)
+        {
+            atomicAdd(&a.ctr->n_local_buckets, 1u);
+            if (!nomove)
+                atomicAdd(&a.ctr->n_local_moved, B.len);
+        }
+        L.nomove = nomove ? 1u : 0u;
+    }
+    pj = __builtin_amdgcn_readfirstlane(pj);
+    pm = __builtin_amdgcn_readfirstlane(pm);
+    pg = __builtin_amdgcn_readfirstlane(pg);
+    const uint32_t sp = L.sp;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const uint32_t s0 = B.start + base[r];
+        if (wj.jstart[r])
+        {
+            const uint32_t slot = pj + wj.jidx[r];
+            if (slot < a.cap_jobs)
+                a.jobs[slot] = Job{s0, wj.jlen[r], wj.single[r] ? 1u : 0u, obuf, B.block, B.gdepth, nd};
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+        }
+        if (med[r])
+        {
+            const uint32_t slot = pm + mex[r];
+            if (slot < a.cap_mjobs)
+                a.mjobs[slot] = Job{s0, tot[r], kd, obuf, B.block, B.gdepth, nd};
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+        }
+        if (fin[r])
+        {
+            const uint32_t slot = pg + gex[r];
+            if (slot < a.cap_groups)
+                a.groups[slot] = Group{s0, tot[r], nd, B.block | (obuf << 31)};
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+        }
+        if (nbn[r])
+        {
+            // a child split in passes that stays put and keeps its carried digits reads them from
+            // the payloads (tile0 = 1: dig[] holds this depth's digit)
+            const uint32_t k = sp + bex[r];
+            if (k < LOCAL_STACK)
+                L.stk[k] = Bucket{s0, tot[r], nd, kd, B.block, obuf, B.gdepth, (nomove && !regather) ? 1u : 0u};
+            else
+                atomicExch(&a.ctr->overflow, 1u);
+        }
+    }
+    if (lane == 0)
+        L.sp = min(sp + nb, LOCAL_STACK);
+}
+
 __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStageS& S = *reinterpret_cast<TileStageS*>(smem);
-    LocalLds&   L = *reinterpret_cast<LocalLds*>(smem + sizeof(TileStageS));
-    const int   lane = lane_id(), wv = threadIdx.x >> 6;
+    TileStageS& S  = *reinterpret_cast<TileStageS*>(smem);
+    LocalLds&   L  = *reinterpret_cast<LocalLds*>(smem + sizeof(TileStageS));
+    const int   wv = threadIdx.x >> 6;
+    const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
     if (threadIdx.x == 0)
         L.sp = 0;
     __syncthreads();
@@ -1574,38 +1684,126 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
         const Bucket B = L.cur;
         if (B.len == 0)
             break;  // uniform: no root left and the stack is empty
-        const PackDesc P    = a.pk[B.block];
-        const uint8_t* pk   = a.packed + P.poff;
-        const uint32_t j    = B.d - B.kd;  // this depth's digit in the payloads (always < CARRY)
-        uint64_t*       ip  = (B.buf ? a.pay1 : a.pay0) + B.start;
-        uint8_t*        id  = (B.buf ? a.dig1 : a.dig0) + B.start;
-        const bool      pdig = B.tile0 != 0;  // the digits are in the payloads, not in dig[]
-        // ---- histogram of the bucket's digits (NC counter copies) ----
-        stage_zero(S);
-        __syncthreads();
+        const PackDesc P  = a.pk[B.block];
+        const uint8_t* pk = a.packed + P.poff;
+        const uint32_t j  = B.d - B.kd;  // this depth's digit in the payloads (always < CARRY)
+        const bool     rg = j + 1 >= CARRY;  // continuing children start a new carry
+        const uint32_t dn = B.d + 1;
+        uint64_t*      ip = (B.buf ? a.pay1 : a.pay0) + B.start;
+        uint8_t*       id = (B.buf ? a.dig1 : a.dig0) + B.start;
+        uint64_t*      op = B.buf ? a.pay0 : a.pay1;
+        uint8_t*       od = B.buf ? a.dig0 : a.dig1;
+        if (B.len <= (uint32_t) TILE)
         {
-            const uint32_t cp = (uint32_t) (lane & (SCATTER_NC - 1)) * CSTRIDE;
-            for (uint32_t e = threadIdx.x * PER_THREAD; e < B.len; e += TILE)
+            // ---- one pass: the payloads are loaded once; their carried digit gives the counts,
+            // the classification and the staging order ----
+            const uint32_t cnt = B.len;
+            uint64_t       v[PER_THREAD];
+            uint32_t       dg[PER_THREAD], rank[PER_THREAD];
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
             {
-                if (pdig)
+                const uint32_t e = threadIdx.x + i * TPB;
+                v[i]             = (e < cnt) ? ip[e] : 0ull;
+                dg[i]            = p_digit(v[i], j);
+            }
+            stage_zero(S);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+                if (threadIdx.x + i * TPB < cnt)
+                    rank[i] = atomicAdd(&S.cnt[cp + dg[i]], 1u);
+            __syncthreads();
+            {
+                uint32_t c[SCATTER_NC], tot = 0;
+#pragma unroll
+                for (int k = 0; k < SCATTER_NC; ++k)
                 {
-#pragma unroll 4
-                    for (int i = 0; i < PER_THREAD; ++i)
-                        if (e + i < B.len)
-                            atomicAdd(&S.cnt[cp + p_digit(ip[e + i], j)], 1u);
+                    c[k] = S.cnt[k * CSTRIDE + threadIdx.x];
+                    tot += c[k];
                 }
-                else if (e + PER_THREAD <= B.len)
+                const uint32_t b = block256_exclusive_sum(tot, S.tmp);
+                S.base[threadIdx.x] = b;
+                L.tot[threadIdx.x]  = tot;
+                uint32_t run        = b;
+#pragma unroll
+                for (int k = 0; k < SCATTER_NC; ++k)
                 {
-                    const uint4    q     = *reinterpret_cast<const uint4_u*>(id + e);
-                    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+                    S.cnt[k * CSTRIDE + threadIdx.x] = run;
+                    run += c[k];
+                }
+            }
+            __syncthreads();
+            if (wv == 0)
+                local_classify(a, L, B);
+            __syncthreads();
+            if (L.nomove)
+            {
+                // nothing moves; the one child re-carries its digits in place when they run out
+                // (it is split in one pass too: no digit bytes)
+                if (rg)
 #pragma unroll
                     for (int i = 0; i < PER_THREAD; ++i)
-                        atomicAdd(&S.cnt[cp + ((w4[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
-                }
-                else
-                    for (uint32_t i = e; i < B.len; ++i)
-                        atomicAdd(&S.cnt[cp + id[i]], 1u);
+                    {
+                        const uint32_t e = threadIdx.x + i * TPB;
+                        if (e < cnt)
+                            ip[e] = p_make(pk, P.b, P.nbits, dn, v[i]);
+                    }
+                __syncthreads();
+                continue;
             }
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+                if (threadIdx.x + i * TPB < cnt)
+                    S.pay[S.cnt[cp + dg[i]] + rank[i]] = v[i];
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < PER_THREAD; ++i)
+            {
+                const uint32_t q = threadIdx.x + i * TPB;
+                if (q < cnt)
+                {
+                    const uint64_t vv   = S.pay[q];
+                    const uint32_t dd   = p_digit(vv, j);
+                    const uint32_t nx   = L.nxt[dd];
+                    const uint32_t slot = L.run[dd] + (q - S.base[dd]);
+                    const uint64_t nv   = (rg && nx) ? p_make(pk, P.b, P.nbits, dn, vv) : vv;
+                    if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "local scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
+                    {
+                        op[slot] = nv;
+                        if (nx == 2)
+                            od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));
+                    }
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        // ---- larger buckets: a histogram pass over the digit bytes (or the payloads' digit),
+        // then the scatter 4096 elements at a time ----
+        const bool pdig = B.tile0 != 0;  // the digits are in the payloads, not in dig[]
+        stage_zero(S);
+        __syncthreads();
+        for (uint32_t e = threadIdx.x * PER_THREAD; e < B.len; e += TILE)
+        {
+            if (pdig)
+            {
+#pragma unroll 4
+                for (int i = 0; i < PER_THREAD; ++i)
+                    if (e + i < B.len)
+                        atomicAdd(&S.cnt[cp + p_digit(ip[e + i], j)], 1u);
+            }
+            else if (e + PER_THREAD <= B.len)
+            {
+                const uint4    q     = *reinterpret_cast<const uint4_u*>(id + e);
+                const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int i = 0; i < PER_THREAD; ++i)
+                    atomicAdd(&S.cnt[cp + ((w4[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
+            }
+            else
+                for (uint32_t i = e; i < B.len; ++i)
+                    atomicAdd(&S.cnt[cp + id[i]], 1u);
         }
         __syncthreads();
         {
@@ -1616,116 +1814,9 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
             L.tot[threadIdx.x] = t;
         }
         __syncthreads();
-        // ---- wave 0: sub-bucket starts, classification, jobs / groups out, children pushed ----
         if (wv == 0)
-        {
-            uint32_t tot[4], base[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                tot[r] = L.tot[lane * 4 + r];
-            wave_excl_sum4(tot, base);
-            const bool     nomove   = __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
-            const bool     regather = B.d + 1 - B.kd >= CARRY;
-            const uint32_t kd       = regather ? B.d + 1 : B.kd;
-            const uint32_t nd       = B.d + 1;
-            const uint32_t obuf     = nomove ? B.buf : 1u - B.buf;
-            bool           med[4], fin[4], nbn[4];
-            uint32_t       cm[4], cg[4], cb[4], mex[4], gex[4], bex[4], nm = 0, ng = 0, nb = 0, gmem = 0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-                const bool big = tot[r] > a.mjob_max;
-                med[r]         = tot[r] > JOB_MAX && !big;
-                fin[r]         = big && nd >= a.dcap;
-                nbn[r]         = big && !fin[r];
-                cm[r]          = med[r] ? 1u : 0u;
-                cg[r]          = fin[r] ? 1u : 0u;
-                cb[r]          = nbn[r] ? 1u : 0u;
-                gmem += fin[r] ? tot[r] : 0u;
-                L.run[lane * 4 + r] = B.start + base[r];
-                L.nxt[lane * 4 + r] = nbn[r] ? 1 : 0;
-            }
-            WaveJobs wj;
-            wave_job_pack(tot, base, B.len, L.Ew, L.Sw, L.nxs, wj);
-            wave_excl_sum4(cm, mex, &nm);
-            wave_excl_sum4(cg, gex, &ng);
-            wave_excl_sum4(cb, bex, &nb);
-            for (int d = 32; d >= 1; d >>= 1)
-                gmem += __shfl_xor(gmem, d, WAVE);
-            uint32_t pj = 0, pm = 0, pg = 0;
-            if (lane == 0)
-            {
-                if (wj.jtot || nm)
-                {
-                    const unsigned long long old =
-                        atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) nm << 32) | wj.jtot);
-                    pj = (uint32_t) old;
-                    pm = (uint32_t) (old >> 32);
-                }
-                if (ng)
-                {
-                    pg = atomicAdd(&a.ctr->n_groups, ng);
-                    atomicAdd(&a.ctr->g_members, gmem);
-                    atomicMin(&a.ctr->hmin, nd);
-                }
-                if (a.account)
-                {
-                    atomicAdd(&a.ctr->n_local_buckets, 1u);
-                    if (!nomove)
-                        atomicAdd(&a.ctr->n_local_moved, B.len);
-                }
-                L.nomove = nomove ? 1u : 0u;
-            }
-            pj = __builtin_amdgcn_readfirstlane(pj);
-            pm = __builtin_amdgcn_readfirstlane(pm);
-            pg = __builtin_amdgcn_readfirstlane(pg);
-            const uint32_t sp = L.sp;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-            {
-                const uint32_t s0 = B.start + base[r];
-                if (wj.jstart[r])
-                {
-                    const uint32_t slot = pj + wj.jidx[r];
-                    if (slot < a.cap_jobs)
-                        a.jobs[slot] = Job{s0, wj.jlen[r], wj.single[r] ? 1u : 0u, obuf, B.block, B.gdepth, nd};
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
-                if (med[r])
-                {
-                    const uint32_t slot = pm + mex[r];
-                    if (slot < a.cap_mjobs)
-                        a.mjobs[slot] = Job{s0, tot[r], kd, obuf, B.block, B.gdepth, nd};
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
-                if (fin[r])
-                {
-                    const uint32_t slot = pg + gex[r];
-                    if (slot < a.cap_groups)
-                        a.groups[slot] = Group{s0, tot[r], nd, B.block | (obuf << 31)};
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
-                if (nbn[r])
-                {
-                    // a child that stays put and keeps its carried digits reads them from the
-                    // payloads (dig[] holds this depth's digit); every other child's digit bytes are
-                    // written below
-                    const uint32_t k = sp + bex[r];
-                    if (k < LOCAL_STACK)
-                        L.stk[k] = Bucket{s0, tot[r], nd, kd, B.block, obuf, B.gdepth, (nomove && !regather) ? 1u : 0u};
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
-            }
-            if (lane == 0)
-                L.sp = min(sp + nb, LOCAL_STACK);
-        }
+            local_classify(a, L, B);
         __syncthreads();
-        const bool     rg = j + 1 >= CARRY;  // continuing children start a new carry
-        const uint32_t dn = B.d + 1;
         if (L.nomove)
         {
             // nothing moves; the one child re-carries its digits in place when they run out
@@ -1739,8 +1830,6 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
             __syncthreads();
             continue;
         }
-        uint64_t* op = B.buf ? a.pay0 : a.pay1;
-        uint8_t*  od = B.buf ? a.dig0 : a.dig1;
         for (uint32_t e0 = 0; e0 < B.len; e0 += TILE)
         {
             const uint32_t cnt = min((uint32_t) TILE, B.len - e0);
@@ -1764,13 +1853,13 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
                 {
                     const uint64_t vv   = S.pay[q];
                     const uint32_t dd   = p_digit(vv, j);
-                    const bool     nx   = L.nxt[dd] != 0;
+                    const uint32_t nx   = L.nxt[dd];
                     const uint32_t slot = L.run[dd] + (q - S.base[dd]);
                     const uint64_t nv   = (rg && nx) ? p_make(pk, P.b, P.nbits, dn, vv) : vv;
                     if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "local scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
                     {
                         op[slot] = nv;
-                        if (nx)
+                        if (nx == 2)
                             od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));
                     }
                 }
@@ -3708,6 +3797,8 @@ struct BwtWorkspace
     uint32_t  local_grid = 768;       // workgroups of k_msd_local: 3 per CU (LDS)
     uint64_t  audit_cap  = 0;
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
+    // the root size limit the LDS stack of k_msd_local covers with this workspace's job sizes
+    uint32_t  local_limit() const { return std::min<uint32_t>(local_max, LOCAL_STACK * (mjob_max() + 1)); }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
@@ -4040,7 +4131,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                        w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
                        w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
                        (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout, w.pkd, nullptr, nullptr,
-                       w.roots, w.cap_roots, MODE == MODE_STRING ? w.local_max : 0u};
+                       w.roots, w.cap_roots, MODE == MODE_STRING ? w.local_limit() : 0u};
             {
                 BRA_PROF(P_BWT_SCAN, s);
                 hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
@@ -4298,7 +4389,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     ScanArgs a0{d_blocks, w.l0b,     nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1, w.pkd,
-                w.l0tot,          w.l0base,    w.roots,     w.cap_roots, w.local_max};
+                w.l0tot,          w.l0base,    w.roots,     w.cap_roots, w.local_limit()};
     {
         BRA_PROF(P_BWT_SCAN, s);
         hipLaunchKernelGGL(k_l0_colscan, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(256 * L0CS_GROUPS), 0, s, w.l0b, nblocks, w.tile_hist,
