@@ -1507,9 +1507,13 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
 // passes between workgroups (a child's elements were written by the workgroup that reads them),
 // so nothing needs a device-wide fence; the roots are claimed with one atomic each.
 // -------------------------------------------------------------------------------------------------
-constexpr uint32_t LOCAL_MAX   = 65536;  // default root size limit (BRA_LOCAL_MAX overrides; 0 = off)
-constexpr uint32_t LOCAL_STACK = 128;    // pending children: disjoint, each > mjob_max >= 256 elements
+constexpr uint32_t LOCAL_MAX     = 48 * 1024;  // default root size limit (BRA_LOCAL_MAX overrides; 0 = off)
+constexpr uint32_t LOCAL_STACK   = 48;         // pending children: disjoint, each > mjob_max elements
 constexpr uint32_t LOCAL_MAX_CAP = LOCAL_STACK * (256 * MJ_WAVES_DEF + 1);  // the largest root the stack bound covers (see local_limit)
+constexpr uint32_t LOCAL_ROOTS   = 4;          // roots claimed per atomic
+constexpr uint32_t LOCAL_JCHUNK  = 64;         // wave-job slots reserved per atomic (unused ones become empty jobs)
+constexpr uint32_t LOCAL_MCHUNK  = 16;         // workgroup-job slots reserved per atomic
+using TileStageLoc = TileStagePN<2>;           // 2 counter copies: 4 workgroups per CU fit the LDS
 
 struct LocalArgs
 {
@@ -1535,26 +1539,27 @@ struct LocalArgs
 struct LocalLds
 {
     Bucket   stk[LOCAL_STACK];
+    Bucket   rt[LOCAL_ROOTS];  // claimed roots not started yet
     Bucket   cur;
-    uint32_t sp;
+    uint32_t sp, nrt, nroots;
+    uint32_t jcur, jend, mcur, mend;  // reserved job / workgroup-job slots not used yet
     uint32_t run[256];  // next free slot of each sub-bucket (absolute)
-    uint32_t tot[256];
     uint8_t  nxt[256];  // 1: the sub-bucket continues (regathered payloads); 2: and it is split in passes (it needs its digit bytes)
-    uint32_t Ew[256], Sw[256];  // wave_job_pack scratch
-    uint8_t  nxs[256];
     uint32_t nomove;    // 1: one sub-bucket holds the whole bucket (nothing moves)
 };
 
-// Wave 0 of k_msd_local: the bucket's sub-buckets from L.tot (the rules of k_scan): cursors and
-// continue flags into L, wave jobs / workgroup jobs / fallback groups into the call's lists,
-// continuing children onto the stack.
-__device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, const Bucket& B)
+// Wave 0 of k_msd_local: the bucket's sub-buckets from tot_s (the rules of k_scan): cursors and
+// continue flags into L, wave jobs / workgroup jobs / fallback groups into the call's lists (job
+// slots from the workgroup's reserved chunks), continuing children onto the stack.  Ew / Sw / nxs:
+// wave_job_pack scratch (inside the staging area, unused at this point).
+__device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, const Bucket& B, const uint32_t* tot_s, uint32_t* Ew, uint32_t* Sw,
+                                               uint8_t* nxs)
 {
     const int lane = lane_id();
     uint32_t  tot[4], base[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-        tot[r] = L.tot[lane * 4 + r];
+        tot[r] = tot_s[lane * 4 + r];
     wave_excl_sum4(tot, base);
     const bool     nomove   = __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
     const bool     regather = B.d + 1 - B.kd >= CARRY;
@@ -1578,7 +1583,7 @@ __device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, 
         L.nxt[lane * 4 + r] = nbn[r] ? (tot[r] > (uint32_t) TILE ? 2 : 1) : 0;
     }
     WaveJobs wj;
-    wave_job_pack(tot, base, B.len, L.Ew, L.Sw, L.nxs, wj);
+    wave_job_pack(tot, base, B.len, Ew, Sw, nxs, wj);
     wave_excl_sum4(cm, mex, &nm);
     wave_excl_sum4(cg, gex, &ng);
     wave_excl_sum4(cb, bex, &nb);
@@ -1587,12 +1592,32 @@ __device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, 
     uint32_t pj = 0, pm = 0, pg = 0;
     if (lane == 0)
     {
-        if (wj.jtot || nm)
+        // job slots come from the workgroup's chunks; one atomic reserves both kinds when either runs out
+        const bool needj = L.jcur + wj.jtot > L.jend, needm = L.mcur + nm > L.mend;
+        if (needj || needm)
         {
-            const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) nm << 32) | wj.jtot);
-            pj = (uint32_t) old;
-            pm = (uint32_t) (old >> 32);
+            const uint32_t cj = needj ? max(LOCAL_JCHUNK, wj.jtot) : 0u, cmk = needm ? max(LOCAL_MCHUNK, nm) : 0u;
+            const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) cmk << 32) | cj);
+            if (needj)
+            {
+                // the rest of the old chunk becomes empty jobs
+                for (uint32_t k = L.jcur; k < L.jend && k < a.cap_jobs; ++k)
+                    a.jobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
+                L.jcur = (uint32_t) old;
+                L.jend = (uint32_t) old + cj;
+            }
+            if (needm)
+            {
+                for (uint32_t k = L.mcur; k < L.mend && k < a.cap_mjobs; ++k)
+                    a.mjobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
+                L.mcur = (uint32_t) (old >> 32);
+                L.mend = (uint32_t) (old >> 32) + cmk;
+            }
         }
+        pj = L.jcur;
+        pm = L.mcur;
+        L.jcur += wj.jtot;
+        L.mcur += nm;
         if (ng)
         {
             pg = atomicAdd(&a.ctr->n_groups, ng);
@@ -1654,15 +1679,24 @@ __device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, 
         L.sp = min(sp + nb, LOCAL_STACK);
 }
 
-__global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
+__global__ void __launch_bounds__(TPB, 4) k_msd_local(LocalArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStageS& S  = *reinterpret_cast<TileStageS*>(smem);
-    LocalLds&   L  = *reinterpret_cast<LocalLds*>(smem + sizeof(TileStageS));
-    const int   wv = threadIdx.x >> 6;
-    const uint32_t cp = (uint32_t) (lane_id() & (SCATTER_NC - 1)) * CSTRIDE;
+    TileStageLoc& S     = *reinterpret_cast<TileStageLoc*>(smem);
+    LocalLds&     L     = *reinterpret_cast<LocalLds*>(smem + sizeof(TileStageLoc));
+    uint32_t*     tot_s = S.goff;  // (the local scatter keeps its cursors in L.run)
+    uint32_t*     Ew    = reinterpret_cast<uint32_t*>(S.pay);  // classification scratch: the staging area is free then
+    uint32_t*     Sw    = Ew + 256;
+    uint8_t*      nxs   = reinterpret_cast<uint8_t*>(Sw + 256);
+    constexpr int NC    = 2;
+    const int     wv    = threadIdx.x >> 6;
+    const uint32_t cp   = (uint32_t) (lane_id() & (NC - 1)) * CSTRIDE;
     if (threadIdx.x == 0)
-        L.sp = 0;
+    {
+        L.sp = L.nrt = 0;
+        L.jcur = L.jend = L.mcur = L.mend = 0;
+        L.nroots = dev_count(&a.ctr->n_local);
+    }
     __syncthreads();
     for (;;)
     {
@@ -1673,10 +1707,15 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
                 b = L.stk[--L.sp];
             else
             {
-                const uint32_t n = dev_count(&a.ctr->n_local);
-                const uint32_t r = atomicAdd(&a.ctr->n_local_claim, 1u);
-                if (r < n)
-                    b = a.roots[r];
+                if (L.nrt == 0)
+                {
+                    const uint32_t r = atomicAdd(&a.ctr->n_local_claim, LOCAL_ROOTS);
+                    const uint32_t e = min(r + LOCAL_ROOTS, L.nroots);
+                    for (uint32_t k = e; k-- > r;)  // popped from the back: in list order
+                        L.rt[L.nrt++] = a.roots[k];
+                }
+                if (L.nrt > 0)
+                    b = L.rt[--L.nrt];
             }
             L.cur = b;
         }
@@ -1715,19 +1754,19 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
                     rank[i] = atomicAdd(&S.cnt[cp + dg[i]], 1u);
             __syncthreads();
             {
-                uint32_t c[SCATTER_NC], tot = 0;
+                uint32_t c[NC], tot = 0;
 #pragma unroll
-                for (int k = 0; k < SCATTER_NC; ++k)
+                for (int k = 0; k < NC; ++k)
                 {
                     c[k] = S.cnt[k * CSTRIDE + threadIdx.x];
                     tot += c[k];
                 }
                 const uint32_t b = block256_exclusive_sum(tot, S.tmp);
                 S.base[threadIdx.x] = b;
-                L.tot[threadIdx.x]  = tot;
+                tot_s[threadIdx.x]  = tot;
                 uint32_t run        = b;
 #pragma unroll
-                for (int k = 0; k < SCATTER_NC; ++k)
+                for (int k = 0; k < NC; ++k)
                 {
                     S.cnt[k * CSTRIDE + threadIdx.x] = run;
                     run += c[k];
@@ -1735,7 +1774,7 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
             }
             __syncthreads();
             if (wv == 0)
-                local_classify(a, L, B);
+                local_classify(a, L, B, tot_s, Ew, Sw, nxs);
             __syncthreads();
             if (L.nomove)
             {
@@ -1809,13 +1848,13 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
         {
             uint32_t t = 0;
 #pragma unroll
-            for (int c = 0; c < SCATTER_NC; ++c)
+            for (int c = 0; c < NC; ++c)
                 t += S.cnt[c * CSTRIDE + threadIdx.x];
-            L.tot[threadIdx.x] = t;
+            tot_s[threadIdx.x] = t;
         }
         __syncthreads();
         if (wv == 0)
-            local_classify(a, L, B);
+            local_classify(a, L, B, tot_s, Ew, Sw, nxs);
         __syncthreads();
         if (L.nomove)
         {
@@ -1871,6 +1910,16 @@ __global__ void __launch_bounds__(TPB, 3) k_msd_local(LocalArgs a)
             }
             __syncthreads();
         }
+    }
+    // the rest of the reserved job chunks: empty jobs (the job kernels skip them)
+    if (threadIdx.x == 0)
+    {
+        for (uint32_t k = L.jcur; k < L.jend && k < a.cap_jobs; ++k)
+            a.jobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t k = L.mcur; k < L.mend && k < a.cap_mjobs; ++k)
+            a.mjobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
+        if (L.jend > a.cap_jobs || L.mend > a.cap_mjobs)
+            atomicExch(&a.ctr->overflow, 1u);
     }
 }
 
@@ -3794,7 +3843,7 @@ struct BwtWorkspace
     Bucket*   roots      = nullptr;   // k_msd_local roots (continuing buckets of <= local_max elements)
     uint32_t  cap_roots  = 0;
     uint32_t  local_max  = LOCAL_MAX; // BRA_LOCAL_MAX (0: the level machinery splits every bucket, as before round 5)
-    uint32_t  local_grid = 768;       // workgroups of k_msd_local: 3 per CU (LDS)
+    uint32_t  local_grid = 1024;      // workgroups of k_msd_local: 4 per CU (LDS)
     uint64_t  audit_cap  = 0;
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
     // the root size limit the LDS stack of k_msd_local covers with this workspace's job sizes
@@ -4423,7 +4472,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         BRA_PROF(P_BWT_LOCAL, s);
         const LocalArgs la{w.roots, w.ctr, w.key[0], w.key[1], w.dig[0], w.dig[1], w.packed, w.pkd, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs,
                            w.groups[0], w.cap_groups, DCAP_BIG, w.mjob_max(), (uint32_t) (g_prof != nullptr)};
-        hipLaunchKernelGGL(k_msd_local, dim3(round8(w.local_grid)), dim3(TPB), sizeof(TileStageS) + sizeof(LocalLds), s, la);
+        hipLaunchKernelGGL(k_msd_local, dim3(round8(w.local_grid)), dim3(TPB), sizeof(TileStageLoc) + sizeof(LocalLds), s, la);
         BRA_DSYNC(s);
         BRA_HIP_CHECK(hipGetLastError());
     }
