@@ -527,7 +527,7 @@ class BlockCodec:
         return out
 
     SLOTS = ("stage.bwt", "stage.mtf", "stage.rle", "stage.huffman",
-             "bwt.l0_hist", "bwt.l0_scatter", "bwt.pack", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.mjobs", "bwt.fallback", "bwt.local",
+             "bwt.l0_hist", "bwt.l0_scatter", "bwt.pack", "bwt.hist", "bwt.scan", "bwt.scatter", "bwt.jobs", "bwt.mjobs", "bwt.fallback",
              "mtf.lastocc", "mtf.scan", "mtf.encode",
              "rle.runs", "rle.link", "rle.sizes", "rle.offsets", "rle.write",
              "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",

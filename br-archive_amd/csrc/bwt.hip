@@ -114,10 +114,6 @@ struct Counters
     alignas(128) uint32_t n_moved;       // elements the level's scatter moves (byte accounting)
     alignas(128) uint32_t n_elems_next;
     alignas(128) uint32_t n_melems;      // elements in workgroup jobs (byte accounting)
-    alignas(128) uint32_t n_local;       // buckets handed to the subtree-local MSD (k_msd_local roots)
-    alignas(128) uint32_t n_local_claim; // roots claimed by k_msd_local workgroups
-    alignas(128) uint32_t n_local_moved; // elements the local MSD scattered (byte accounting)
-    uint32_t              n_local_buckets;  // buckets it split
 };
 
 // A STRING-mode MSD tile as the hist and scatter kernels need it (built with the tile order, so a
@@ -719,9 +715,6 @@ struct ScanArgs
     const PackDesc* pk;        // STRING: packed key strings per block
     const uint32_t* btot;      // level 0: per-bucket digit totals (k_l0_colscan) instead of the tile rows
     uint32_t*       bbase;     // level 0: per-bucket sub-bucket starts (| NEXT_FLAG), added to the tiles' running counts by the scatter
-    Bucket*         roots;     // STRING: continuing sub-buckets of <= local_max elements go here (k_msd_local), not to the next level
-    uint32_t        cap_roots;
-    uint32_t        local_max;  // 0: none (RANK mode)
 };
 
 // One wave per bucket (SCAN_WAVES buckets per workgroup), lane = 4 consecutive digits.  Sub-bucket offsets
@@ -733,97 +726,8 @@ constexpr int SCAN_WAVES = 4;  // buckets (waves) per scan workgroup: 16 and 8 m
 
 struct ScanWaveCounts
 {
-    uint32_t jobs, mjobs, big, tiles, groups, moved, melems, elems_next, gmembers, hmin, local;
+    uint32_t jobs, mjobs, big, tiles, groups, moved, melems, elems_next, gmembers, hmin;
 };
-
-// Wave jobs of one bucket (one wave, lane = 4 consecutive digits): greedy packing of consecutive
-// sub-buckets of <= JOB_MAX elements.  The non-empty sub-buckets form a list in digit order; a
-// wave-job sub-bucket weighs its size, a larger one JOB_MAX + 1 (it never shares a job).  A job
-// starting at entry i takes entries i .. next(i) - 1, next(i) = the first entry whose end weight
-// exceeds the start weight + JOB_MAX (binary search on the weight prefix); the jobs are the chain
-// from entry 0 (one lane follows it: one step per job).  Greedy packing fills wave jobs to ~175
-// elements on text instead of ~124 with fixed windows of JOB_MAX / 2: 29 % fewer jobs, 21 % fewer
-// network stages.  Ew / Sw / nxs: 256-entry LDS scratch of the wave.
-struct WaveJobs
-{
-    bool     jstart[4], single[4];  // a job starts at this sub-bucket; the job is this one sub-bucket
-    uint32_t jlen[4], jidx[4], jtot;  // its length, its index among the bucket's jobs, the jobs of the bucket
-};
-
-__device__ __forceinline__ void wave_job_pack(const uint32_t (&tot)[4], const uint32_t (&base)[4], uint32_t blen, uint32_t* Ew, uint32_t* Sw,
-                                              uint8_t* nxs, WaveJobs& J)
-{
-    const int lane = lane_id();
-    uint32_t  li[4], wt[4], wx[4], nlist;
-    {
-        uint32_t ne[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            ne[r] = tot[r] ? 1u : 0u;
-            wt[r] = tot[r] == 0 ? 0u : (tot[r] <= JOB_MAX ? tot[r] : JOB_MAX + 1u);
-        }
-        wave_excl_sum4(ne, li, &nlist);
-        wave_excl_sum4(wt, wx);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (tot[r])
-        {
-            Ew[li[r]]  = wx[r] + wt[r];  // end weight of each list entry
-            Sw[li[r]]  = base[r];        // first slot (bucket-relative) of each list entry
-            nxs[li[r]] = 0;
-        }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t nxt[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        nxt[r] = li[r] + 1;
-        if (tot[r] && tot[r] <= JOB_MAX)
-        {
-            const uint32_t lim = wx[r] + JOB_MAX;
-            uint32_t       lo = li[r] + 1, hi = nlist;  // first entry in [lo, hi) with Ew > lim
-            while (lo < hi)
-            {
-                const uint32_t m = (lo + hi) >> 1;
-                if (Ew[m] > lim)
-                    hi = m;
-                else
-                    lo = m + 1;
-            }
-            nxt[r] = lo;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        if (tot[r])
-            Ew[li[r]] = nxt[r];  // the end weights are no longer needed: next(i) replaces them
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0)
-        for (uint32_t c = 0; c < nlist; c = Ew[c])
-            nxs[c] = 1;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t js[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        J.jstart[r] = tot[r] && tot[r] <= JOB_MAX && nxs[li[r]];
-        J.single[r] = nxt[r] == li[r] + 1;
-        js[r]       = J.jstart[r] ? 1u : 0u;
-        J.jlen[r]   = J.jstart[r] ? (nxt[r] < nlist ? Sw[nxt[r]] : blen) - base[r] : 0u;
-    }
-    wave_excl_sum4(js, J.jidx, &J.jtot);
-}
 
 template <uint32_t MODE>
 __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
@@ -832,7 +736,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
     __shared__ uint32_t       jlen_s[SCAN_WAVES][256];
     __shared__ uint8_t        nx_s[SCAN_WAVES][256];
     __shared__ ScanWaveCounts cnt_s[SCAN_WAVES];
-    __shared__ uint32_t       base_s[SCAN_WAVES][6];  // jobs, mjobs, big, tiles, groups, local roots
+    __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
     const int                 lane = lane_id(), w = threadIdx.x >> 6;
     const uint32_t            nbuckets = a.lin ? dev_count(&a.lin->n_big) : a.nbuckets;
     const uint32_t            bstride  = gridDim.x * SCAN_WAVES;
@@ -930,24 +834,100 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
         if (active && lane == 0)
             a.nomove[bi] = nomove ? (nm_next ? 2 : 1) : 0;
-        bool big[4], med[4], fin[4], nbn[4], loc[4];
+        bool big[4], med[4], fin[4], nbn[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
             big[r] = tot[r] > a.mjob_max;
             med[r] = tot[r] > JOB_MAX && !big[r];
             fin[r] = big[r] && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
-            loc[r] = big[r] && !fin[r] && tot[r] <= a.local_max;  // the whole subtree in one workgroup (k_msd_local)
-            nbn[r] = big[r] && !fin[r] && !loc[r];
+            nbn[r] = big[r] && !fin[r];
         }
-        WaveJobs wj;
-        wave_job_pack(tot, base, B.len, key_s[w], jlen_s[w], nx_s[w], wj);
-        const bool(&jstart)[4] = wj.jstart;
-        const uint32_t(&jlen)[4] = wj.jlen;
-        const uint32_t(&jidx)[4] = wj.jidx;
-        const uint32_t jtot      = wj.jtot;
+        // ---- wave jobs: greedy packing of consecutive sub-buckets of <= JOB_MAX elements ----
+        // The non-empty sub-buckets form a list in digit order; a wave-job sub-bucket weighs its
+        // size, a larger one JOB_MAX + 1 (it never shares a job).  A job starting at entry i takes
+        // entries i .. next(i) - 1, next(i) = the first entry whose end weight exceeds the start
+        // weight + JOB_MAX (binary search on the weight prefix); the jobs are the chain from entry 0
+        // (one lane follows it: one step per job).  Greedy packing fills wave jobs to ~175 elements
+        // on text instead of ~124 with fixed windows of JOB_MAX / 2: 29 % fewer jobs, 21 % fewer
+        // network stages.
+        uint32_t* const Ew = key_s[w];   // end weight of each list entry
+        uint32_t* const Sw = jlen_s[w];  // first slot (bucket-relative) of each list entry
+        uint32_t        li[4], wt[4], wx[4], nlist;
+        {
+            uint32_t ne[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                ne[r] = tot[r] ? 1u : 0u;
+                wt[r] = tot[r] == 0 ? 0u : (tot[r] <= JOB_MAX ? tot[r] : JOB_MAX + 1u);
+            }
+            wave_excl_sum4(ne, li, &nlist);
+            wave_excl_sum4(wt, wx);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (tot[r])
+            {
+                Ew[li[r]] = wx[r] + wt[r];
+                Sw[li[r]] = base[r];
+                nx_s[w][li[r]] = 0;
+            }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t nxt[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            nxt[r] = li[r] + 1;
+            if (tot[r] && tot[r] <= JOB_MAX)
+            {
+                const uint32_t lim = wx[r] + JOB_MAX;
+                uint32_t       lo = li[r] + 1, hi = nlist;  // first entry in [lo, hi) with Ew > lim
+                while (lo < hi)
+                {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (Ew[m] > lim)
+                        hi = m;
+                    else
+                        lo = m + 1;
+                }
+                nxt[r] = lo;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (tot[r])
+                Ew[li[r]] = nxt[r];  // the end weights are no longer needed: next(i) replaces them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0)
+            for (uint32_t c = 0; c < nlist; c = Ew[c])
+                nx_s[w][c] = 1;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        bool     jstart[4];
+        uint32_t js[4], jex[4], jtot, jlen[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            jstart[r] = tot[r] && tot[r] <= JOB_MAX && nx_s[w][li[r]];
+            js[r]     = jstart[r] ? 1u : 0u;
+            jlen[r]   = jstart[r] ? (nxt[r] < nlist ? Sw[nxt[r]] : B.len) - base[r] : 0u;
+        }
+        wave_excl_sum4(js, jex, &jtot);
+        uint32_t jidx[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            jidx[r] = jex[r];
         // ---- workgroup jobs, next-level buckets, fallback groups ----
-        uint32_t cm[4], cb[4], ct[4], cg[4], cl[4], mex[4], bex[4], tex[4], gex[4], lex[4], ntl[4];
+        uint32_t cm[4], cb[4], ct[4], cg[4], mex[4], bex[4], tex[4], gex[4], ntl[4];
         uint32_t melems = 0, enext = 0, gmem = 0, gmin = 0xFFFFFFFFu;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -957,9 +937,8 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
             cb[r]  = nbn[r] ? 1u : 0u;
             ct[r]  = ntl[r];
             cg[r]  = fin[r] ? 1u : 0u;
-            cl[r]  = loc[r] ? 1u : 0u;
             melems += med[r] ? tot[r] : 0;
-            enext += (nbn[r] || loc[r]) ? tot[r] : 0;
+            enext += nbn[r] ? tot[r] : 0;
             gmem += fin[r] ? tot[r] : 0;
         }
         ScanWaveCounts C{};
@@ -967,10 +946,9 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         wave_excl_sum4(cb, bex, &C.big);
         wave_excl_sum4(ct, tex, &C.tiles);
         wave_excl_sum4(cg, gex, &C.groups);
-        wave_excl_sum4(cl, lex, &C.local);
         C.jobs = active ? jtot : 0;
         if (!active)
-            C.mjobs = C.big = C.tiles = C.groups = C.local = 0;
+            C.mjobs = C.big = C.tiles = C.groups = 0;
         if (a.account || C.groups)
         {
             for (int d = 32; d >= 1; d >>= 1)
@@ -991,7 +969,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         __syncthreads();
         if (threadIdx.x == 0)
         {
-            uint32_t pre[6] = {0, 0, 0, 0, 0, 0}, tj = 0, tm = 0, tb = 0, tt = 0, tg = 0, tl = 0;
+            uint32_t pre[5] = {0, 0, 0, 0, 0}, tj = 0, tm = 0, tb = 0, tt = 0, tg = 0;
             ScanWaveCounts T{};
             T.hmin = 0xFFFFFFFFu;
             for (int v = 0; v < SCAN_WAVES; ++v)
@@ -1002,8 +980,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                 base_s[v][2] = tb;
                 base_s[v][3] = tt;
                 base_s[v][4] = tg;
-                base_s[v][5] = tl;
-                tl += c.local;
                 tj += c.jobs;
                 tm += c.mjobs;
                 tb += c.big;
@@ -1029,8 +1005,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                 pre[2] = (uint32_t) old;
                 pre[3] = (uint32_t) (old >> 32);
             }
-            if (tl)
-                pre[5] = atomicAdd(&a.ctr->n_local, tl);
             if (tg)
             {
                 pre[4] = atomicAdd(&a.ctr->n_groups, tg);
@@ -1047,7 +1021,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                     atomicAdd(&a.lout->n_elems_next, T.elems_next);
             }
             for (int v = 0; v < SCAN_WAVES; ++v)
-                for (int q = 0; q < 6; ++q)
+                for (int q = 0; q < 5; ++q)
                     base_s[v][q] += pre[q];
         }
         __syncthreads();
@@ -1063,7 +1037,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                     if (slot < a.cap_jobs)
                         // STRING: the kd field of a job flags a single sub-bucket (its keys can start at
                         // the first unshared byte; jobs do not use kd otherwise)
-                        a.jobs[slot] = Job{s0, jlen[r], MODE == MODE_STRING ? (wj.single[r] ? 1u : 0u) : kd, obuf, B.block, B.gdepth, nd};
+                        a.jobs[slot] = Job{s0, jlen[r], MODE == MODE_STRING ? (nxt[r] == li[r] + 1 ? 1u : 0u) : kd, obuf, B.block, B.gdepth, nd};
                     else
                         atomicExch(&a.ctr->overflow, 1u);
                 }
@@ -1092,16 +1066,6 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
                                                                 (nomove && !regather) ? 1u : 0u, P.b};
                         }
                     }
-                    else
-                        atomicExch(&a.ctr->overflow, 1u);
-                }
-                if (MODE == MODE_STRING && loc[r])
-                {
-                    // a local root: the digits of depth nd are in dig[obuf] (the scatter writes them:
-                    // NEXT_FLAG) or, for a bucket that stays put, in the payloads (tile0 = 1)
-                    const uint32_t slot = base_s[w][5] + lex[r];
-                    if (slot < a.cap_roots)
-                        a.roots[slot] = Bucket{s0, tot[r], nd, kd, B.block, obuf, B.gdepth, (nomove && !regather) ? 1u : 0u};
                     else
                         atomicExch(&a.ctr->overflow, 1u);
                 }
@@ -1489,437 +1453,6 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
             }
         }
         __syncthreads();
-    }
-}
-
-// -------------------------------------------------------------------------------------------------
-// Subtree-local MSD (round 5).  A continuing sub-bucket of at most local_max elements is not split
-// by the level machinery (tile lists, per-level histogram / scan / scatter launches, host-paced
-// level loop); it becomes a root of k_msd_local, where ONE workgroup splits it and every
-// descendant that still needs splitting, depth first, until all of them are jobs or fallback
-// groups.  Per bucket: a histogram of its digits (the digit bytes the parent's scatter wrote, or
-// the payloads' carried digit), the scan and classification of its 256 sub-buckets by wave 0 (the
-// same rules as k_scan: wave jobs packed greedily, workgroup jobs, fallback groups at the depth
-// cap), and an LDS-staged scatter 4096 elements at a time with the sub-bucket cursors in LDS (the
-// order inside a sub-bucket is free: L and pi are tie-order independent).  Continuing children go
-// on a stack in LDS: they are disjoint and each holds more than mjob_max >= 256 elements, so a
-// root of <= local_max elements never has more than local_max / 257 of them pending.  No data
-// passes between workgroups (a child's elements were written by the workgroup that reads them),
-// so nothing needs a device-wide fence; the roots are claimed with one atomic each.
-// -------------------------------------------------------------------------------------------------
-constexpr uint32_t LOCAL_MAX     = 48 * 1024;  // default root size limit (BRA_LOCAL_MAX overrides; 0 = off)
-constexpr uint32_t LOCAL_STACK   = 48;         // pending children: disjoint, each > mjob_max elements
-constexpr uint32_t LOCAL_MAX_CAP = LOCAL_STACK * (256 * MJ_WAVES_DEF + 1);  // the largest root the stack bound covers (see local_limit)
-constexpr uint32_t LOCAL_ROOTS   = 4;          // roots claimed per atomic
-constexpr uint32_t LOCAL_JCHUNK  = 64;         // wave-job slots reserved per atomic (unused ones become empty jobs)
-constexpr uint32_t LOCAL_MCHUNK  = 16;         // workgroup-job slots reserved per atomic
-using TileStageLoc = TileStagePN<2>;           // 2 counter copies: 4 workgroups per CU fit the LDS
-
-struct LocalArgs
-{
-    const Bucket*   roots;
-    Counters*       ctr;  // slot 0: n_local (roots), n_local_claim, the job / group lists
-    uint64_t*       pay0;
-    uint64_t*       pay1;
-    uint8_t*        dig0;
-    uint8_t*        dig1;
-    const uint8_t*  packed;
-    const PackDesc* pk;
-    Job*            jobs;
-    uint32_t        cap_jobs;
-    Job*            mjobs;
-    uint32_t        cap_mjobs;
-    Group*          groups;
-    uint32_t        cap_groups;
-    uint32_t        dcap;
-    uint32_t        mjob_max;
-    uint32_t        account;
-};
-
-struct LocalLds
-{
-    Bucket   stk[LOCAL_STACK];
-    Bucket   rt[LOCAL_ROOTS];  // claimed roots not started yet
-    Bucket   cur;
-    uint32_t sp, nrt, nroots;
-    uint32_t jcur, jend, mcur, mend;  // reserved job / workgroup-job slots not used yet
-    uint32_t run[256];  // next free slot of each sub-bucket (absolute)
-    uint8_t  nxt[256];  // 1: the sub-bucket continues (regathered payloads); 2: and it is split in passes (it needs its digit bytes)
-    uint32_t nomove;    // 1: one sub-bucket holds the whole bucket (nothing moves)
-};
-
-// Wave 0 of k_msd_local: the bucket's sub-buckets from tot_s (the rules of k_scan): cursors and
-// continue flags into L, wave jobs / workgroup jobs / fallback groups into the call's lists (job
-// slots from the workgroup's reserved chunks), continuing children onto the stack.  Ew / Sw / nxs:
-// wave_job_pack scratch (inside the staging area, unused at this point).
-__device__ __forceinline__ void local_classify(const LocalArgs& a, LocalLds& L, const Bucket& B, const uint32_t* tot_s, uint32_t* Ew, uint32_t* Sw,
-                                               uint8_t* nxs)
-{
-    const int lane = lane_id();
-    uint32_t  tot[4], base[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-        tot[r] = tot_s[lane * 4 + r];
-    wave_excl_sum4(tot, base);
-    const bool     nomove   = __any(tot[0] == B.len || tot[1] == B.len || tot[2] == B.len || tot[3] == B.len);
-    const bool     regather = B.d + 1 - B.kd >= CARRY;
-    const uint32_t kd       = regather ? B.d + 1 : B.kd;
-    const uint32_t nd       = B.d + 1;
-    const uint32_t obuf     = nomove ? B.buf : 1u - B.buf;
-    bool           med[4], fin[4], nbn[4];
-    uint32_t       cm[4], cg[4], cb[4], mex[4], gex[4], bex[4], nm = 0, ng = 0, nb = 0, gmem = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        const bool big = tot[r] > a.mjob_max;
-        med[r]         = tot[r] > JOB_MAX && !big;
-        fin[r]         = big && nd >= a.dcap;
-        nbn[r]         = big && !fin[r];
-        cm[r]          = med[r] ? 1u : 0u;
-        cg[r]          = fin[r] ? 1u : 0u;
-        cb[r]          = nbn[r] ? 1u : 0u;
-        gmem += fin[r] ? tot[r] : 0u;
-        L.run[lane * 4 + r] = B.start + base[r];
-        L.nxt[lane * 4 + r] = nbn[r] ? (tot[r] > (uint32_t) TILE ? 2 : 1) : 0;
-    }
-    WaveJobs wj;
-    wave_job_pack(tot, base, B.len, Ew, Sw, nxs, wj);
-    wave_excl_sum4(cm, mex, &nm);
-    wave_excl_sum4(cg, gex, &ng);
-    wave_excl_sum4(cb, bex, &nb);
-    for (int d = 32; d >= 1; d >>= 1)
-        gmem += __shfl_xor(gmem, d, WAVE);
-    uint32_t pj = 0, pm = 0, pg = 0;
-    if (lane == 0)
-    {
-        // job slots come from the workgroup's chunks; one atomic reserves both kinds when either runs out
-        const bool needj = L.jcur + wj.jtot > L.jend, needm = L.mcur + nm > L.mend;
-        if (needj || needm)
-        {
-            const uint32_t cj = needj ? max(LOCAL_JCHUNK, wj.jtot) : 0u, cmk = needm ? max(LOCAL_MCHUNK, nm) : 0u;
-            const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(&a.ctr->n_jobs), ((unsigned long long) cmk << 32) | cj);
-            if (needj)
-            {
-                // the rest of the old chunk becomes empty jobs
-                for (uint32_t k = L.jcur; k < L.jend && k < a.cap_jobs; ++k)
-                    a.jobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
-                L.jcur = (uint32_t) old;
-                L.jend = (uint32_t) old + cj;
-            }
-            if (needm)
-            {
-                for (uint32_t k = L.mcur; k < L.mend && k < a.cap_mjobs; ++k)
-                    a.mjobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
-                L.mcur = (uint32_t) (old >> 32);
-                L.mend = (uint32_t) (old >> 32) + cmk;
-            }
-        }
-        pj = L.jcur;
-        pm = L.mcur;
-        L.jcur += wj.jtot;
-        L.mcur += nm;
-        if (ng)
-        {
-            pg = atomicAdd(&a.ctr->n_groups, ng);
-            atomicAdd(&a.ctr->g_members, gmem);
-            atomicMin(&a.ctr->hmin, nd);
-        }
-        if (a.account)
-        {
-            atomicAdd(&a.ctr->n_local_buckets, 1u);
-            if (!nomove)
-                atomicAdd(&a.ctr->n_local_moved, B.len);
-        }
-        L.nomove = nomove ? 1u : 0u;
-    }
-    pj = __builtin_amdgcn_readfirstlane(pj);
-    pm = __builtin_amdgcn_readfirstlane(pm);
-    pg = __builtin_amdgcn_readfirstlane(pg);
-    const uint32_t sp = L.sp;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        const uint32_t s0 = B.start + base[r];
-        if (wj.jstart[r])
-        {
-            const uint32_t slot = pj + wj.jidx[r];
-            if (slot < a.cap_jobs)
-                a.jobs[slot] = Job{s0, wj.jlen[r], wj.single[r] ? 1u : 0u, obuf, B.block, B.gdepth, nd};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (med[r])
-        {
-            const uint32_t slot = pm + mex[r];
-            if (slot < a.cap_mjobs)
-                a.mjobs[slot] = Job{s0, tot[r], kd, obuf, B.block, B.gdepth, nd};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (fin[r])
-        {
-            const uint32_t slot = pg + gex[r];
-            if (slot < a.cap_groups)
-                a.groups[slot] = Group{s0, tot[r], nd, B.block | (obuf << 31)};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-        if (nbn[r])
-        {
-            // a child split in passes that stays put and keeps its carried digits reads them from
-            // the payloads (tile0 = 1: dig[] holds this depth's digit)
-            const uint32_t k = sp + bex[r];
-            if (k < LOCAL_STACK)
-                L.stk[k] = Bucket{s0, tot[r], nd, kd, B.block, obuf, B.gdepth, (nomove && !regather) ? 1u : 0u};
-            else
-                atomicExch(&a.ctr->overflow, 1u);
-        }
-    }
-    if (lane == 0)
-        L.sp = min(sp + nb, LOCAL_STACK);
-}
-
-__global__ void __launch_bounds__(TPB, 4) k_msd_local(LocalArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    TileStageLoc& S     = *reinterpret_cast<TileStageLoc*>(smem);
-    LocalLds&     L     = *reinterpret_cast<LocalLds*>(smem + sizeof(TileStageLoc));
-    uint32_t*     tot_s = S.goff;  // (the local scatter keeps its cursors in L.run)
-    uint32_t*     Ew    = reinterpret_cast<uint32_t*>(S.pay);  // classification scratch: the staging area is free then
-    uint32_t*     Sw    = Ew + 256;
-    uint8_t*      nxs   = reinterpret_cast<uint8_t*>(Sw + 256);
-    constexpr int NC    = 2;
-    const int     wv    = threadIdx.x >> 6;
-    const uint32_t cp   = (uint32_t) (lane_id() & (NC - 1)) * CSTRIDE;
-    if (threadIdx.x == 0)
-    {
-        L.sp = L.nrt = 0;
-        L.jcur = L.jend = L.mcur = L.mend = 0;
-        L.nroots = dev_count(&a.ctr->n_local);
-    }
-    __syncthreads();
-    for (;;)
-    {
-        if (threadIdx.x == 0)
-        {
-            Bucket b{};
-            if (L.sp > 0)
-                b = L.stk[--L.sp];
-            else
-            {
-                if (L.nrt == 0)
-                {
-                    const uint32_t r = atomicAdd(&a.ctr->n_local_claim, LOCAL_ROOTS);
-                    const uint32_t e = min(r + LOCAL_ROOTS, L.nroots);
-                    for (uint32_t k = e; k-- > r;)  // popped from the back: in list order
-                        L.rt[L.nrt++] = a.roots[k];
-                }
-                if (L.nrt > 0)
-                    b = L.rt[--L.nrt];
-            }
-            L.cur = b;
-        }
-        __syncthreads();
-        const Bucket B = L.cur;
-        if (B.len == 0)
-            break;  // uniform: no root left and the stack is empty
-        const PackDesc P  = a.pk[B.block];
-        const uint8_t* pk = a.packed + P.poff;
-        const uint32_t j  = B.d - B.kd;  // this depth's digit in the payloads (always < CARRY)
-        const bool     rg = j + 1 >= CARRY;  // continuing children start a new carry
-        const uint32_t dn = B.d + 1;
-        uint64_t*      ip = (B.buf ? a.pay1 : a.pay0) + B.start;
-        uint8_t*       id = (B.buf ? a.dig1 : a.dig0) + B.start;
-        uint64_t*      op = B.buf ? a.pay0 : a.pay1;
-        uint8_t*       od = B.buf ? a.dig0 : a.dig1;
-        if (B.len <= (uint32_t) TILE)
-        {
-            // ---- one pass: the payloads are loaded once; their carried digit gives the counts,
-            // the classification and the staging order ----
-            const uint32_t cnt = B.len;
-            uint64_t       v[PER_THREAD];
-            uint32_t       dg[PER_THREAD], rank[PER_THREAD];
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-            {
-                const uint32_t e = threadIdx.x + i * TPB;
-                v[i]             = (e < cnt) ? ip[e] : 0ull;
-                dg[i]            = p_digit(v[i], j);
-            }
-            stage_zero(S);
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-                if (threadIdx.x + i * TPB < cnt)
-                    rank[i] = atomicAdd(&S.cnt[cp + dg[i]], 1u);
-            __syncthreads();
-            {
-                uint32_t c[NC], tot = 0;
-#pragma unroll
-                for (int k = 0; k < NC; ++k)
-                {
-                    c[k] = S.cnt[k * CSTRIDE + threadIdx.x];
-                    tot += c[k];
-                }
-                const uint32_t b = block256_exclusive_sum(tot, S.tmp);
-                S.base[threadIdx.x] = b;
-                tot_s[threadIdx.x]  = tot;
-                uint32_t run        = b;
-#pragma unroll
-                for (int k = 0; k < NC; ++k)
-                {
-                    S.cnt[k * CSTRIDE + threadIdx.x] = run;
-                    run += c[k];
-                }
-            }
-            __syncthreads();
-            if (wv == 0)
-                local_classify(a, L, B, tot_s, Ew, Sw, nxs);
-            __syncthreads();
-            if (L.nomove)
-            {
-                // nothing moves; the one child re-carries its digits in place when they run out
-                // (it is split in one pass too: no digit bytes)
-                if (rg)
-#pragma unroll
-                    for (int i = 0; i < PER_THREAD; ++i)
-                    {
-                        const uint32_t e = threadIdx.x + i * TPB;
-                        if (e < cnt)
-                            ip[e] = p_make(pk, P.b, P.nbits, dn, v[i]);
-                    }
-                __syncthreads();
-                continue;
-            }
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-                if (threadIdx.x + i * TPB < cnt)
-                    S.pay[S.cnt[cp + dg[i]] + rank[i]] = v[i];
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-            {
-                const uint32_t q = threadIdx.x + i * TPB;
-                if (q < cnt)
-                {
-                    const uint64_t vv   = S.pay[q];
-                    const uint32_t dd   = p_digit(vv, j);
-                    const uint32_t nx   = L.nxt[dd];
-                    const uint32_t slot = L.run[dd] + (q - S.base[dd]);
-                    const uint64_t nv   = (rg && nx) ? p_make(pk, P.b, P.nbits, dn, vv) : vv;
-                    if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "local scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
-                    {
-                        op[slot] = nv;
-                        if (nx == 2)
-                            od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));
-                    }
-                }
-            }
-            __syncthreads();
-            continue;
-        }
-        // ---- larger buckets: a histogram pass over the digit bytes (or the payloads' digit),
-        // then the scatter 4096 elements at a time ----
-        const bool pdig = B.tile0 != 0;  // the digits are in the payloads, not in dig[]
-        stage_zero(S);
-        __syncthreads();
-        for (uint32_t e = threadIdx.x * PER_THREAD; e < B.len; e += TILE)
-        {
-            if (pdig)
-            {
-#pragma unroll 4
-                for (int i = 0; i < PER_THREAD; ++i)
-                    if (e + i < B.len)
-                        atomicAdd(&S.cnt[cp + p_digit(ip[e + i], j)], 1u);
-            }
-            else if (e + PER_THREAD <= B.len)
-            {
-                const uint4    q     = *reinterpret_cast<const uint4_u*>(id + e);
-                const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int i = 0; i < PER_THREAD; ++i)
-                    atomicAdd(&S.cnt[cp + ((w4[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
-            }
-            else
-                for (uint32_t i = e; i < B.len; ++i)
-                    atomicAdd(&S.cnt[cp + id[i]], 1u);
-        }
-        __syncthreads();
-        {
-            uint32_t t = 0;
-#pragma unroll
-            for (int c = 0; c < NC; ++c)
-                t += S.cnt[c * CSTRIDE + threadIdx.x];
-            tot_s[threadIdx.x] = t;
-        }
-        __syncthreads();
-        if (wv == 0)
-            local_classify(a, L, B, tot_s, Ew, Sw, nxs);
-        __syncthreads();
-        if (L.nomove)
-        {
-            // nothing moves; the one child re-carries its digits in place when they run out
-            if (rg)
-                for (uint32_t e = threadIdx.x; e < B.len; e += TPB)
-                {
-                    const uint64_t np = p_make(pk, P.b, P.nbits, dn, ip[e]);
-                    ip[e]             = np;
-                    id[e]             = (uint8_t) p_digit(np, 0);
-                }
-            __syncthreads();
-            continue;
-        }
-        for (uint32_t e0 = 0; e0 < B.len; e0 += TILE)
-        {
-            const uint32_t cnt = min((uint32_t) TILE, B.len - e0);
-            stage_zero(S);
-            __syncthreads();
-            uint64_t v[PER_THREAD];
-            uint32_t dg[PER_THREAD];
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-            {
-                const uint32_t e = threadIdx.x + i * TPB;
-                v[i]             = (e < cnt) ? ip[e0 + e] : 0ull;
-                dg[i]            = p_digit(v[i], j);
-            }
-            stage_p(S, v, dg, cnt);
-#pragma unroll
-            for (int i = 0; i < PER_THREAD; ++i)
-            {
-                const uint32_t q = threadIdx.x + i * TPB;
-                if (q < cnt)
-                {
-                    const uint64_t vv   = S.pay[q];
-                    const uint32_t dd   = p_digit(vv, j);
-                    const uint32_t nx   = L.nxt[dd];
-                    const uint32_t slot = L.run[dd] + (q - S.base[dd]);
-                    const uint64_t nv   = (rg && nx) ? p_make(pk, P.b, P.nbits, dn, vv) : vv;
-                    if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "local scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
-                    {
-                        op[slot] = nv;
-                        if (nx == 2)
-                            od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));
-                    }
-                }
-            }
-            __syncthreads();
-            {
-                const uint32_t d = threadIdx.x;
-                L.run[d] += (d < 255 ? S.base[d + 1] : cnt) - S.base[d];
-            }
-            __syncthreads();
-        }
-    }
-    // the rest of the reserved job chunks: empty jobs (the job kernels skip them)
-    if (threadIdx.x == 0)
-    {
-        for (uint32_t k = L.jcur; k < L.jend && k < a.cap_jobs; ++k)
-            a.jobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t k = L.mcur; k < L.mend && k < a.cap_mjobs; ++k)
-            a.mjobs[k] = Job{0, 0, 0, 0, 0, 0, 0};
-        if (L.jend > a.cap_jobs || L.mend > a.cap_mjobs)
-            atomicExch(&a.ctr->overflow, 1u);
     }
 }
 
@@ -3840,14 +3373,8 @@ struct BwtWorkspace
     JobPhase  last_ph{};                // job launches and batch size of the last STRING encode (diagnostics)
     uint64_t  last_n     = 0;         // 0: no job phase to re-run (none yet, a fallback rewrote the lists, or another call ran since)
     uint32_t* audit_cnt  = nullptr;   // slot-cover counts of the job audit (allocated on first use)
-    Bucket*   roots      = nullptr;   // k_msd_local roots (continuing buckets of <= local_max elements)
-    uint32_t  cap_roots  = 0;
-    uint32_t  local_max  = LOCAL_MAX; // BRA_LOCAL_MAX (0: the level machinery splits every bucket, as before round 5)
-    uint32_t  local_grid = 1024;      // workgroups of k_msd_local: 4 per CU (LDS)
     uint64_t  audit_cap  = 0;
     uint32_t  mj_classes() const { return mj_waves >= 4 ? 2u : 1u; }
-    // the root size limit the LDS stack of k_msd_local covers with this workspace's job sizes
-    uint32_t  local_limit() const { return std::min<uint32_t>(local_max, LOCAL_STACK * (mjob_max() + 1)); }
     uint32_t  mjob_max() const { return mj_waves ? 256u * (uint32_t) mj_waves : JOB_MAX; }
 };
 
@@ -3971,15 +3498,6 @@ static void launch_mjobs(int waves, uint32_t n, const JobArgs& a, hipStream_t s)
 #endif
 }
 
-static uint32_t local_max_setting()
-{
-    static const uint32_t v = [] {
-        const char* e = getenv("BRA_LOCAL_MAX");  // measurement knob: 0 = no subtree-local MSD
-        return e ? std::min<uint32_t>((uint32_t) strtoul(e, nullptr, 0), LOCAL_MAX_CAP) : LOCAL_MAX;
-    }();
-    return v;
-}
-
 static void ws_free(BwtWorkspace& w)
 {
     for (int i = 0; i < 2; ++i)
@@ -3994,7 +3512,7 @@ static void ws_free(BwtWorkspace& w)
     }
     void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
                    w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask, w.l0tot, w.l0base,
-                   w.audit_cnt, w.roots};
+                   w.audit_cnt};
     for (void* p : dev)
         (void) hipFree(p);
     if (w.h_ctr)
@@ -4008,15 +3526,9 @@ static void ws_free(BwtWorkspace& w)
     const uint32_t seq = w.mail_seq;
     w                  = BwtWorkspace{};
     w.mail_seq         = seq;
-    w.local_max        = local_max_setting();
 }
 
-BwtWorkspace* bwt_workspace_create()
-{
-    BwtWorkspace* w = new BwtWorkspace();
-    w->local_max    = local_max_setting();
-    return w;
-}
+BwtWorkspace* bwt_workspace_create() { return new BwtWorkspace(); }
 const uint32_t* bwt_alpha_masks(const BwtWorkspace* w) { return w ? w->amask : nullptr; }
 const uint32_t* bwt_sa(const BwtWorkspace* w) { return w ? w->fsa : nullptr; }
 void            bwt_forget_jobs(BwtWorkspace* w)
@@ -4051,7 +3563,6 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
     w.cap_jobs   = (uint32_t) (N / 2 + B + 1024);
     w.cap_groups = (uint32_t) (N / 2 + B + 64);
     w.cap_mjobs  = (uint32_t) (N / JOB_MAX + B + 64);
-    w.cap_roots  = (uint32_t) (N / (JOB_MAX + 1) + B + 64);  // disjoint, each > mjob_max >= JOB_MAX elements
     const uint32_t cap_sorted = (uint32_t) (N / 8 + B + 1024);
     bool ok = true;
     for (int i = 0; i < 2 && ok; ++i)
@@ -4066,8 +3577,7 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
          dev_alloc(w.tile_cnt, 2 * nkeys + 16) && dev_alloc(w.tile_order, w.cap_tiles) && dev_alloc(w.ctr, MAX_LEVELS) &&
          dev_alloc(w.jobq, (1 + MJ_CLASSES) * 8 * 32) && dev_alloc(w.l0tiles, w.cap_l0) && dev_alloc(w.l0b, B) &&
          dev_alloc(w.packed, N + (uint64_t) PACK_PAD * B + 128) && dev_alloc(w.pkd, B) && dev_alloc(w.amask, 8ull * B) &&
-         dev_alloc(w.tmask, 8ull * w.cap_l0) && dev_alloc(w.l0tot, 256ull * B) && dev_alloc(w.l0base, 256ull * B) &&
-         dev_alloc(w.roots, w.cap_roots);
+         dev_alloc(w.tmask, 8ull * w.cap_l0) && dev_alloc(w.l0tot, 256ull * B) && dev_alloc(w.l0base, 256ull * B);
     if (ok && hipHostMalloc(&w.h_ctr, MAX_LEVELS * sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         w.h_ctr = nullptr, ok = false;
     if (ok && hipHostMalloc(&w.h_mail, MAX_LEVELS * sizeof(Mail), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
@@ -4180,7 +3690,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                        w.cap_big,   w.tile_bucket[cur ^ 1],   w.tdesc[cur ^ 1], w.cap_tiles, w.jobs,       w.cap_jobs,
                        w.mjobs,     w.cap_mjobs, groups_out,  w.cap_groups, w.ctr, MODE == MODE_STRING ? DCAP_BIG : RANK_KEYBYTES,
                        (uint32_t) (g_prof != nullptr), w.mjob_max(), lin, lout, w.pkd, nullptr, nullptr,
-                       w.roots, w.cap_roots, MODE == MODE_STRING ? w.local_limit() : 0u};
+};
             {
                 BRA_PROF(P_BWT_SCAN, s);
                 hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
@@ -4219,16 +3729,11 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
 template <uint32_t MODE>
 static bool account_levels(BwtWorkspace& w, hipStream_t s)
 {
-    if (!g_prof || !(g_prof->mask >> P_BWT_HIST & 1 || g_prof->mask >> P_BWT_SCAN & 1 || g_prof->mask >> P_BWT_SCATTER & 1 ||
-                     g_prof->mask >> P_BWT_LOCAL & 1))
+    if (!g_prof || !(g_prof->mask >> P_BWT_HIST & 1 || g_prof->mask >> P_BWT_SCAN & 1 || g_prof->mask >> P_BWT_SCATTER & 1))
         return true;
     const uint32_t ns = std::min<uint32_t>(w.levels + 2, MAX_LEVELS);
     BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, ns * sizeof(Counters), hipMemcpyDeviceToHost, s));
     BRA_HIP_CHECK(hipStreamSynchronize(s));
-    if (MODE == MODE_STRING)
-        // local MSD: per moved element a digit byte read, the payload read and written, the next
-        // digit byte written
-        prof_bytes(P_BWT_LOCAL, 18.0 * w.h_ctr[0].n_local_moved);
     // STRING: 8-byte payloads moved (+ the next digit gathered for elements that stay in big buckets)
     const double eb = 8.0, mb = (MODE == MODE_STRING) ? 16.0 + 8.0 / CARRY : 24.0;
     for (uint32_t k = 1; k + 1 < ns; ++k)
@@ -4438,7 +3943,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     ScanArgs a0{d_blocks, w.l0b,     nblocks,         w.tile_hist, w.tile_off, w.nomove,   w.big[0],    w.cap_big,
                 w.tile_bucket[0], w.tdesc[0], w.cap_tiles, w.jobs,     w.cap_jobs, w.mjobs,    w.cap_mjobs, w.groups[0],
                 w.cap_groups,     w.ctr,       DCAP_BIG,   (uint32_t) (g_prof != nullptr), w.mjob_max(), nullptr, w.ctr + 1, w.pkd,
-                w.l0tot,          w.l0base,    w.roots,     w.cap_roots, w.local_limit()};
+                w.l0tot,          w.l0base};
     {
         BRA_PROF(P_BWT_SCAN, s);
         hipLaunchKernelGGL(k_l0_colscan, dim3(std::min<uint32_t>(nblocks, 65535u)), dim3(256 * L0CS_GROUPS), 0, s, w.l0b, nblocks, w.tile_hist,
@@ -4466,16 +3971,6 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     ph.nblocks = nblocks;
     if (!run_levels<MODE_STRING>(w, d_in, d_blocks, 0, w.groups[0], s, post(w, 1, s)))
         return false;
-    if (w.local_max)
-    {
-        // every continuing bucket of <= local_max elements the levels handed over, split to the end
-        BRA_PROF(P_BWT_LOCAL, s);
-        const LocalArgs la{w.roots, w.ctr, w.key[0], w.key[1], w.dig[0], w.dig[1], w.packed, w.pkd, w.jobs, w.cap_jobs, w.mjobs, w.cap_mjobs,
-                           w.groups[0], w.cap_groups, DCAP_BIG, w.mjob_max(), (uint32_t) (g_prof != nullptr)};
-        hipLaunchKernelGGL(k_msd_local, dim3(round8(w.local_grid)), dim3(TPB), sizeof(TileStageLoc) + sizeof(LocalLds), s, la);
-        BRA_DSYNC(s);
-        BRA_HIP_CHECK(hipGetLastError());
-    }
     if (!run_jobs(w, ph, s))
         return false;
     // posted here, waited for in bwt_encode_finish after the caller has queued its later stages:
@@ -4499,8 +3994,8 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
         BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, ns * sizeof(Counters), hipMemcpyDeviceToHost, s));
         BRA_HIP_CHECK(hipStreamSynchronize(s));
         const Counters& c0 = w.h_ctr[0];
-        fprintf(stderr, "[bwt levels] N %llu jobs %u mjobs %u melems %u groups %u | local roots %u buckets %u moved %u\n", (unsigned long long) N,
-                c0.n_jobs, c0.n_mjobs, c0.n_melems, c0.n_groups, c0.n_local, c0.n_local_buckets, c0.n_local_moved);
+        fprintf(stderr, "[bwt levels] N %llu jobs %u mjobs %u melems %u groups %u\n", (unsigned long long) N, c0.n_jobs,
+                c0.n_mjobs, c0.n_melems, c0.n_groups);
         for (uint32_t k = 1; k < ns; ++k)
             fprintf(stderr, "[bwt levels] slot %u: buckets %u tiles %u elems %u moved(into) %u\n", k, w.h_ctr[k].n_big, w.h_ctr[k].n_tiles_next,
                     w.h_ctr[k].n_elems_next, w.h_ctr[k].n_moved);

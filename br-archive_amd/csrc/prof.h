@@ -13,7 +13,7 @@ namespace bra {
 enum ProfSlot : int
 {
     P_STAGE_BWT, P_STAGE_MTF, P_STAGE_RLE, P_STAGE_HUF,
-    P_BWT_L0HIST, P_BWT_L0SCATTER, P_BWT_PACK, P_BWT_HIST, P_BWT_SCAN, P_BWT_SCATTER, P_BWT_JOBS, P_BWT_MJOBS, P_BWT_FALLBACK, P_BWT_LOCAL,
+    P_BWT_L0HIST, P_BWT_L0SCATTER, P_BWT_PACK, P_BWT_HIST, P_BWT_SCAN, P_BWT_SCATTER, P_BWT_JOBS, P_BWT_MJOBS, P_BWT_FALLBACK,
     P_MTF_LASTOCC, P_MTF_SCAN, P_MTF_ENCODE,
     P_RLE_RUNS, P_RLE_LINK, P_RLE_SIZES, P_RLE_OFFSETS, P_RLE_WRITE,
     P_HUF_BUILD, P_HUF_OFFSETS, P_HUF_TILEBITS, P_HUF_TILESCAN, P_HUF_ZERO, P_HUF_PACK,
