@@ -19,7 +19,7 @@ def main():
 
     import bench
 
-    nbatch = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    nbatch = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     kind = sys.argv[2] if len(sys.argv) > 2 else "text"
     bs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
     bra = importlib.import_module("br-archive_amd")
@@ -36,7 +36,9 @@ def main():
         codec.encode(d, bs, hdr, off, pay, stream=ws)  # warm-up (allocations, geometry upload)
     torch.cuda.synchronize()
     payload_bytes = int(off[nb].item())
-    res = bench.pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, ws, nbatch)
+    codec2 = bra.BlockCodec(0)
+    res = bench.pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, ws, nbatch, codec2)
+    codec2.close()
     res["device_resident_reference"] = "bench.py value (same input, one 256 MiB batch)"
     print(json.dumps(res), flush=True)
     codec.close()
