@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--profile-all", action="store_true", help="time every kernel during the timed steps")
     ap.add_argument("--no-secondary", action="store_true", help="skip the decode and PCIe-inclusive measurements")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
-    ap.add_argument("--pcie-batches", type=int, default=2, help="batches of the overlapped transfer-inclusive encode")
+    ap.add_argument("--pcie-batches", type=int, default=4, help="batches of the split transfer-inclusive encode (two contexts)")
+    ap.add_argument("--pcie-stream", type=int, default=4, help="batches of the streamed transfer-inclusive encode (pipelined API)")
     return ap.parse_args()
 
 
@@ -223,7 +224,7 @@ def check_vs_reference(H, O, P, kind, bs, nbg, global_total, world, threads):
     return res
 
 
-def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work_stream, nbatch, codec2=None):
+def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work_stream, nbatch, codec2=None, split=None):
     """Transfer-inclusive encode (SURVEY 8.1(d) secondary): pinned host input -> HBM, encode, chunk
     headers + payload back to pinned host memory, timed from the first byte sent to the last byte
     received.  Serial: one copy in, one encode, the copies out, on one stream.  Overlapped: the
@@ -256,11 +257,22 @@ def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work
     if codec2 is None:
         return res
     # overlapped: batches of whole blocks
-    per = max(1, -(-nb // nbatch))
-    parts = [(b0, min(nb, b0 + per)) for b0 in range(0, nb, per)]
-    h2d = torch.cuda.Stream()
+    if split:  # batch sizes in blocks (the rest of the input, if any, is one more batch)
+        cuts = [0]
+        for c in split:
+            cuts.append(min(nb, cuts[-1] + c))
+        if cuts[-1] < nb:
+            cuts.append(nb)
+        parts = [(a, b) for a, b in zip(cuts, cuts[1:]) if b > a]
+    else:
+        per = max(1, -(-nb // nbatch))
+        parts = [(b0, min(nb, b0 + per)) for b0 in range(0, nb, per)]
+    # copy streams at high priority: HIP shares a few hardware queues among a process's streams of
+    # one priority, and a kernel queued behind a copy's barrier on a shared queue waits for that
+    # copy (batch k's encode then waited for batch k + 1's input; scripts/micro/ev_wait.py)
+    h2d = torch.cuda.Stream(priority=-1)
     streams = [work_stream, torch.cuda.Stream()]
-    d2hs = [torch.cuda.Stream(), torch.cuda.Stream()]
+    d2hs = [torch.cuda.Stream(priority=-1), torch.cuda.Stream(priority=-1)]
     codecs = [codec, codec2]
     offs = [torch.empty((b1 - b0 + 1,), dtype=torch.int64, device=d.device) for b0, b1 in parts]
     # payload room per batch: a block's payload never exceeds its RLE bytes + 1 (an optimal prefix
@@ -326,6 +338,70 @@ def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work
     res["encode_pcie_inclusive_batches"] = len(parts)
     res["encode_pcie_inclusive_contexts"] = 2
     res["encode_pcie_inclusive_bytes_back"] = int(sum(hb) + hdr.numel())
+    return res
+
+
+def pcie_stream(bra, codec, data_np, kind, bs, nstream):
+    """Transfer-inclusive encode of a stream of host batches (SURVEY 8.1(d) secondary; the front
+    end's loop): `nstream` batches of the configs[1] size go host -> HBM -> chunk records -> host
+    through the library's pipelined API (bra_gpu_compress_chunks_stage / _submit / _collect, one
+    context): batch k + 1's input copy is queued before batch k is submitted and batch k - 1's records
+    come back while batch k's later stages run.  Timed from the first copy queued to the last record
+    byte received; the input sits in pinned host memory (two distinct synthetic batches alternate).
+    A batch's records are checked against the same batch's earlier records."""
+    import ctypes as C
+
+    lib = bra.lib
+    total = data_np.size
+    nb = -(-total // bs)
+    second = bra.synth_fill(KINDS[kind], total, bs, first_block=nb)
+    cap = lib.bra_gpu_chunks_bound(total, bs)
+    hin = [lib.bra_gpu_host_alloc(codec.ctx, total) for _ in range(2)]
+    hout = lib.bra_gpu_host_alloc(codec.ctx, cap)
+    res = {}
+    try:
+        if not all(hin) or not hout:
+            return res
+        C.memmove(hin[0], data_np.ctypes.data, total)
+        C.memmove(hin[1], second.ctypes.data, total)
+        seen = {}
+
+        def run(nbat):
+            back = 0
+
+            def collect(k):
+                nonlocal back
+                size, crc = C.c_uint64(), C.c_uint32()
+                rc = lib.bra_gpu_compress_chunks_collect(codec.ctx, k % 2, hout, cap, C.byref(size), C.byref(crc))
+                if rc < 0:
+                    raise RuntimeError(f"bra_gpu_compress_chunks_collect failed ({rc})")
+                back += size.value
+                key = (size.value, crc.value, C.string_at(hout, min(size.value, 1 << 16)))
+                if seen.setdefault(k % 2, key) != key:
+                    raise RuntimeError("pipelined encode: the same batch gave different records")
+
+            if lib.bra_gpu_compress_chunks_stage(codec.ctx, 0, hin[0], total) != 0:
+                raise RuntimeError("bra_gpu_compress_chunks_stage failed")
+            for k in range(nbat):
+                if k + 1 < nbat and lib.bra_gpu_compress_chunks_stage(codec.ctx, (k + 1) % 2, hin[(k + 1) % 2], total) != 0:
+                    raise RuntimeError("bra_gpu_compress_chunks_stage failed")
+                if lib.bra_gpu_compress_chunks_submit(codec.ctx, k % 2, hin[k % 2], total, bs) != 0:
+                    raise RuntimeError("bra_gpu_compress_chunks_submit failed")
+                if k:
+                    collect(k - 1)
+            collect(nbat - 1)
+            return back
+
+        run(2)  # untimed: the pipeline's buffers are allocated
+        t0 = time.perf_counter()
+        back = run(nstream)
+        dt = time.perf_counter() - t0
+        res["encode_pcie_stream_GBps"] = round(nstream * total / dt / 1e9, 4)
+        res["encode_pcie_stream"] = {"batches": nstream, "batch_bytes": int(total), "records_bytes_back": int(back), "contexts": 1}
+    finally:
+        for p in (*hin, hout):
+            if p:
+                lib.bra_gpu_host_free(codec.ctx, p)
     return res
 
 
@@ -529,6 +605,7 @@ def main():
             codec2 = bra.BlockCodec(local)
             secondary.update(pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work_stream, args.pcie_batches, codec2))
             codec2.close()
+            secondary.update(pcie_stream(bra, codec, data_np, args.kind, bs, args.pcie_stream))
 
         line = {
             "metric": METRIC,
@@ -594,6 +671,19 @@ def main():
                 if k:
                     line["roofline"]["traffic"] = k.get("hbm_bytes_per_launch")
                     line["roofline"]["traffic_source"] = f"profiles/pmc_summary.json workloads.{args.kind}_{bs} ({wl.get('source', '?')})"
+                # the compute side of the job kernels (sorting networks and string compares, not HBM
+                # bound): VALU issue fraction of the chip and VALU instructions per input byte of the
+                # launch (one launch covers the whole batch), from the SQ / GRBM passes
+                valu = {}
+                for slot in dict.fromkeys((dominant, "bwt.jobs", "bwt.mjobs")):
+                    e = wl.get("kernels", {}).get(slot, {})
+                    if "valu_frac" in e:
+                        valu[slot] = {"valu_frac": e["valu_frac"],
+                                      "valu_insts_per_element": round(e.get("valu_insts_per_launch", 0) * 64 / my_bytes, 2)}
+                if dominant in valu:
+                    line["roofline"].update(valu[dominant])
+                if valu:
+                    line["roofline"]["valu"] = valu
             except (OSError, ValueError, AttributeError):
                 pass
         if not args.no_check:

@@ -41,7 +41,7 @@ ABI_SYMBOLS = (
     "bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host",
     "bra_gpu_chunks_crc32c_shard", "bra_gpu_assemble_shards",
     "bra_gpu_debug_rerun_jobs", "bra_gpu_sortnet_selftest",
-    "bra_gpu_host_alloc", "bra_gpu_host_free", "bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect",
+    "bra_gpu_host_alloc", "bra_gpu_host_free", "bra_gpu_compress_chunks_stage", "bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect",
 )
 MAX_CHUNK_SIZE = 256 * 1024  # BRA_MAX_CHUNK_SIZE (src/lib_bra_defs.h:93): the .BRa chunk size
 
@@ -153,6 +153,8 @@ def _load() -> C.CDLL:
     lib.bra_gpu_host_alloc.restype = vp
     lib.bra_gpu_host_free.argtypes = [vp, vp]
     lib.bra_gpu_host_free.restype = None
+    lib.bra_gpu_compress_chunks_stage.argtypes = [vp, C.c_int, vp, C.c_uint64]
+    lib.bra_gpu_compress_chunks_stage.restype = C.c_int
     lib.bra_gpu_compress_chunks_submit.argtypes = [vp, C.c_int, vp, C.c_uint64, C.c_uint32]
     lib.bra_gpu_compress_chunks_submit.restype = C.c_int
     lib.bra_gpu_compress_chunks_collect.argtypes = [vp, C.c_int, vp, C.c_uint64, u64p, u32p]
@@ -411,11 +413,11 @@ class BlockCodec:
             raise RuntimeError(f"bra_gpu_compress_chunks failed ({rc})")
         return out[: size.value], crc.value, rc == 1
 
-    def compress_chunks_pipelined(self, data_np, batch_bytes: int, block_size: int = MAX_CHUNK_SIZE):
-        """Host-buffer compression in batches with two in flight (bra_gpu_compress_chunks_submit /
-        _collect, the front end's loop): [(records bytes, batch crc, compressed?)] per batch."""
-        import numpy as np
-
+    def compress_chunks_pipelined(self, data_np, batch_bytes: int, block_size: int = MAX_CHUNK_SIZE, stage_ahead: bool = True):
+        """Host-buffer compression in batches with two in flight (bra_gpu_compress_chunks_stage /
+        _submit / _collect, the front end's loop): [(records bytes, batch crc, compressed?)] per batch.
+        stage_ahead: batch k + 1's input copy is queued before batch k is submitted (else submit
+        makes each batch's copy itself)."""
         total = int(data_np.size)
         bb = max(block_size, batch_bytes // block_size * block_size)
         spans = [(o, min(total, o + bb)) for o in range(0, total, bb)]
@@ -426,21 +428,45 @@ class BlockCodec:
             raise RuntimeError("bra_gpu_host_alloc failed")
         res = []
         try:
-            def submit(k):
+            def fill(k):
                 lo, hi = spans[k]
                 C.memmove(hin[k % 2], data_np[lo:hi].ctypes.data, hi - lo)
+
+            def stage(k):
+                lo, hi = spans[k]
+                fill(k)
+                if lib.bra_gpu_compress_chunks_stage(self.ctx, k % 2, hin[k % 2], hi - lo) != 0:
+                    raise RuntimeError("bra_gpu_compress_chunks_stage failed")
+
+            def submit(k):
+                lo, hi = spans[k]
                 if lib.bra_gpu_compress_chunks_submit(self.ctx, k % 2, hin[k % 2], hi - lo, block_size) != 0:
                     raise RuntimeError("bra_gpu_compress_chunks_submit failed")
 
-            submit(0)
-            for k in range(len(spans)):
-                if k + 1 < len(spans):
-                    submit(k + 1)
+            def collect(k):
                 size, crc = C.c_uint64(), C.c_uint32()
                 rc = lib.bra_gpu_compress_chunks_collect(self.ctx, k % 2, hout, cap, C.byref(size), C.byref(crc))
                 if rc < 0:
                     raise RuntimeError(f"bra_gpu_compress_chunks_collect failed ({rc})")
                 res.append((C.string_at(hout, size.value), crc.value, rc == 1))
+
+            if stage_ahead:
+                stage(0)
+                for k in range(len(spans)):
+                    if k + 1 < len(spans):
+                        stage(k + 1)  # slot (k + 1) % 2: batch k - 1 there is submitted, its input consumed on the device first
+                    submit(k)
+                    if k:
+                        collect(k - 1)
+                collect(len(spans) - 1)
+            else:
+                fill(0)
+                submit(0)
+                for k in range(len(spans)):
+                    if k + 1 < len(spans):
+                        fill(k + 1)
+                        submit(k + 1)
+                    collect(k)
         finally:
             for p in (*hin, hout):
                 lib.bra_gpu_host_free(self.ctx, p)

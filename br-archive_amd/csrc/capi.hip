@@ -230,6 +230,10 @@ struct bra_gpu_ctx_s
         uint64_t   data_size = 0;
         uint32_t   nb = 0;
         int        state = 0;  // 0 free, 1 submitted
+        // an input copy queued ahead by bra_gpu_compress_chunks_stage (the slot's next batch)
+        bool           staged = false;
+        const uint8_t* st_ptr = nullptr;
+        uint64_t       st_size = 0;
     } pipe[2];
     hipStream_t    copy_in = nullptr, copy_out = nullptr;
     uint64_t*      h_pipe_mail = nullptr;  // pinned: per slot {payload bytes, chunk-stream CRC}
@@ -959,7 +963,58 @@ void bra_gpu_host_free(bra_gpu_ctx_t* c, void* p)
     if (!c || !p)
         return;
     DevGuard dg(c->device);
+    if (c->copy_in)  // a staged input copy may still read the buffer
+        (void) hipStreamSynchronize(c->copy_in);
     (void) hipHostFree(p);
+}
+
+// The pipeline's streams, pinned mailbox and the slot's events, created on first use.
+static bool pipe_init(bra_gpu_ctx_s* c, bra_gpu_ctx_s::PipeSlot& ps)
+{
+    // The copy streams get the highest priority: HIP maps a process's streams onto a few hardware
+    // queues per priority (GPU_MAX_HW_QUEUES), and a kernel queued behind a copy's completion barrier
+    // on a shared queue waits for that copy -- a normal-priority copy stream sharing a queue with the
+    // encode stream made batch k's kernels wait for batch k + 1's input (scripts/micro/ev_wait.py).
+    int least = 0, greatest = 0;
+    if (!c->copy_in && (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                        hipStreamCreateWithPriority(&c->copy_in, hipStreamNonBlocking, greatest) != hipSuccess ||
+                        hipStreamCreateWithPriority(&c->copy_out, hipStreamNonBlocking, greatest) != hipSuccess))
+        return false;
+    if (!c->h_pipe_mail && hipHostMalloc(&c->h_pipe_mail, 4 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
+    {
+        c->h_pipe_mail = nullptr;
+        return false;
+    }
+    return (ps.ev_in || hipEventCreateWithFlags(&ps.ev_in, hipEventDisableTiming) == hipSuccess) &&
+           (ps.ev_done || hipEventCreateWithFlags(&ps.ev_done, hipEventDisableTiming) == hipSuccess);
+}
+
+// The slot's input copy on the copy stream, after the device has finished the slot's previous batch
+// (its BWT and CRC read d_in; ev_done is recorded after both).  The buffer only grows while the slot
+// holds no batch.
+static bool pipe_copy_in(bra_gpu_ctx_s* c, bra_gpu_ctx_s::PipeSlot& ps, const uint8_t* h_in, uint64_t data_size)
+{
+    if (data_size + 16 > ps.cap_in && (ps.state != 0 || !grow(ps.d_in, ps.cap_in, data_size + 16)))
+        return false;
+    return hipStreamWaitEvent(c->copy_in, ps.ev_done, 0) == hipSuccess &&
+           hipMemcpyAsync(ps.d_in, h_in, data_size, hipMemcpyHostToDevice, c->copy_in) == hipSuccess &&
+           hipEventRecord(ps.ev_in, c->copy_in) == hipSuccess;
+}
+
+int bra_gpu_compress_chunks_stage(bra_gpu_ctx_t* c, int slot, const uint8_t* h_in, uint64_t data_size)
+{
+    if (!c || slot < 0 || slot > 1 || !h_in || !data_size)
+        return -1;
+    auto& ps = c->pipe[slot];
+    if (ps.staged)
+        return -1;  // submit the staged batch first
+    DevGuard dg(c->device);
+    if (!dg.ok || !pipe_init(c, ps) || !pipe_copy_in(c, ps, h_in, data_size))
+        return -1;
+    ps.staged  = true;
+    ps.st_ptr  = h_in;
+    ps.st_size = data_size;
+    return 0;
 }
 
 int bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* c, int slot, const uint8_t* h_in, uint64_t data_size, uint32_t block_size)
@@ -969,29 +1024,21 @@ int bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* c, int slot, const uint8_t* h_
     auto& ps = c->pipe[slot];
     if (ps.state != 0)
         return -1;  // collect the slot first
+    if (ps.staged && (ps.st_ptr != h_in || ps.st_size != data_size))
+        return -1;  // not the batch staged for this slot
     DevGuard dg(c->device);
-    if (!dg.ok)
+    if (!dg.ok || !pipe_init(c, ps))
         return -1;
-    if (!c->copy_in && (hipStreamCreateWithFlags(&c->copy_in, hipStreamNonBlocking) != hipSuccess ||
-                        hipStreamCreateWithFlags(&c->copy_out, hipStreamNonBlocking) != hipSuccess))
+    const bool     staged = ps.staged;
+    ps.staged             = false;
+    const auto     hb     = geometry(data_size, block_size);
+    const uint32_t nb     = (uint32_t) hb.size();
+    const uint64_t rb     = pipe_records_bound(hb);
+    hipStream_t    s      = c->stream;
+    if (!grow(ps.d_out, ps.cap_out, rb + 16) || !grow(c->d_hdr, c->cap_hdr, nb) || !grow(c->d_off, c->cap_off, nb + 1) ||
+        !grow(c->d_pay, c->cap_pay, rb) || !grow(c->d_word, c->cap_word, 4))
         return -1;
-    if (!c->h_pipe_mail && hipHostMalloc(&c->h_pipe_mail, 4 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
-    {
-        c->h_pipe_mail = nullptr;
-        return -1;
-    }
-    if ((!ps.ev_in && hipEventCreateWithFlags(&ps.ev_in, hipEventDisableTiming) != hipSuccess) ||
-        (!ps.ev_done && hipEventCreateWithFlags(&ps.ev_done, hipEventDisableTiming) != hipSuccess))
-        return -1;
-    const auto     hb  = geometry(data_size, block_size);
-    const uint32_t nb  = (uint32_t) hb.size();
-    const uint64_t rb  = pipe_records_bound(hb);
-    hipStream_t    s   = c->stream;
-    if (!grow(ps.d_in, ps.cap_in, data_size + 16) || !grow(ps.d_out, ps.cap_out, rb + 16) || !grow(c->d_hdr, c->cap_hdr, nb) ||
-        !grow(c->d_off, c->cap_off, nb + 1) || !grow(c->d_pay, c->cap_pay, rb) || !grow(c->d_word, c->cap_word, 4))
-        return -1;
-    if (hipMemcpyAsync(ps.d_in, h_in, data_size, hipMemcpyHostToDevice, c->copy_in) != hipSuccess || hipEventRecord(ps.ev_in, c->copy_in) != hipSuccess ||
-        hipStreamWaitEvent(s, ps.ev_in, 0) != hipSuccess)
+    if ((!staged && !pipe_copy_in(c, ps, h_in, data_size)) || hipStreamWaitEvent(s, ps.ev_in, 0) != hipSuccess)
         return -1;
     g_prof = c->prof.mask ? &c->prof : nullptr;
     int rc = encode_impl(c, ps.d_in, hb, c->d_hdr, c->d_off, c->d_pay, c->cap_pay, s, nullptr);
@@ -1002,6 +1049,10 @@ int bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* c, int slot, const uint8_t* h_
          !crc_stream_device(ps.d_in, data_size, block_size, reinterpret_cast<const uint8_t*>(c->d_hdr), 0, c->d_word, s) ||
          hipMemcpyAsync(mail, c->d_off + nb, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
          hipMemcpyAsync(mail + 1, c->d_word, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipEventRecord(ps.ev_done, s) != hipSuccess))
+        rc = -1;
+    // the caller may refill h_in once this returns (the encode's host waits came after the copy;
+    // this wait is for the error paths and says so explicitly)
+    if (hipEventSynchronize(ps.ev_in) != hipSuccess)
         rc = -1;
     if (rc != 0)
     {
@@ -1016,12 +1067,22 @@ int bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* c, int slot, const uint8_t* h_
 
 int bra_gpu_compress_chunks_collect(bra_gpu_ctx_t* c, int slot, uint8_t* h_out, uint64_t out_cap, uint64_t* out_size, uint32_t* chunks_crc)
 {
-    if (!c || slot < 0 || slot > 1 || c->pipe[slot].state != 1)
+    if (!c || slot < 0 || slot > 1)
         return -1;
-    auto& ps = c->pipe[slot];
-    ps.state = 0;
+    auto&    ps = c->pipe[slot];
     DevGuard dg(c->device);
-    if (!dg.ok || hipEventSynchronize(ps.ev_done) != hipSuccess)
+    if (!dg.ok)
+        return -1;
+    if (!h_out && ps.staged)
+    {
+        // a drain (no output buffer) also drops the slot's staged input copy
+        (void) hipStreamSynchronize(c->copy_in);
+        ps.staged = false;
+    }
+    if (ps.state != 1)
+        return -1;
+    ps.state = 0;
+    if (hipEventSynchronize(ps.ev_done) != hipSuccess)
         return -1;
     const uint64_t* mail = c->h_pipe_mail + 2 * slot;
     const uint64_t  need = mail[0] + (uint64_t) CHUNK_HDR_DISK * ps.nb;

@@ -203,10 +203,11 @@ bool bra_io_file_chunks_compress_file(bra_io_file_t* dst, bra_io_file_t* src, co
         bra_log_error("unable to compress file: %s", src->fn);
         return false;
     }
-    // Batches of BATCH_CHUNKS chunks, two in flight on the device (bra_gpu_compress_chunks_submit /
-    // _collect): batch k + 1's input copy and kernels are queued before batch k's records are
-    // copied back and written, and batch k + 2 is read from the file meanwhile.  Pinned host
-    // buffers make the copies asynchronous.
+    // Batches of BATCH_CHUNKS chunks, two in flight on the device (bra_gpu_compress_chunks_stage /
+    // _submit / _collect): batch k + 1's input copy is queued before batch k is submitted, so it
+    // arrives while batch k's kernels run; batch k - 1's records are copied back and written while
+    // batch k's later stages run; batch k + 2 is read from the file meanwhile.  Pinned host buffers
+    // make the copies asynchronous.
     const uint64_t batch  = _bra_min((uint64_t) BATCH_CHUNKS * CHUNK_SIZE, data_size);
     const uint64_t nbatch = batch ? (data_size + batch - 1) / batch : 0;
     const uint64_t cap    = bra_gpu_chunks_bound(batch, (uint32_t) CHUNK_SIZE);
@@ -214,59 +215,65 @@ bool bra_io_file_chunks_compress_file(bra_io_file_t* dst, bra_io_file_t* src, co
     uint8_t*       out    = (uint8_t*) bra_gpu_host_alloc(ctx, cap ? cap : 1);
     uint32_t       crc32  = BRA_CRC32C_INIT; /* the running CRC of header + source chunk pairs (:214,248-249) */
     bool           ok     = in[0] != NULL && in[1] != NULL && out != NULL;
-    bool           read_failed = false, pending[2] = {false, false};
+    bool           read_failed = false;
     batch_read_t   rd;
     memset(&rd, 0, sizeof rd);
 #define BATCH_LEN(k) _bra_min(batch, data_size - (uint64_t) (k) * batch)
+#define STAGE(k) (bra_gpu_compress_chunks_stage(ctx, (int) ((k) % 2), in[(k) % 2], BATCH_LEN(k)) == 0)
     if (ok && nbatch > 0)
     {
         read_failed = !bra_io_file_read(src, in[0], BATCH_LEN(0));
-        ok          = !read_failed && bra_gpu_compress_chunks_submit(ctx, 0, in[0], BATCH_LEN(0), (uint32_t) CHUNK_SIZE) == 0;
-        pending[0]  = ok;
+        ok          = !read_failed && STAGE(0);
         if (ok && nbatch > 1)
             batch_read_start(&rd, src, in[1], BATCH_LEN(1));
     }
-    for (uint64_t k = 0; ok && k < nbatch; ++k)
+    for (uint64_t k = 0; ok && k <= nbatch; ++k)
     {
-        bra_log_printf("%3u%%", (unsigned int) (k * batch * 100 / data_size));
-        bra_log_printf("\b\b\b\b");
-        if (k + 1 < nbatch)
+        if (k < nbatch)
         {
-            // batch k + 1 was read into in[(k + 1) % 2]; in[k % 2] is free (batch k's input copy ended
-            // before its jobs, which its submit waited for): batch k + 2 is read into it meanwhile
-            if (!batch_read_join(&rd))
-            {
-                read_failed = true;
+            bra_log_printf("%3u%%", (unsigned int) (k * batch * 100 / data_size));
+            bra_log_printf("\b\b\b\b");
+            // batch k + 1 (read into in[(k + 1) % 2]) is staged ahead of batch k's submit -- after it
+            // for the first batch, which goes to the device before the second one has been read
+            const bool stage_ahead = k > 0 && k + 1 < nbatch;
+            if (stage_ahead && !(read_failed = !batch_read_join(&rd)) && !STAGE(k + 1))
+                ok = false;
+            if (read_failed || !ok)
                 break;
-            }
-            if (k + 2 < nbatch)
-                batch_read_start(&rd, src, in[k % 2], BATCH_LEN(k + 2));
-            if (bra_gpu_compress_chunks_submit(ctx, (int) ((k + 1) % 2), in[(k + 1) % 2], BATCH_LEN(k + 1), (uint32_t) CHUNK_SIZE) != 0)
+            if (bra_gpu_compress_chunks_submit(ctx, (int) (k % 2), in[k % 2], BATCH_LEN(k), (uint32_t) CHUNK_SIZE) != 0)
             {
-                bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, (k + 1) * batch);
+                bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, k * batch);
                 ok = false;
                 break;
             }
-            pending[(k + 1) % 2] = true;
+            if (k == 0 && nbatch > 1 && !(read_failed = !batch_read_join(&rd)) && !STAGE(1))
+                ok = false;
+            if (read_failed || !ok)
+                break;
+            // in[k % 2] is free once batch k's submit has returned: batch k + 2 is read into it
+            if (k + 2 < nbatch)
+                batch_read_start(&rd, src, in[k % 2], BATCH_LEN(k + 2));
         }
+        if (k == 0)
+            continue;
         uint64_t osz  = 0;
         uint32_t bcrc = 0;
-        pending[k % 2] = false;
-        if (bra_gpu_compress_chunks_collect(ctx, (int) (k % 2), out, cap, &osz, &bcrc) < 0)
+        if (bra_gpu_compress_chunks_collect(ctx, (int) ((k - 1) % 2), out, cap, &osz, &bcrc) < 0)
         {
-            bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, k * batch);
+            bra_log_error("GPU chunk encoder failed: %s (chunks from %" PRIu64 ")", src->fn, (k - 1) * batch);
             ok = false;
             break;
         }
         // this batch's share of the running CRC: its headers and chunks follow the previous ones
-        const uint64_t n = BATCH_LEN(k);
+        const uint64_t n = BATCH_LEN(k - 1);
         crc32 = bra_gpu_crc32c_combine(crc32, bcrc, n + num_chunks(n) * sizeof(bra_io_chunk_header_t));
         ok    = bra_io_file_write(&tmpfile, out, (size_t) osz);
     }
+#undef STAGE
 #undef BATCH_LEN
     (void) batch_read_join(&rd);
-    for (int q = 0; q < 2; ++q)
-        if (pending[q])  // a batch still in flight after an error: drained, its records dropped
+    if (read_failed || !ok)
+        for (int q = 0; q < 2; ++q)  // batches still in flight or staged after an error: drained, dropped
             (void) bra_gpu_compress_chunks_collect(ctx, q, NULL, 0, NULL, NULL);
     bra_gpu_host_free(ctx, in[0]);
     bra_gpu_host_free(ctx, in[1]);

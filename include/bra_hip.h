@@ -209,19 +209,24 @@ int bra_gpu_decompress_chunks_host(bra_gpu_ctx_t* ctx, const uint8_t* h_stream, 
 
 /*
  * The same compression with two batches in flight (the front end's overlapped batch loop, replacing
- * the reference's per-chunk loop lib_bra_io_file_chunks.c:199-266).  bra_gpu_compress_chunks_submit
- * copies h_in to the device on the context's input-copy stream and queues the batch's encode,
- * framing and chunk-stream CRC behind that copy in slot 0 or 1; it returns once the batch's BWT jobs
- * are done, with the rest of the batch still queued.  bra_gpu_compress_chunks_collect waits for the
- * slot's batch, copies its chunk records into h_out on the output-copy stream and returns what
- * bra_gpu_compress_chunks_host returns (1 smaller than the input, 0 not smaller, -2 out_cap too
- * small: *out_size = the bytes needed, -1 error); a slot is collected before it is submitted again.
- * Submitting batch k + 1 before collecting batch k overlaps its input copy with batch k's kernels
- * and batch k's output copy with its own.  Host buffers from bra_gpu_host_alloc (pinned) make the
- * copies asynchronous; bra_gpu_host_free releases them.
+ * the reference's per-chunk loop lib_bra_io_file_chunks.c:199-266).  bra_gpu_compress_chunks_stage
+ * queues the copy of h_in into slot 0 or 1 on the context's input-copy stream, behind the device's
+ * use of the slot's previous batch; bra_gpu_compress_chunks_submit queues the slot's encode, framing
+ * and chunk-stream CRC behind that copy (it makes the copy itself when the slot has none staged; a
+ * staged slot must be submitted with the same h_in and data_size) and returns once the batch's BWT
+ * jobs are done, with the rest of the batch still queued; h_in may be refilled from then on.
+ * bra_gpu_compress_chunks_collect waits for the slot's batch, copies its chunk records into h_out on
+ * the output-copy stream and returns what bra_gpu_compress_chunks_host returns (1 smaller than the
+ * input, 0 not smaller, -2 out_cap too small: *out_size = the bytes needed, -1 error); a slot is
+ * collected before it is submitted again.  Collect with h_out NULL drains the slot: it waits for the
+ * submitted batch and drops it, and drops a staged copy.  The overlapped order: stage(k + 1) before submit(k)
+ * (batch k + 1's input arrives while batch k's kernels run), then collect(k - 1) (its records return
+ * under batch k's kernels).  Host buffers from bra_gpu_host_alloc (pinned) make the copies
+ * asynchronous; bra_gpu_host_free releases them.
  */
 void* bra_gpu_host_alloc(bra_gpu_ctx_t* ctx, uint64_t bytes);
 void  bra_gpu_host_free(bra_gpu_ctx_t* ctx, void* p);
+int   bra_gpu_compress_chunks_stage(bra_gpu_ctx_t* ctx, int slot, const uint8_t* h_in, uint64_t data_size);
 int   bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* ctx, int slot, const uint8_t* h_in, uint64_t data_size, uint32_t block_size);
 int   bra_gpu_compress_chunks_collect(bra_gpu_ctx_t* ctx, int slot, uint8_t* h_out, uint64_t out_cap, uint64_t* out_size, uint32_t* chunks_crc);
 

@@ -6,7 +6,8 @@ usage: make_pmc_summary.py <run_dir> <workload key> [<out.json>]
 The file holds one entry per workload key: {"workloads": {key: {"source", "kernels": {slot: ...}}}};
 other keys already in the file are kept.  A slot's launch is the group of kernels its BRA_PROF scope
 covers (bwt.mjobs = the workgroup-job kernels of one encode, one per size class); hbm bytes =
-2 * FETCH_SIZE + WRITE_SIZE (the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md).
+2 * FETCH_SIZE + WRITE_SIZE (the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md); with the SQ
+and GRBM passes, the slot's VALU instructions per launch and valu_frac (scripts/pmc_summary.py).
 """
 import json
 import os
@@ -39,10 +40,17 @@ if __name__ == "__main__":
         have = [k[n] for n in names if n in k]
         if not have:
             continue
-        entry["kernels"][slot] = {
+        ks = entry["kernels"][slot] = {
             "hbm_bytes_per_launch": int(sum(e["hbm_bytes_per_launch"] for e in have)),
             "kernels": {n: k[n] for n in names if n in k},
         }
+        # VALU of the slot's launch: its kernels run one after the other, so their cycles add
+        if all("valu_insts_per_launch" in e for e in have):
+            ks["valu_insts_per_launch"] = int(sum(e["valu_insts_per_launch"] for e in have))
+        if all("valu_frac" in e for e in have):
+            quads = sum(e["active_valu_quads_per_launch"] for e in have)
+            cyc = sum(e["gui_active_per_launch"] for e in have) / 8
+            ks["valu_frac"] = round(4 * quads / (cyc * 1024), 4)
     res["workloads"][key] = entry
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for s_, e in entry["kernels"].items():

@@ -2,7 +2,7 @@
 kernel + memory-copy trace that shows the copies under the kernels (measurement only):
 
     rocprofv3 --kernel-trace --memory-copy-trace -d <dir> -o run --output-format csv -- \
-        python3 scripts/pcie_trace.py [batches] [kind] [block_size]
+        python3 scripts/pcie_trace.py [batches | b1,b2,...] [kind] [block_size]
 
 Prints the JSON of bench.pcie_inclusive (serial and overlapped GB/s)."""
 import importlib
@@ -19,7 +19,10 @@ def main():
 
     import bench
 
-    nbatch = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    # batches: a count (equal batches) or a comma-separated list of batch sizes in blocks
+    arg = sys.argv[1] if len(sys.argv) > 1 else "2"
+    split = [int(v) for v in arg.split(",")] if "," in arg else None
+    nbatch = len(split) if split else int(arg)
     kind = sys.argv[2] if len(sys.argv) > 2 else "text"
     bs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
     bra = importlib.import_module("br-archive_amd")
@@ -37,7 +40,7 @@ def main():
     torch.cuda.synchronize()
     payload_bytes = int(off[nb].item())
     codec2 = bra.BlockCodec(0)
-    res = bench.pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, ws, nbatch, codec2)
+    res = bench.pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, ws, nbatch, codec2, split)
     codec2.close()
     res["device_resident_reference"] = "bench.py value (same input, one 256 MiB batch)"
     print(json.dumps(res), flush=True)

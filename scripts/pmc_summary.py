@@ -1,8 +1,13 @@
 """Summarise rocprofv3 --pmc passes per kernel (test/measurement tooling, not product code).
 
-usage: pmc_summary.py <run_dir>  -- reads <run_dir>/{fetch,write,sq1}/run_counter_collection.csv.
+usage: pmc_summary.py <run_dir>  -- reads <run_dir>/{fetch,write,sq1,grbm}/run_counter_collection.csv.
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE reports half of the bytes of
 wide coalesced reads (MI355X_MICROARCH.md, HBM section), so hbm_bytes = 2 * FETCH + WRITE.
+VALU: SQ_INSTS_VALU = wave-level VALU instructions issued; SQ_ACTIVE_INST_VALU counts quad-cycles
+(MI355X_MICROARCH.md, "s_memtime tick vs SQ PMC units") over all waves; GRBM_GUI_ACTIVE is summed
+over the 8 XCDs, so a dispatch lasts GRBM_GUI_ACTIVE / 8 cycles and the chip has 256 CUs x 4 SIMDs
+= 1024 VALU issue ports: valu_frac = 4 * SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 * 1024), the
+fraction of the chip's VALU issue cycles the dispatch used.
 """
 import collections
 import csv
@@ -10,6 +15,8 @@ import json
 import os
 import re
 import sys
+
+N_SIMD = 256 * 4  # VALU issue ports: 256 CUs x 4 SIMDs
 
 
 def short(name):
@@ -30,6 +37,7 @@ def main(d):
     f = load(os.path.join(d, "fetch", "run_counter_collection.csv"))
     w = load(os.path.join(d, "write", "run_counter_collection.csv"))
     sq = load(os.path.join(d, "sq1", "run_counter_collection.csv"))
+    gr = load(os.path.join(d, "grbm", "run_counter_collection.csv"))
     out = {}
     for k in sorted(set(f) | set(w)):
         fs = f[k].get("FETCH_SIZE", [0.0])
@@ -41,6 +49,14 @@ def main(d):
             wc = sum(c["SQ_WAVE_CYCLES"])
             e["sq_frac_of_wave_cycles"] = {n: round(sum(v) / wc, 3) for n, v in c.items() if n.startswith(("SQ_WAIT", "SQ_ACTIVE"))}
             e["valu_insts_per_lds_inst"] = round(sum(c.get("SQ_INSTS_VALU", [0])) / max(1.0, sum(c.get("SQ_INSTS_LDS", [0]))), 2)
+            n = len(c["SQ_WAVE_CYCLES"])
+            e["valu_insts_per_launch"] = sum(c.get("SQ_INSTS_VALU", [0])) / n
+            e["active_valu_quads_per_launch"] = sum(c.get("SQ_ACTIVE_INST_VALU", [0])) / n
+        g = gr.get(k)
+        if g and g.get("GRBM_GUI_ACTIVE"):
+            e["gui_active_per_launch"] = sum(g["GRBM_GUI_ACTIVE"]) / len(g["GRBM_GUI_ACTIVE"])
+            if "active_valu_quads_per_launch" in e:
+                e["valu_frac"] = round(4 * e["active_valu_quads_per_launch"] / (e["gui_active_per_launch"] / 8 * N_SIMD), 4)
         out[k] = e
     return out
 
@@ -49,6 +65,6 @@ if __name__ == "__main__":
     res = main(sys.argv[1])
     for k, e in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"]):
         print(f"{k[:34]:34s} n={e['launches']:3d} hbm/launch {e['hbm_bytes_per_launch'] / 1e6:10.2f} MB", e.get("sq_frac_of_wave_cycles", ""),
-              e.get("valu_insts_per_lds_inst", ""))
+              e.get("valu_insts_per_lds_inst", ""), e.get("valu_frac", ""))
     if len(sys.argv) > 2:
         json.dump(res, open(sys.argv[2], "w"), indent=1)

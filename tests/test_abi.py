@@ -24,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     out = subprocess.check_output(["nm", "-D", "--defined-only", bra.LIB_PATH], text=True)
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     declared = _header_functions()
-    assert len(declared) == 45
+    assert len(declared) == 46
     missing = [f for f in declared if f not in exported]
     assert not missing, missing
     assert sorted(bra.ABI_SYMBOLS) == declared
@@ -90,4 +90,4 @@ def test_lib_bra_links_against_gpu_library(lib):
     if lib == "libbralib_hipenc.so":  # the reference's own chunk loop calls the drop-in encoders
         assert {"bra_bwt_encode2", "bra_mtf_encode2", "bra_rle_encode", "bra_huffman_encode", "bra_huffman_chunk_free"} <= need
     else:  # the batched front end calls the batch ABI
-        assert {"bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect", "bra_gpu_decompress_chunks_host"} <= need
+        assert {"bra_gpu_compress_chunks_stage", "bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect", "bra_gpu_decompress_chunks_host"} <= need

@@ -317,10 +317,49 @@ def test_pipelined_host_compression_long_stream(bra, codec):
 
     data = bra.synth_fill(0, (6 << 20) + 100, CS)
     want, wcrc, _ = codec.compress_chunks(torch.from_numpy(data).cuda(), CS)
-    res = codec.compress_chunks_pipelined(data, 1 << 20, CS)
-    assert b"".join(r[0] for r in res) == want.cpu().numpy().tobytes()
-    crc = 0
-    for (_, bcrc, _), o in zip(res, range(0, data.size, 1 << 20)):
-        n = min(1 << 20, data.size - o)
-        crc = bra.crc32c_combine(crc, bcrc, n + (-(-n // CS)) * 268)
-    assert crc == wcrc
+    for stage_ahead in (True, False):  # staged copies (the front end's order) and submit-made copies
+        res = codec.compress_chunks_pipelined(data, 1 << 20, CS, stage_ahead=stage_ahead)
+        assert b"".join(r[0] for r in res) == want.cpu().numpy().tobytes()
+        crc = 0
+        for (_, bcrc, _), o in zip(res, range(0, data.size, 1 << 20)):
+            n = min(1 << 20, data.size - o)
+            crc = bra.crc32c_combine(crc, bcrc, n + (-(-n // CS)) * 268)
+        assert crc == wcrc
+
+
+@pytest.mark.gpu
+def test_pipelined_stage_protocol(bra):
+    """bra_gpu_compress_chunks_stage: one staged copy per slot, a submit must name the staged batch,
+    a drain (collect with no output) drops a staged copy and the slot is usable again."""
+    import ctypes as C
+
+    lib = bra.lib
+    c = bra.BlockCodec(0)
+    data = bra.synth_fill(0, 3 * CS + 7, CS)
+    n = data.size
+    h = [lib.bra_gpu_host_alloc(c.ctx, n) for _ in range(2)]
+    cap = lib.bra_gpu_chunks_bound(n, CS)
+    out = lib.bra_gpu_host_alloc(c.ctx, cap)
+    try:
+        for p in h:
+            C.memmove(p, data.ctypes.data, n)
+        assert lib.bra_gpu_compress_chunks_stage(c.ctx, 0, h[0], n) == 0
+        assert lib.bra_gpu_compress_chunks_stage(c.ctx, 0, h[0], n) == -1  # already staged
+        assert lib.bra_gpu_compress_chunks_submit(c.ctx, 0, h[1], n, CS) == -1  # not the staged buffer
+        assert lib.bra_gpu_compress_chunks_submit(c.ctx, 0, h[0], n - 1, CS) == -1  # not the staged size
+        assert lib.bra_gpu_compress_chunks_collect(c.ctx, 0, None, 0, None, None) == -1  # drain: nothing submitted
+        assert lib.bra_gpu_compress_chunks_stage(c.ctx, 0, h[1], n) == 0  # the staged copy was dropped
+        assert lib.bra_gpu_compress_chunks_submit(c.ctx, 0, h[1], n, CS) == 0
+        # slot 1 staged while slot 0's batch is in flight, submitted after slot 0 is collected
+        assert lib.bra_gpu_compress_chunks_stage(c.ctx, 1, h[0], n) == 0
+        size, crc = C.c_uint64(), C.c_uint32()
+        assert lib.bra_gpu_compress_chunks_collect(c.ctx, 0, out, cap, C.byref(size), C.byref(crc)) == 1
+        first = C.string_at(out, size.value)
+        assert lib.bra_gpu_compress_chunks_submit(c.ctx, 1, h[0], n, CS) == 0
+        size2, crc2 = C.c_uint64(), C.c_uint32()
+        assert lib.bra_gpu_compress_chunks_collect(c.ctx, 1, out, cap, C.byref(size2), C.byref(crc2)) == 1
+        assert C.string_at(out, size2.value) == first and crc2.value == crc.value
+    finally:
+        for p in (*h, out):
+            lib.bra_gpu_host_free(c.ctx, p)
+        c.close()
