@@ -2,7 +2,7 @@
 kernel + memory-copy trace that shows the copies under the kernels (measurement only):
 
     rocprofv3 --kernel-trace --memory-copy-trace -d <dir> -o run --output-format csv -- \
-        python3 scripts/pcie_trace.py [batches | b1,b2,...] [kind] [block_size]
+        python3 scripts/pcie_trace.py [batches | b1,b2,... | stream[:S]] [kind] [block_size]
 
 Prints the JSON of bench.pcie_inclusive (serial and overlapped GB/s)."""
 import importlib
@@ -15,14 +15,25 @@ sys.path.insert(0, ROOT)
 
 
 def main():
-    import torch
-
     import bench
 
-    # batches: a count (equal batches) or a comma-separated list of batch sizes in blocks
+    # batches: a count (equal batches), a comma-separated list of batch sizes in blocks, or
+    # "stream[:S]" (S batches of 256 MiB through the pipelined API, bench.pcie_stream)
     arg = sys.argv[1] if len(sys.argv) > 1 else "2"
+    if arg.startswith("stream"):
+        kind = sys.argv[2] if len(sys.argv) > 2 else "text"
+        bs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
+        bra = importlib.import_module("br-archive_amd")
+        data_np = bra.synth_fill(bench.KINDS[kind], 256 << 20, bs)
+        codec = bra.BlockCodec(0)
+        res = bench.pcie_stream(bra, codec, data_np, kind, bs, int(arg.split(":")[1]) if ":" in arg else 4)
+        codec.close()
+        print(json.dumps(res), flush=True)
+        return
     split = [int(v) for v in arg.split(",")] if "," in arg else None
     nbatch = len(split) if split else int(arg)
+    import torch
+
     kind = sys.argv[2] if len(sys.argv) > 2 else "text"
     bs = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
     bra = importlib.import_module("br-archive_amd")
