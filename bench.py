@@ -452,7 +452,9 @@ def main():
     per_batch = max(1, args.batch_bytes // bs)
     batches = [(b0, min(nb, b0 + per_batch)) for b0 in range(0, nb, per_batch)]
     off_b = torch.empty((per_batch + 1,), dtype=torch.int64, device=dev)
-    gather = dmod.ChunkGather(dist, rank, world) if world > 1 else None
+    # sizes from the geometry: the payloads travel at their bound, no rank waits on the host for the
+    # others' encodes (unmeasured on hardware until a driver SCALE record exists)
+    gather = dmod.ChunkGather(dist, rank, world, geometry=(global_total, bs)) if world > 1 else None
     work_stream = torch.cuda.Stream()
     gather_stream = torch.cuda.Stream() if world > 1 else None
     result = {}
@@ -461,8 +463,8 @@ def main():
     def gather_assemble(k, ev):
         """Gather output set k (its encode ended at event ev) to rank 0 and assemble it there, on the
         gather stream: the collectives wait for that encode only, not for the one queued after it, so
-        the host's read of the gathered sizes (ChunkGather) finds them ready and the transfers run
-        under the next step's kernels."""
+        the transfers run under the next step's kernels (the gather posts them at the geometry's
+        payload bounds, with no host read of the gathered sizes)."""
         with torch.cuda.stream(gather_stream):
             gather_stream.wait_event(ev)
             parts = gather(*outs[k])

@@ -5,10 +5,13 @@ is encoded by rank b mod G (round robin, as configs[3] states); a rank's blocks 
 its own HBM in ascending global order.  The one exchange step gathers the compressed chunks to
 rank 0:
 
-  1. all_gather of each rank's payload byte count (one int64 per rank),
+  1. all_gather of each rank's payload byte count (one int64 per rank) -- or, when the gather knows
+     the global geometry, nothing: every rank's block count and payload bound follow from it
+     (`shard_payload_bound`), so no rank waits on the host for another rank's encode,
   2. per peer one send/recv of its chunk headers (nblocks x 268 B, `bra_io_chunk_header_t`), its
-     payload offsets, its payload bytes and its 4-byte share of the chunk-stream CRC, posted
-     together with batch_isend_irecv,
+     payload offsets, its payload bytes (the exact count, or the bound: the assembly reads the
+     offsets on the device) and its 4-byte share of the chunk-stream CRC, posted together with
+     batch_isend_irecv,
   3. on rank 0, `BlockCodec.assemble_shards` interleaves the parts back into global block order on
      the device, and the CRC shares XOR to the CRC32C of the whole chunk stream (every rank computed
      its share with `chunks_crc32c_shard`, positions taken in the global stream).
@@ -43,13 +46,33 @@ def shard_bytes(total: int, block_size: int, rank: int, world: int) -> int:
     return (len(mine) - 1) * block_size + min(block_size, total - last * block_size)
 
 
+def shard_payload_bound(total: int, block_size: int, rank: int, world: int) -> int:
+    """Payload bytes rank `rank`'s blocks can take at most: per block its PackBits RLE capacity
+    (n + ceil(n / 128) + 16, csrc/rle.h) plus a 16-byte word of padding, + 64 -- the bound the encode
+    chain itself relies on (csrc/capi.hip encode_impl, `cap_ok`): an optimal prefix code over byte
+    symbols is never longer than the 8-bit code of the RLE bytes."""
+    nb = num_blocks(total, block_size)
+    r = 64
+    for b in shard_blocks(nb, rank, world):
+        n = min(block_size, total - b * block_size)
+        r += n + (n + 127) // 128 + 16 + 16
+    return r
+
+
 class ChunkGather:
     """Gathers (headers, offsets, payload, crc share) of every rank to rank 0; receive buffers are
-    kept between calls."""
+    kept between calls.  With `geometry` = (global_total, block_size) (round-robin shards) the
+    payloads travel at their bound and no sizes are exchanged: the call queues its transfers
+    without a host wait (RCCL); the assembly reads the received offsets on the device."""
 
-    def __init__(self, dist, rank: int, world: int):
+    def __init__(self, dist, rank: int, world: int, geometry: tuple[int, int] | None = None):
         self.dist, self.rank, self.world = dist, rank, world
         self.bufs: dict[int, tuple] = {}
+        self.bounds = None
+        if geometry is not None:
+            total, bs = geometry
+            nb = num_blocks(total, bs)
+            self.bounds = [(len(shard_blocks(nb, r, world)), shard_payload_bound(total, bs, r, world)) for r in range(world)]
 
     def __call__(self, hdr, off, pay, crc):
         """hdr: uint8 [nb, 268]; off: int64 [nb + 1] (off[nb] = this rank's payload bytes); pay: uint8
@@ -62,15 +85,23 @@ class ChunkGather:
         # through host copies; RCCL moves the device tensors themselves
         host = hdr.is_cuda and dist.get_backend() == "gloo"
         dev = hdr.device
-        if host:
-            hdr, off, pay, crc = hdr.cpu(), off.cpu(), pay[: int(off[-1].item())].cpu(), crc.cpu()
-        # (payload bytes, block count) of every rank in one small all_gather
-        meta = torch.cat([off[-1:], torch.full((1,), hdr.shape[0], dtype=torch.int64, device=off.device)])
-        metas = [torch.empty_like(meta) for _ in range(world)]
-        dist.all_gather(metas, meta)
-        metas = [m.tolist() for m in metas]
-        sizes = [int(m[0]) for m in metas]
-        nbs = [int(m[1]) for m in metas]
+        if self.bounds is not None:
+            nbs = [b[0] for b in self.bounds]
+            sizes = [b[1] for b in self.bounds]
+            if hdr.shape[0] != nbs[rank] or pay.numel() < sizes[rank]:
+                raise ValueError("ChunkGather: this rank's output does not match the geometry's shard")
+            if host:
+                hdr, off, pay, crc = hdr.cpu(), off.cpu(), pay[: sizes[rank]].cpu(), crc.cpu()
+        else:
+            if host:
+                hdr, off, pay, crc = hdr.cpu(), off.cpu(), pay[: int(off[-1].item())].cpu(), crc.cpu()
+            # (payload bytes, block count) of every rank in one small all_gather
+            meta = torch.cat([off[-1:], torch.full((1,), hdr.shape[0], dtype=torch.int64, device=off.device)])
+            metas = [torch.empty_like(meta) for _ in range(world)]
+            dist.all_gather(metas, meta)
+            metas = [m.tolist() for m in metas]  # (the host waits for every rank's encode here)
+            sizes = [int(m[0]) for m in metas]
+            nbs = [int(m[1]) for m in metas]
         ops = []
         if rank == 0:
             for r in range(1, world):
@@ -78,7 +109,7 @@ class ChunkGather:
                 if b is None or b[2].numel() < sizes[r] or b[0].shape[0] != nbs[r]:
                     b = (torch.empty((nbs[r], HEADER_BYTES), dtype=torch.uint8, device=hdr.device),
                          torch.empty((nbs[r] + 1,), dtype=torch.int64, device=hdr.device),
-                         torch.empty((int(sizes[r] * 1.1) + 4096,), dtype=torch.uint8, device=pay.device),
+                         torch.empty((sizes[r] if self.bounds else int(sizes[r] * 1.1) + 4096,), dtype=torch.uint8, device=pay.device),
                          torch.empty((1,), dtype=torch.int32, device=hdr.device))
                     self.bufs[r] = b
                 ops.append(dist.P2POp(dist.irecv, b[0], r))

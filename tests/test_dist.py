@@ -81,9 +81,10 @@ def _rank_output(orc, rank, world, total):
     return torch.from_numpy(hdr), torch.from_numpy(off), torch.from_numpy(pay), crc_t
 
 
-def _worker(rank, world, port, total, q):
+def _worker(rank, world, port, total, q, bound=False):
     try:
         sys.path.insert(0, ROOT)
+        import torch
         import torch.distributed as dist
 
         from oracle import Oracle
@@ -93,7 +94,14 @@ def _worker(rank, world, port, total, q):
         dmod = importlib.import_module("br-archive_amd.dist")
         orc = Oracle()
         hdr, off, pay, crc = _rank_output(orc, rank, world, total)
-        g = dmod.ChunkGather(dist, rank, world)
+        if bound:
+            # sizes from the geometry: the payload travels at its bound (its tail is padding)
+            g = dmod.ChunkGather(dist, rank, world, geometry=(total, BS))
+            pb = dmod.shard_payload_bound(total, BS, rank, world)
+            assert pb >= pay.numel() - 64
+            pay = torch.cat([pay, torch.full((pb + 64 - pay.numel(),), 0xEE, dtype=torch.uint8)])
+        else:
+            g = dmod.ChunkGather(dist, rank, world)
         for _ in range(2):  # the second call reuses the receive buffers
             parts = g(hdr, off, pay, crc)
         ok = True
@@ -116,14 +124,16 @@ def _worker(rank, world, port, total, q):
         q.put((rank, repr(e) + traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,total", [(2, 7 * BS - 3096), (3, 8 * BS), (2, 1 * BS)])
-def test_gather_chunks_gloo(world, total):
+@pytest.mark.parametrize("world,total,bound", [(2, 7 * BS - 3096, False), (3, 8 * BS, False), (2, 1 * BS, False), (2, 7 * BS - 3096, True),
+                                               (3, 8 * BS, True)])
+def test_gather_chunks_gloo(world, total, bound):
+    """bound: sizes from the geometry (no size all_gather), payloads at their bound."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q, bound)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=180) for _ in procs)
