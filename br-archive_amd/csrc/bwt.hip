@@ -63,7 +63,7 @@ constexpr uint32_t DCAP_JOB     = 512;  // refinement depth after which a tied g
 constexpr uint32_t RANK_KEYBYTES = 4;   // rank keys are 32-bit
 constexpr uint32_t CSTRIDE    = 256 + 16;  // digit-counter copies (TileStagePN, k_hist): 16 banks apart
 constexpr int      SCATTER_NC = 4;  // digit-counter copies of the MSD scatter
-constexpr int      HIST_NC    = 4;  // counter copies of the MSD histogram (copy = lane & (NC - 1))
+constexpr int      HIST_NC    = 4;  // counter copies of the MSD histogram (copy = lane & (NC - 1)), [digit][copy]; 1 / 2 / 8 / 16 measured slower
 constexpr uint32_t JQ_CHUNK   = 2;  // wave jobs a wave claims with one atomic (8: equal)
 // Former compile-time tuning knobs are constants now: a build that still passes one fails here
 // instead of measuring the default under another label.
@@ -561,10 +561,13 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
         // (dig[buf][slot] = the element's digit at this level): 16 contiguous digits per lane and
         // 1 KiB step, 4 steps per tile.  The next tile's descriptor is loaded before the current one
         // is counted.
-        __shared__ __attribute__((aligned(16))) uint32_t hw[TPB / 64][HIST_NC * CSTRIDE];  // 16-aligned: read back as uint4
+        // Counters [digit][copy], HIST_NC copies, copy = lane % HIST_NC: the lanes of one atomic that
+        // share a digit hit HIST_NC different banks (skewed digits: few lanes per address), and the
+        // read-back of a lane's 4 digits is 4 x HIST_NC contiguous words.
+        __shared__ __attribute__((aligned(16))) uint32_t hw[TPB / 64][256 * HIST_NC];
         const uint32_t      wv = threadIdx.x >> 6, lane = (uint32_t) lane_id();
         uint32_t* const     hc = hw[wv];
-        const uint32_t      cp = (lane & (HIST_NC - 1)) * CSTRIDE;
+        const uint32_t      cp = lane & (HIST_NC - 1);
         uint32_t            p  = tile_pos_wave(to, 0, ntiles, wv, TPB / 64);
         TileDesc            D{};
         if (p != ~0u)
@@ -575,8 +578,9 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
             TileDesc       Dn{};
             if (pn != ~0u)
                 Dn = to.desc[pn];
-            for (uint32_t c = lane; c < HIST_NC * CSTRIDE; c += 64)
-                hc[c] = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < 256 * HIST_NC / 256; ++c)
+                reinterpret_cast<uint4*>(hc)[c * 64 + lane] = make_uint4(0, 0, 0, 0);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): without it the wave's own LDS phases overlapped (wrong counts, GPU-measured)
@@ -587,52 +591,70 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
                 const uint64_t* pay = (D.buf ? key1 : key0) + D.s0;
                 const uint32_t  jj  = D.d - D.kd;
                 for (uint32_t i = lane; i < D.cnt; i += 64)
-                    atomicAdd(&hc[cp + p_digit(pay[i], jj)], 1u);
+                    atomicAdd(&hc[p_digit(pay[i], jj) * HIST_NC + cp], 1u);
             }
-            else
+            else if (D.cnt == TILE)
             {
+                // a full tile: the four 16-byte loads in flight together, no per-digit guards
                 const uint8_t* g = (D.buf ? dig1 : dig0) + D.s0;
                 uint4          w4[TILE / 1024];
 #pragma unroll
                 for (int j = 0; j < TILE / 1024; ++j)
-                {
-                    const uint32_t e = (uint32_t) j * 1024 + lane * 16;
-                    if (e + 16 <= D.cnt)
-                        w4[j] = *reinterpret_cast<const uint4_u*>(g + e);
-                    else
-                    {
-                        uint32_t x[4] = {0, 0, 0, 0};
-                        for (uint32_t i = 0; e + i < D.cnt && i < 16; ++i)
-                            x[i >> 2] |= (uint32_t) g[e + i] << (8 * (i & 3));
-                        w4[j] = make_uint4(x[0], x[1], x[2], x[3]);
-                    }
-                }
+                    w4[j] = *reinterpret_cast<const uint4_u*>(g + j * 1024 + lane * 16);
 #pragma unroll
                 for (int j = 0; j < TILE / 1024; ++j)
                 {
                     const uint32_t wd[4] = {w4[j].x, w4[j].y, w4[j].z, w4[j].w};
-                    const uint32_t e     = (uint32_t) j * 1024 + lane * 16;
 #pragma unroll
                     for (int i = 0; i < 16; ++i)
-                        if (e + i < D.cnt)
-                            atomicAdd(&hc[cp + ((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu)], 1u);
+                        atomicAdd(&hc[((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu) * HIST_NC + cp], 1u);
+                }
+            }
+            else
+            {
+                const uint8_t* g = (D.buf ? dig1 : dig0) + D.s0;
+                for (uint32_t e = lane * 16; e < D.cnt; e += 1024)
+                {
+                    uint32_t x[4] = {0, 0, 0, 0};
+                    if (e + 16 <= D.cnt)
+                    {
+                        const uint4 q = *reinterpret_cast<const uint4_u*>(g + e);
+                        x[0] = q.x, x[1] = q.y, x[2] = q.z, x[3] = q.w;
+                    }
+                    else
+                        for (uint32_t i = 0; e + i < D.cnt && i < 16; ++i)
+                            x[i >> 2] |= (uint32_t) g[e + i] << (8 * (i & 3));
+                    const uint32_t m = min(16u, D.cnt - e);
+                    for (uint32_t i = 0; i < m; ++i)
+                        atomicAdd(&hc[((x[i >> 2] >> (8 * (i & 3))) & 0xFFu) * HIST_NC + cp], 1u);
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): without it the wave's own LDS phases overlapped (wrong counts, GPU-measured)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint4 tot = make_uint4(0, 0, 0, 0);
+            uint32_t tot[4];
 #pragma unroll
-            for (int c = 0; c < HIST_NC; ++c)
+            for (int k = 0; k < 4; ++k)
             {
-                const uint4 h = *reinterpret_cast<const uint4*>(&hc[c * CSTRIDE + lane * 4]);
-                tot.x += h.x;
-                tot.y += h.y;
-                tot.z += h.z;
-                tot.w += h.w;
+                uint32_t t = 0;
+                if constexpr (HIST_NC >= 4)
+                {
+                    const uint4* row = reinterpret_cast<const uint4*>(&hc[(lane * 4 + k) * HIST_NC]);
+#pragma unroll
+                    for (int c = 0; c < HIST_NC / 4; ++c)
+                    {
+                        const uint4 h = row[c];
+                        t += h.x + h.y + h.z + h.w;
+                    }
+                }
+                else
+#pragma unroll
+                    for (int c = 0; c < HIST_NC; ++c)
+                        t += hc[(lane * 4 + k) * HIST_NC + c];
+                tot[k] = t;
             }
-            reinterpret_cast<uint4*>(tile_hist + (size_t) D.t * 256)[lane] = tot;
+            reinterpret_cast<uint4*>(tile_hist + (size_t) D.t * 256)[lane] = make_uint4(tot[0], tot[1], tot[2], tot[3]);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): without it the wave's own LDS phases overlapped (wrong counts, GPU-measured)
