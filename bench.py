@@ -676,12 +676,17 @@ def main():
                 # the compute side of the job kernels (sorting networks and string compares, not HBM
                 # bound): VALU issue fraction of the chip and VALU instructions per input byte of the
                 # launch (one launch covers the whole batch), from the SQ / GRBM passes
+                # (valu_frac = 4 x SQ_ACTIVE_INST_VALU quad-cycles / the chip's VALU issue cycles: about 1
+                # means VALU-issue saturated; valu_insts_per_element = lane instructions per element the
+                # launch covers: the job slots' 11 algorithmic bytes per element, else the batch)
                 valu = {}
                 for slot in dict.fromkeys((dominant, "bwt.jobs", "bwt.mjobs")):
                     e = wl.get("kernels", {}).get(slot, {})
                     if "valu_frac" in e:
+                        pe = prof0.get(slot)
+                        elems = pe[2] / max(1, pe[1]) / 11.0 if slot.startswith("bwt.") and "jobs" in slot and pe and pe[2] else my_bytes
                         valu[slot] = {"valu_frac": e["valu_frac"],
-                                      "valu_insts_per_element": round(e.get("valu_insts_per_launch", 0) * 64 / my_bytes, 2)}
+                                      "valu_insts_per_element": round(e.get("valu_insts_per_launch", 0) * 64 / max(1.0, elems), 1)}
                 if dominant in valu:
                     line["roofline"].update(valu[dominant])
                 if valu:
