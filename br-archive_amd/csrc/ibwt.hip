@@ -15,7 +15,7 @@
 //        lanes that finish claim the next splitter at once, so no lane idles on a long hop;
 //   k_ib_chain3  one workgroup per block ranks the splitter list from the primary splitter by
 //        pointer jumping in LDS -> output offset of every hop (and the primary cycle's length);
-//   k_ib_copy4   one lane per hop streams its staged bytes to their output offset.
+//   k_ib_copy16  sixteen lanes per hop stream its staged bytes to their output offset.
 // A primary index on a cycle shorter than n (a periodic block) makes the output periodic with that
 // cycle length, exactly like the reference (k_ib_repeat).  The round-1 two-walk kernels remain for
 // blocks of >= 2^24 bytes, for callers that want the transform itself, and as the fallback when
@@ -667,90 +667,64 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
     }
 }
 
-// Lane-per-hop copy: hops average S = 64 bytes, so a wave per hop left most lanes idle and paid
-// three dependent global round trips per 64 bytes.  A lane streams its slot (16-byte aligned) into
-// the output with aligned dword stores (alignbyte of consecutive source dwords; the bytes of the
-// first and last partial dwords go one at a time, the neighbouring hops own the rest of them).
-__device__ __forceinline__ void copy_bytes_al(uint8_t* dst, const uint32_t* src32, uint32_t n)
-{
-    // 64 source bytes per round as four independent 16-byte loads (a dependent dword load per
-    // step serialised the loop on memory latency); the destination gets aligned dwords built with
-    // alignbyte, its partial first and last dwords byte by byte
-    const uint32_t a = (uint32_t) ((uintptr_t) dst & 3u), h = (4u - a) & 3u;  // h: bytes before the first aligned dword
-    const uint4*   s4 = reinterpret_cast<const uint4*>(src32);
-    uint32_t       carry = 0;  // source dword just below the current round (for alignbyte)
-    for (uint32_t r0 = 0; r0 < n; r0 += 64)
-    {
-        uint32_t w[17];
-        w[0] = carry;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-        {
-            const uint4 v = s4[(r0 >> 4) + k];
-            w[1 + 4 * k] = v.x, w[2 + 4 * k] = v.y, w[3 + 4 * k] = v.z, w[4 + 4 * k] = v.w;
-        }
-        carry = w[16];
-        // output byte i (0 <= i < n) = source byte i; aligned destination dwords start at i = h + 4 m
-#pragma unroll
-        for (int m = 0; m < 16; ++m)
-        {
-            // destination dword at offset lo = r0 + 4 (m - 1) + h (h > 0: source dwords w[m], w[m + 1],
-            // shifted by h bytes) or r0 + 4 m (h == 0: source dword w[m + 1])
-            const uint32_t i = r0 + (uint32_t) m * 4;
-            const int32_t  lo = h ? (int32_t) (i + h) - 4 : (int32_t) i;
-            const uint32_t v  = h ? __builtin_amdgcn_alignbyte(w[m + 1], w[m], h) : w[m + 1];
-            if (lo >= 0 && (uint32_t) lo + 4 <= n)
-                *reinterpret_cast<uint32_t*>(dst + lo) = v;
-            else
-                for (int t = 0; t < 4; ++t)
-                    if (lo + t >= 0 && (uint32_t) (lo + t) < n)
-                        dst[lo + t] = (uint8_t) (v >> (8 * t));
-        }
-        if (h)
-        {
-            // the destination dword [r0 + 64 + h - 4, r0 + 64 + h) needs the next round's first
-            // source dword: it is written there (as m = 0 of the next round) or, past the end,
-            // its bytes below n are written here
-            const uint32_t lo = r0 + 64 + h - 4;
-            if (r0 + 64 >= n)
-                for (uint32_t t = 0; t < 4; ++t)
-                    if (lo + t < n)
-                        dst[lo + t] = (uint8_t) (w[16] >> (8 * (h + t)));
-        }
-    }
-}
+// Sixteen lanes per hop, four hops per wave: lane l copies source dwords l, l + 16, ... of its
+// hop's slot to the output with unaligned dword stores, so one store instruction writes four
+// contiguous 64-byte stretches (k_ib_copy4's lane-per-hop stores touched 64 lines per instruction,
+// 4 bytes each: bound by the L2 request rate, not by bytes).  The hop's last partial dword goes byte
+// by byte (the next hop owns the bytes after it).
+typedef uint32_t __attribute__((aligned(1))) u32_u;
+typedef uint4 __attribute__((aligned(1))) u128_u;
 
-__global__ void __launch_bounds__(256) k_ib_copy4(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ cum, const uint32_t* __restrict__ cnt,
-                                                  const uint32_t* __restrict__ order, uint32_t nblocks,
-                                                  const uint32_t* __restrict__ start, const uint32_t* __restrict__ hop_len,
-                                                  const uint32_t* __restrict__ hop_ovf, const uint32_t* __restrict__ ovl_next,
-                                                  const uint8_t* __restrict__ slots, const uint8_t* __restrict__ pool, uint32_t pool_cap,
-                                                  uint8_t* __restrict__ out)
+__global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ cum, const uint32_t* __restrict__ cnt,
+                                                   const uint32_t* __restrict__ order, uint32_t nblocks,
+                                                   const uint32_t* __restrict__ start, const uint32_t* __restrict__ hop_len,
+                                                   const uint32_t* __restrict__ hop_ovf, const uint32_t* __restrict__ ovl_next,
+                                                   const uint8_t* __restrict__ slots, const uint8_t* __restrict__ pool, uint32_t pool_cap,
+                                                   uint8_t* __restrict__ out)
 {
+    const uint32_t l = (uint32_t) lane_id() & 15u;
     for (uint32_t b = blockIdx.y; b < nblocks; b += gridDim.y)
     {
         const IbBlk    B    = blk[b];
         const uint32_t base = cum[b], nn = cum[b + 1] - base, cap = 4u << B.shift;
         uint8_t*       ob   = out + B.off;
-        const uint32_t nc = cnt[b];
-        for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nc && r < nn; r += gridDim.x * blockDim.x)
+        const uint32_t nh   = min(cnt[b], nn);
+        for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; r < nh; r += (gridDim.x * blockDim.x) >> 4)
         {
-            // hops in output order: neighbouring lanes write neighbouring output ranges (whole
-            // lines per store instruction; in splitter order every 64-byte hop landed at a random
-            // place and its partial lines cost a read-modify-write each)
             const uint32_t q  = order[base + r];
             const uint32_t st = start[base + q];
             if (st == 0xFFFFFFFFu || st >= B.len)
                 continue;
-            const uint32_t len = min(hop_len[base + q], B.len - st);
-            copy_bytes_al(ob + st, reinterpret_cast<const uint32_t*>(slots + B.tslot + (size_t) q * cap), min(len, cap));
+            const uint32_t  len = min(hop_len[base + q], B.len - st);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(slots + B.tslot + (size_t) q * cap);
+            const uint32_t  m   = min(len, cap);
+            uint8_t*        dst = ob + st;
+            for (uint32_t o = 4 * l; o < m; o += 64)
+            {
+                const uint32_t v = src[o >> 2];
+                if (o + 4 <= m)
+                    *reinterpret_cast<u32_u*>(dst + o) = v;
+                else
+                    for (uint32_t t = 0; o + t < m; ++t)
+                        dst[o + t] = (uint8_t) (v >> (8 * t));
+            }
             uint32_t c = len > cap ? hop_ovf[base + q] : 0xFFFFFFFFu;
             for (uint32_t o0 = cap; o0 < len && c < pool_cap; o0 += IB_CHUNK)
             {
                 const uint8_t* cs = pool + (size_t) c * IB_CHUNK;
-                const uint32_t m  = min(IB_CHUNK, len - o0);
-                for (uint32_t j = 0; j < m; ++j)
-                    ob[st + o0 + j] = cs[j];
+                const uint32_t mm = min(IB_CHUNK, len - o0);
+                for (uint32_t o = 16 * l; o < mm; o += 256)
+                {
+                    const uint4 v = *reinterpret_cast<const uint4*>(cs + o);
+                    if (o + 16 <= mm)
+                        *reinterpret_cast<u128_u*>(dst + o0 + o) = v;
+                    else
+                    {
+                        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                        for (uint32_t t = 0; o + t < mm; ++t)
+                            dst[o0 + o + t] = (uint8_t) (w[t >> 2] >> (8 * (t & 3)));
+                    }
+                }
                 c = ovl_next[c];
             }
         }
@@ -930,8 +904,8 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
     }
     hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
                        w.m_len, w.m_start, w.cyc, w.m_order, w.m_cnt);
-    hipLaunchKernelGGL(k_ib_copy4, dim3(16, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, blk, w.cum, w.m_cnt, w.m_order, nblocks, w.m_start, w.m_len,
-                       w.m_ovf, w.ovl_next, w.slot, w.pool, w.pool_cap, d_out);
+    hipLaunchKernelGGL(k_ib_copy16, dim3(64, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, blk, w.cum, w.m_cnt, w.m_order, nblocks, w.m_start,
+                       w.m_len, w.m_ovf, w.ovl_next, w.slot, w.pool, w.pool_cap, d_out);
     hipLaunchKernelGGL(k_ib_repeat, dim3(64, std::min<uint32_t>(nblocks, 65535)), dim3(256), 0, s, d_blocks, nblocks, w.cyc, d_out);
     BRA_HIP_CHECK(hipGetLastError());
     // overflow pool exhausted (hops far longer than 4 S, e.g. adversarial inputs): redo the batch
