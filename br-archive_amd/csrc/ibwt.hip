@@ -669,9 +669,9 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
 
 // Sixteen lanes per hop, four hops per wave: lane l copies source dwords l, l + 16, ... of its
 // hop's slot to the output with unaligned dword stores, so one store instruction writes four
-// contiguous 64-byte stretches (k_ib_copy4's lane-per-hop stores touched 64 lines per instruction,
-// 4 bytes each: bound by the L2 request rate, not by bytes).  The hop's last partial dword goes byte
-// by byte (the next hop owns the bytes after it).
+// contiguous 64-byte stretches (the round-4 lane-per-hop copy stored 4 bytes to each of 64 lines per
+// instruction: bound by the L2 request rate, not by bytes; iBWT 4.86 -> 4.72 ms on 256 x 1 MiB
+// text).  The hop's last partial dword goes byte by byte (the next hop owns the bytes after it).
 typedef uint32_t __attribute__((aligned(1))) u32_u;
 typedef uint4 __attribute__((aligned(1))) u128_u;
 
