@@ -6,7 +6,7 @@
 //
 // The pointer chase is split with splitters: every S-th transform index plus the primary index.
 // Main path (blocks < 2^24 bytes):
-//   k_ib_hist / k_ib_scan / k_ib_scatter2  TL[k] = transform[k] | L[transform[k]] << 24, so one
+//   k_ib_hist / k_ib_scan / k_ib_scatter2 + 3  TL[k] = transform[k] | L[transform[k]] << 24, so one
 //        4-byte load per step gives both the next index and the output byte;
 //   k_ib_walk3   persistent waves claim splitters from per-XCD queues (each XCD works through its
 //        own range of blocks, so the random loads of an XCD stay in few blocks' TL); a lane walks
@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t split_step(uint32_t n)
 
 // per tile byte histogram of L
 __global__ void __launch_bounds__(TPB) k_ib_hist(const uint8_t* __restrict__ L, const Piece* __restrict__ tiles, uint32_t ntiles,
-                                                 uint32_t* __restrict__ th)
+                                                 uint32_t* __restrict__ th, uint8_t* __restrict__ runny)
 {
     // 16 consecutive bytes per thread, one LDS atomic per run of equal bytes (BWT output is
     // run-heavy: one atomic per byte made the lanes of a run serialise on one counter), 4 counter
@@ -100,7 +100,13 @@ __global__ void __launch_bounds__(TPB) k_ib_hist(const uint8_t* __restrict__ L, 
             atomicAdd(&h[cp + prev], run);
         }
         __syncthreads();
-        th[(size_t) t * 256 + threadIdx.x] = h[threadIdx.x] + h[HS + threadIdx.x] + h[2 * HS + threadIdx.x] + h[3 * HS + threadIdx.x];
+        const uint32_t hv = h[threadIdx.x] + h[HS + threadIdx.x] + h[2 * HS + threadIdx.x] + h[3 * HS + threadIdx.x];
+        th[(size_t) t * 256 + threadIdx.x] = hv;
+        // k_ib_scatter2's tiles: few distinct bytes (a 64-position round then stores to few runs of
+        // destinations: text, 16-symbol data); k_ib_scatter3's: many (uniform random data)
+        const int distinct = __syncthreads_count(hv != 0);
+        if (threadIdx.x == 0)
+            runny[t] = distinct <= 48 ? 1 : 0;
         __syncthreads();
     }
 }
@@ -349,7 +355,7 @@ __global__ void k_ib_repeat(const BlockDesc* __restrict__ blocks, uint32_t nbloc
 // stable scatter of (index | byte << 24): as k_ib_scatter, packed
 __global__ void __launch_bounds__(64) k_ib_scatter2(const uint8_t* __restrict__ L, const Piece* __restrict__ tiles, uint32_t ntiles,
                                                     const uint32_t* __restrict__ th, const BlockDesc* __restrict__ blocks,
-                                                    uint32_t* __restrict__ TL)
+                                                    uint32_t* __restrict__ TL, const uint8_t* __restrict__ runny)
 {
     __shared__ uint32_t cnt[256];
     __shared__ uint4    tb4[ITILE / 16];  // the tile's bytes, loaded once (a byte load per step was a global round trip per 64 positions)
@@ -357,6 +363,8 @@ __global__ void __launch_bounds__(64) k_ib_scatter2(const uint8_t* __restrict__ 
     const int           lane = lane_id();
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {
+        if (!runny[t])
+            continue;  // k_ib_scatter3's tile
         const Piece P = tiles[t];
         for (int i = lane; i < 256; i += 64)
             cnt[i] = th[(size_t) t * 256 + i];
@@ -399,6 +407,110 @@ __global__ void __launch_bounds__(64) k_ib_scatter2(const uint8_t* __restrict__ 
             }
             __syncthreads();
         }
+    }
+}
+
+// The same stable scatter staged through LDS: four waves per tile, wave w ranks positions
+// [1024 w, 1024 w + 1024) among equal bytes (ballot match per 64 positions, a running count per
+// byte and wave), the tile's entries are placed in LDS in their sorted order with their
+// destinations beside them, and thread j stores the j-th of them: the stores of a workgroup run
+// along the byte runs of the destination (k_ib_scatter2's store instructions hit up to 64
+// destinations each).  For tiles of many distinct bytes (uniform random data); a tile of few
+// distinct bytes (text, 16-symbol data: k_ib_hist's flag) stores to few runs of destinations per
+// instruction already and stays with k_ib_scatter2, which is cheaper for it.
+constexpr uint32_t IBS_WAVES = 4;
+__global__ void __launch_bounds__(64 * IBS_WAVES) k_ib_scatter3(const uint8_t* __restrict__ L, const Piece* __restrict__ tiles, uint32_t ntiles,
+                                                               const uint32_t* __restrict__ th, const BlockDesc* __restrict__ blocks,
+                                                               uint32_t* __restrict__ TL, const uint8_t* __restrict__ runny)
+{
+    constexpr uint32_t PER = ITILE / IBS_WAVES;  // positions per wave
+    __shared__ uint4    tb4[ITILE / 16];
+    __shared__ uint32_t wrun[IBS_WAVES][256];    // per wave and byte: count (then: offset among the tile's equal bytes)
+    __shared__ uint32_t lstart[256];             // first sorted position of each byte in the tile
+    __shared__ uint32_t gbase[256];              // block-local TL position of the tile's first entry of each byte
+    __shared__ uint16_t rk[ITILE];               // rank among equal bytes before it in the wave's part
+    __shared__ uint32_t sval[ITILE], sdst[ITILE];
+    __shared__ uint32_t tmp[8];
+    const uint8_t* tb   = reinterpret_cast<const uint8_t*>(tb4);
+    const uint32_t lane = (uint32_t) lane_id(), w = threadIdx.x >> 6;
+    const uint64_t lt   = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+    {
+        if (runny[t])
+            continue;  // k_ib_scatter2's tile
+        const Piece P = tiles[t];
+        gbase[threadIdx.x] = th[(size_t) t * 256 + threadIdx.x];
+#pragma unroll
+        for (uint32_t v = 0; v < IBS_WAVES; ++v)
+            wrun[v][threadIdx.x] = 0;
+        const uint8_t* src = L + P.off;
+        if (P.len == ITILE && (((uintptr_t) src) & 15) == 0)
+            tb4[threadIdx.x] = reinterpret_cast<const uint4*>(src)[threadIdx.x];
+        else
+            for (uint32_t i = threadIdx.x; i < P.len; i += 64 * IBS_WAVES)
+                reinterpret_cast<uint8_t*>(tb4)[i] = src[i];
+        __syncthreads();
+        // ranks inside the wave's part, counts per byte
+        for (uint32_t r = 0; r < PER / 64; ++r)
+        {
+            const uint32_t i     = w * PER + r * 64 + lane;
+            const bool     valid = i < P.len;
+            const uint32_t c     = valid ? tb[i] : 0u;
+            uint64_t       m     = __ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit)
+            {
+                const uint64_t bb = __ballot(valid && ((c >> bit) & 1));
+                m &= ((c >> bit) & 1) ? bb : ~bb;
+            }
+            const uint32_t rank = (uint32_t) __popcll(m & lt), tot = (uint32_t) __popcll(m);
+            uint32_t       before = 0;
+            if (valid)
+                before = wrun[w][c];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (valid)
+            {
+                rk[i] = (uint16_t) (before + rank);
+                if (rank == tot - 1)
+                    wrun[w][c] = before + tot;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        __syncthreads();
+        // per byte (thread c): the waves' offsets among the tile's equal bytes, the tile total and
+        // the byte's first sorted position in the tile
+        {
+            const uint32_t c   = threadIdx.x;
+            uint32_t       run = 0;
+#pragma unroll
+            for (uint32_t v = 0; v < IBS_WAVES; ++v)
+            {
+                const uint32_t n = wrun[v][c];
+                wrun[v][c]       = run;
+                run += n;
+            }
+            lstart[c] = block256_exclusive_sum(run, tmp);
+        }
+        __syncthreads();
+        for (uint32_t r = 0; r < PER / 64; ++r)
+        {
+            const uint32_t i = w * PER + r * 64 + lane;
+            if (i < P.len)
+            {
+                const uint32_t c = tb[i], k = wrun[w][c] + rk[i];
+                sval[lstart[c] + k] = (P.start + i) | (c << 24);
+                sdst[lstart[c] + k] = gbase[c] + k;
+            }
+        }
+        __syncthreads();
+        uint32_t* tl = TL + blocks[P.block].off;
+        for (uint32_t j = threadIdx.x; j < P.len; j += 64 * IBS_WAVES)
+            tl[sdst[j]] = sval[j];
+        __syncthreads();
     }
 }
 
@@ -747,7 +859,7 @@ bool IbwtWorkspace::reserve(uint64_t n, uint32_t nblocks, uint32_t ntiles)
     {
         cap_t            = 0;
         const uint32_t c = ntiles + ntiles / 4 + 64;
-        if (!dev_alloc(th, (uint64_t) c * 256))
+        if (!dev_alloc(th, (uint64_t) c * 256 + c / 4 + 1))  // + one byte per tile (k_ib_hist's run flag)
             return false;
         cap_t = c;
     }
@@ -842,7 +954,8 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
     const uint32_t nt = w.tiling.n;
     if (!w.reserve(N, nblocks, nt))
         return false;
-    hipLaunchKernelGGL(k_ib_hist, dim3(std::min<uint32_t>(nt, 8192)), dim3(TPB), 0, s, d_L, w.tiling.d_pieces, nt, w.th);
+    uint8_t* runny = reinterpret_cast<uint8_t*>(w.th + (size_t) w.cap_t * 256);  // per tile: k_ib_scatter2 (1) or k_ib_scatter3 (0)
+    hipLaunchKernelGGL(k_ib_hist, dim3(std::min<uint32_t>(nt, 8192)), dim3(TPB), 0, s, d_L, w.tiling.d_pieces, nt, w.th, runny);
     hipLaunchKernelGGL(k_ib_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, w.th);
     if (!main_path)
         return ibwt_two_walk(w, d_L, d_pi, d_blocks, nblocks, d_out, s);
@@ -889,7 +1002,11 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
     // ctl[0..255]: 8 claim counters (32-word stride), ctl[256..264]: XCD block ranges, ctl[300]: pool counter
     BRA_HIP_CHECK(hipMemsetAsync(w.ctl, 0, 256 * 4, s));
     BRA_HIP_CHECK(hipMemsetAsync(w.ctl + 300, 0, 4, s));
-    hipLaunchKernelGGL(k_ib_scatter2, dim3(std::min<uint32_t>(nt, 16384)), dim3(64), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks, w.T);
+    hipLaunchKernelGGL(k_ib_scatter2, dim3(std::min<uint32_t>(nt, 16384)), dim3(64), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks, w.T, runny);
+    // (about the resident capacity: 50 KiB of LDS per workgroup, 3 per CU; on text every tile is
+    // k_ib_scatter2's and this launch only reads the flags)
+    hipLaunchKernelGGL(k_ib_scatter3, dim3(std::min<uint32_t>(nt, 1024)), dim3(64 * IBS_WAVES), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks,
+                       w.T, runny);
     WalkArgs a{blk, d_pi, w.cum, w.ctl + 256, w.ctl, w.T, w.slot, w.pool, w.ctl + 300, w.pool_cap, w.ovl_next, w.m_next, w.m_len, w.m_ovf};
     {
         BRA_PROF(P_DEC_IB_WALK, s);

@@ -1192,7 +1192,27 @@ __global__ void __launch_bounds__(TPB) k_mtf_dec_relabel(const uint8_t* __restri
             reinterpret_cast<uint32_t*>(S)[threadIdx.x] = perm[(size_t) s * 64 + threadIdx.x];
         __syncthreads();
         const Piece P = segs[s];
-        for (uint32_t i = threadIdx.x; i < P.len; i += TPB)
+        // 8 bytes per thread and round where the segment is 8-aligned (MTF_SEG = 2048 = 256 x 8:
+        // one round; a byte per thread cost an instruction per byte)
+        uint32_t done = 0;
+        if ((P.off & 7u) == 0)
+        {
+            done = P.len & ~7u;
+            for (uint32_t i = threadIdx.x * 8; i < done; i += TPB * 8)
+            {
+                const uint2 v = *reinterpret_cast<const uint2*>(lab + P.off + i);
+                uint32_t    o[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                {
+                    const uint32_t x = h ? v.y : v.x;
+                    o[h] = (uint32_t) S[x & 0xFFu] | ((uint32_t) S[(x >> 8) & 0xFFu] << 8) | ((uint32_t) S[(x >> 16) & 0xFFu] << 16) |
+                           ((uint32_t) S[x >> 24] << 24);
+                }
+                *reinterpret_cast<uint2*>(out + P.off + i) = make_uint2(o[0], o[1]);
+            }
+        }
+        for (uint32_t i = done + threadIdx.x; i < P.len; i += TPB)
             out[P.off + i] = S[lab[P.off + i]];
         __syncthreads();
     }
