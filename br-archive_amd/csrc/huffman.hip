@@ -1416,25 +1416,26 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_write2(const HuffMetaRec* __rest
         uint32_t       p      = j * HD2_SEG + e, len = 0, sym = 0;
         W.init(p);
         uint8_t* dst = out + out_base[b] + off;
-        // bytes until dst is dword aligned, then whole dwords, then the rest
+        // bytes until dst is 16-byte aligned, then 16 bytes per store (a lane writes its own
+        // range: dword stores cost a request per 4 bytes), then the rest
         uint32_t i = 0;
-        for (; i < n && (((uintptr_t) (dst + i)) & 3); ++i)
+        for (; i < n && (((uintptr_t) (dst + i)) & 15); ++i)
         {
             (void) hd2_dec(L, W.peek(p), len, sym);
             p += len;
             dst[i] = (uint8_t) sym;
         }
-        for (; i + 4 <= n; i += 4)
+        for (; i + 16 <= n; i += 16)
         {
-            uint32_t wv = 0;
+            uint32_t wv[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
+            for (int k = 0; k < 16; ++k)
             {
                 (void) hd2_dec(L, W.peek(p), len, sym);
                 p += len;
-                wv |= sym << (8 * k);
+                wv[k >> 2] |= sym << (8 * (k & 3));
             }
-            *reinterpret_cast<uint32_t*>(dst + i) = wv;
+            *reinterpret_cast<uint4*>(dst + i) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
         }
         for (; i < n; ++i)
         {

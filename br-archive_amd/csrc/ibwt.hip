@@ -794,50 +794,65 @@ __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk
                                                    const uint8_t* __restrict__ slots, const uint8_t* __restrict__ pool, uint32_t pool_cap,
                                                    uint8_t* __restrict__ out)
 {
-    const uint32_t l = (uint32_t) lane_id() & 15u;
+    const uint32_t lane = (uint32_t) lane_id(), l = lane & 15u, g0 = lane & ~15u;  // g0: the group's first lane
     for (uint32_t b = blockIdx.y; b < nblocks; b += gridDim.y)
     {
         const IbBlk    B    = blk[b];
         const uint32_t base = cum[b], nn = cum[b + 1] - base, cap = 4u << B.shift;
         uint8_t*       ob   = out + B.off;
         const uint32_t nh   = min(cnt[b], nn);
-        for (uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; r < nh; r += (gridDim.x * blockDim.x) >> 4)
+        // a group takes 16 consecutive hops in output order at a time: lane l loads hop l's record
+        // (two dependent round trips for 16 hops, not per hop), then the group copies the 16 hops
+        // one after the other (they are adjacent in the output)
+        for (uint32_t r0 = ((blockIdx.x * blockDim.x + threadIdx.x) >> 4) * 16; r0 < nh; r0 += ((gridDim.x * blockDim.x) >> 4) * 16)
         {
-            const uint32_t q  = order[base + r];
-            const uint32_t st = start[base + q];
-            if (st == 0xFFFFFFFFu || st >= B.len)
-                continue;
-            const uint32_t  len = min(hop_len[base + q], B.len - st);
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(slots + B.tslot + (size_t) q * cap);
-            const uint32_t  m   = min(len, cap);
-            uint8_t*        dst = ob + st;
-            for (uint32_t o = 4 * l; o < m; o += 64)
+            const uint32_t r   = r0 + l;
+            uint32_t       q   = 0, st = 0xFFFFFFFFu, len = 0;
+            if (r < nh)
             {
-                const uint32_t v = src[o >> 2];
-                if (o + 4 <= m)
-                    *reinterpret_cast<u32_u*>(dst + o) = v;
-                else
-                    for (uint32_t t = 0; o + t < m; ++t)
-                        dst[o + t] = (uint8_t) (v >> (8 * t));
+                q  = order[base + r];
+                st = start[base + q];
+                if (st < B.len)
+                    len = min(hop_len[base + q], B.len - st);
             }
-            uint32_t c = len > cap ? hop_ovf[base + q] : 0xFFFFFFFFu;
-            for (uint32_t o0 = cap; o0 < len && c < pool_cap; o0 += IB_CHUNK)
+            for (uint32_t h = 0; h < 16; ++h)
             {
-                const uint8_t* cs = pool + (size_t) c * IB_CHUNK;
-                const uint32_t mm = min(IB_CHUNK, len - o0);
-                for (uint32_t o = 16 * l; o < mm; o += 256)
+                const uint32_t hq = (uint32_t) __shfl((int) q, (int) (g0 + h), 64);
+                const uint32_t hs = (uint32_t) __shfl((int) st, (int) (g0 + h), 64);
+                const uint32_t hl = (uint32_t) __shfl((int) len, (int) (g0 + h), 64);
+                if (hs == 0xFFFFFFFFu || hs >= B.len || hl == 0)
+                    continue;
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(slots + B.tslot + (size_t) hq * cap);
+                const uint32_t  m   = min(hl, cap);
+                uint8_t*        dst = ob + hs;
+                for (uint32_t o = 4 * l; o < m; o += 64)
                 {
-                    const uint4 v = *reinterpret_cast<const uint4*>(cs + o);
-                    if (o + 16 <= mm)
-                        *reinterpret_cast<u128_u*>(dst + o0 + o) = v;
+                    const uint32_t v = src[o >> 2];
+                    if (o + 4 <= m)
+                        *reinterpret_cast<u32_u*>(dst + o) = v;
                     else
-                    {
-                        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-                        for (uint32_t t = 0; o + t < mm; ++t)
-                            dst[o0 + o + t] = (uint8_t) (w[t >> 2] >> (8 * (t & 3)));
-                    }
+                        for (uint32_t t = 0; o + t < m; ++t)
+                            dst[o + t] = (uint8_t) (v >> (8 * t));
                 }
-                c = ovl_next[c];
+                uint32_t c = hl > cap ? hop_ovf[base + hq] : 0xFFFFFFFFu;
+                for (uint32_t o0 = cap; o0 < hl && c < pool_cap; o0 += IB_CHUNK)
+                {
+                    const uint8_t* cs = pool + (size_t) c * IB_CHUNK;
+                    const uint32_t mm = min(IB_CHUNK, hl - o0);
+                    for (uint32_t o = 16 * l; o < mm; o += 256)
+                    {
+                        const uint4 v = *reinterpret_cast<const uint4*>(cs + o);
+                        if (o + 16 <= mm)
+                            *reinterpret_cast<u128_u*>(dst + o0 + o) = v;
+                        else
+                        {
+                            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                            for (uint32_t t = 0; o + t < mm; ++t)
+                                dst[o0 + o + t] = (uint8_t) (w[t >> 2] >> (8 * (t & 3)));
+                        }
+                    }
+                    c = ovl_next[c];
+                }
             }
         }
     }
