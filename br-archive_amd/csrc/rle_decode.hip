@@ -41,6 +41,7 @@ constexpr uint32_t RD_WIN   = RD_WAVES * RD_SUB;    // 16 KiB window
 constexpr uint32_t RD_HALO  = 256;                  // a literal's payload runs up to 128 bytes past its window
 constexpr uint32_t RD_LOAD  = (RD_WIN + RD_HALO) / 16;  // 16-byte loads per window (<= 2 per thread)
 constexpr uint32_t RD_NENT  = 129;                  // entry offsets into a segment: [0, 128]
+typedef uint4 __attribute__((aligned(1))) u128_u;
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -339,14 +340,8 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                     }
                     const uint64_t a = (uint64_t) ob0 + o0;  // block output offset
                     uint8_t*       q = dst + a;
-                    if (nb == 16 && a + 16 <= cap && (((uintptr_t) q) & 15) == 0)
-                        *reinterpret_cast<uint4*>(q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-                    else if (nb == 16 && a + 16 <= cap && (((uintptr_t) q) & 3) == 0)
-                    {
-#pragma unroll
-                        for (int h = 0; h < 4; ++h)
-                            reinterpret_cast<uint32_t*>(q)[h] = wv[h];
-                    }
+                    if (nb == 16 && a + 16 <= cap)  // one (unaligned) 16-byte store: the output offsets have any alignment
+                        *reinterpret_cast<u128_u*>(q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
                     else
                         for (uint32_t j = 0; j < nb; ++j)
                             if (a + j < cap)
