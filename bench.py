@@ -341,6 +341,27 @@ def pcie_inclusive(codec, data_np, d, bs, nb, hdr, off, pay, payload_bytes, work
     return res
 
 
+def copy_peak_GBps(dev, nbytes=512 << 20, reps=10):
+    """A measured device copy-kernel peak (SURVEY 8.1 row d: report the fraction of it beside the
+    spec peak): torch's copy kernel over nbytes, read + write bytes per second, HIP events."""
+    import torch
+
+    a = torch.empty((nbytes,), dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbps
+
+
 def pcie_stream(bra, codec, data_np, kind, bs, nstream):
     """Transfer-inclusive encode of a stream of host batches (SURVEY 8.1(d) secondary; the front
     end's loop): `nstream` batches of the configs[1] size go host -> HBM -> chunk records -> host
@@ -663,6 +684,11 @@ def main():
         if args.profile_all:
             line["kernels"] = {k: {"ms": round(v[0] / max(1, v[1]), 4), "launches": v[1], "GBps": round(v[2] / max(v[0], 1e-9) / 1e6, 1)}
                                for k, v in prof.items() if v[1]}
+        if world == 1:
+            cp = copy_peak_GBps(dev)
+            line["roofline"]["measured_copy_peak"] = round(cp, 1)
+            line["roofline"]["frac_of_copy_peak"] = round(line["roofline"]["achieved"] / cp, 4)
+            line["pipeline"]["frac_of_copy_peak"] = round(pipeline_alg / (ms_per_step / 1e3) / (cp * 1e9), 4)
         # traffic: HBM bytes per launch of the same kernel slot on the same workload (input kind and
         # block size) from the committed rocprofv3 PMC passes (profiles/pmc_summary.json)
         pmc = os.path.join(ROOT, "profiles", "pmc_summary.json")
