@@ -18,13 +18,15 @@
 //                 of the output (the Huffman frequencies, bra_huffman.c:368-370)
 #include "rle.h"
 #include "prof.h"
+#include "rle_tile.h"
 
 namespace bra {
 
 namespace {
 
+using namespace rle_tile;  // per-thread classification and output (PT positions per thread)
 constexpr int TPB = 256;
-constexpr int PT  = RLE_TILE / TPB;  // 16 bytes per thread
+static_assert(RLE_TILE == TPB * PT, "one tile per workgroup, PT positions per thread");
 
 struct TileRun
 {
@@ -131,26 +133,6 @@ __device__ __forceinline__ uint32_t block_sum_excl1(uint32_t v, uint32_t* tmp, u
     return pre + x - v;
 }
 
-__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[4], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
-
-// Bit i set iff byte i differs from byte i-1 (bit 0: from `prev`), for the PT bytes of w.
-__device__ __forceinline__ uint32_t diff_mask(const uint32_t (&w)[4], uint32_t prev)
-{
-    uint32_t m = 0, carry = prev & 0xFFu;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-    {
-        const uint32_t z  = w[d] ^ ((w[d] << 8) | carry);          // byte j: x[j] ^ x[j-1]
-        const uint32_t nz = (((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;  // bit 7 of byte j: nonzero
-        m |= ((((nz >> 7) * 0x01020408u) >> 24) & 0xFu) << (4 * d);
-        carry = w[d] >> 24;
-    }
-    return m;
-}
-
-__device__ __forceinline__ uint32_t hi_bit(uint32_t m) { return 31u - (uint32_t) __builtin_clz(m); }  // m != 0
-__device__ __forceinline__ uint32_t lo_bit(uint32_t m) { return (uint32_t) __builtin_ctz(m); }        // m != 0
-
 // One tile as the workgroup sees it: thread t holds positions [16t, 16t + nt) of the tile.
 struct TileThread
 {
@@ -190,90 +172,13 @@ __device__ __forceinline__ void tile_load(const uint8_t* __restrict__ in, const 
     T.bm = T.nt ? bm & ((1u << T.nt) - 1u) : 0u;
 }
 
-// Classify the thread's positions: nl = non-literal (covered by run blocks), rs = run-block
-// starts, clen[i] = block length at a run-block start.  left / right: run extension into the tile
-// from before / after it (TileLink).
-__device__ __forceinline__ void tile_runs(const TileThread& T, uint32_t left, uint32_t right, uint32_t* tmp, uint32_t& nl, uint32_t& rs,
-                                          uint32_t (&clen)[PT])
+// Run classification of the thread's positions (rle_tile.h) from the boundary scans.
+__device__ __forceinline__ RunCls tile_cls(const TileThread& T, uint32_t left, uint32_t right, uint32_t* tmp)
 {
-    const uint32_t lastB  = T.bm ? T.base + hi_bit(T.bm) : 0u;
-    const uint32_t firstB = T.bm ? T.base + lo_bit(T.bm) : T.n;
-    uint32_t       Sprev, Enext, u0, u1;
-    block_scan_pair<true, false>(lastB, 0u, 0u, OpMax(), Sprev, u0, firstB, T.n, T.n, OpMin(), Enext, u1, tmp);
-    nl = rs = 0;
-#pragma unroll
-    for (int i = 0; i < PT; ++i)
-    {
-        clen[i] = 0;
-        if ((uint32_t) i >= T.nt)
-            continue;
-        const uint32_t p  = T.base + i;
-        const uint32_t sm = T.bm & ((2u << i) - 1u);
-        const uint32_t em = T.bm & ~((2u << i) - 1u);
-        const uint32_t S  = sm ? T.base + hi_bit(sm) : Sprev;
-        const uint32_t E  = em ? T.base + lo_bit(em) : Enext;
-        const uint32_t k  = p - S + (S == 0 ? left : 0u);       // position inside the maximal run
-        const uint32_t r  = E - p + (E == T.n ? right : 0u);    // positions from p to the run end
-        const uint32_t L  = k + r, tail = L & 127u;
-        const uint32_t cut = tail < 3 ? tail : 0u;              // 1 or 2 tail bytes become literals
-        if (L >= 3 && k < L - cut)
-        {
-            nl |= 1u << i;
-            if ((k & 127u) == 0)
-            {
-                rs |= 1u << i;
-                clen[i] = min(128u, L - k);
-            }
-        }
-    }
-}
-
-// Output bytes of the thread's positions; with WRITE, also stages them at stage[pos...].
-// g_in: gap offset of the tile's first position if the gap comes from before the tile;
-// rem_after: literals following the tile in its trailing gap.
-template <bool WRITE>
-__device__ __forceinline__ uint32_t tile_emit(const TileThread& T, uint32_t nl, uint32_t rs, const uint32_t (&clen)[PT], uint32_t GSprev,
-                                              uint32_t GEnext, uint32_t g_in, uint32_t rem_after, uint8_t* stage, uint32_t pos)
-{
-    uint32_t bytes = 0;
-#pragma unroll
-    for (int i = 0; i < PT; ++i)
-    {
-        if ((uint32_t) i >= T.nt)
-            continue;
-        const uint32_t p = T.base + i;
-        const uint32_t x = byte_at(T.w, i);
-        if (nl & (1u << i))
-        {
-            if (rs & (1u << i))
-            {
-                if (WRITE)
-                {
-                    stage[pos + bytes]     = (uint8_t) (int8_t) (1 - (int) clen[i]);
-                    stage[pos + bytes + 1] = (uint8_t) x;
-                }
-                bytes += 2;
-            }
-            continue;
-        }
-        const uint32_t gm  = nl & ((1u << i) - 1u);
-        const uint32_t GS  = gm ? T.base + hi_bit(gm) + 1 : GSprev;   // start of the literal gap
-        const uint32_t go  = p - GS + (GS == 0 ? g_in : 0u);
-        const bool     ctl = (go & 127u) == 0;
-        if (WRITE)
-        {
-            if (ctl)
-            {
-                const uint32_t em  = nl & ~((2u << i) - 1u);
-                const uint32_t GE  = em ? T.base + lo_bit(em) : GEnext;  // end of the literal gap
-                const uint32_t rem = GE - p + (GE == T.n ? rem_after : 0u);
-                stage[pos + bytes] = (uint8_t) (min(rem, 128u) - 1);
-            }
-            stage[pos + bytes + (ctl ? 1 : 0)] = (uint8_t) x;
-        }
-        bytes += ctl ? 2 : 1;
-    }
-    return bytes;
+    uint32_t Sprev, Enext, u0, u1;
+    block_scan_pair<true, false>(T.bm ? T.base + hi_bit(T.bm) : 0u, 0u, 0u, OpMax(), Sprev, u0, T.bm ? T.base + lo_bit(T.bm) : T.n, T.n, T.n,
+                                 OpMin(), Enext, u1, tmp);
+    return cls_thread(T.bm, T.nt, T.base, T.n, Sprev, Enext, left, right);
 }
 
 // Tile run summary: leading / trailing run length, first / last byte, all one run.
@@ -408,12 +313,12 @@ __global__ void __launch_bounds__(TPB) k_rle_sizes(const uint8_t* __restrict__ i
         const TileLink K = link[t];
         TileThread     T;
         tile_load(in, P, T);
-        uint32_t nl, rs, clen[PT];
-        tile_runs(T, K.left, K.right, tmp[0], nl, rs, clen);
+        const RunCls C = tile_cls(T, K.left, K.right, tmp[0]);
+        const uint32_t nl = C.nl;
         uint32_t maxNL, minNL, GSprev, u0;
         block_scan_pair<true, true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), GSprev, maxNL, nl ? T.base + lo_bit(nl) : T.n, T.n, T.n,
                                     OpMin(), u0, minNL, tmp[1]);
-        const uint32_t bytes = tile_emit<false>(T, nl, rs, clen, GSprev, 0, 0, 0, nullptr, 0);
+        const uint32_t bytes = out_bytes(C, T.nt, T.base, GSprev, 0u);
         uint32_t       total;
         block_sum_excl1(bytes, tmp[2], total);
         if (threadIdx.x == 0)
@@ -489,7 +394,7 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
                                                    const uint64_t* __restrict__ rle_base, uint8_t* __restrict__ out,
                                                    uint32_t* __restrict__ hist)
 {
-    __shared__ uint32_t tmp[2][8];  // tile_runs' scan pair, then the two-barrier scans
+    __shared__ uint32_t tmp[2][8];  // tile_cls' scan pair, then the two-barrier scans
     __shared__ uint8_t  stage[RLE_TILE + RLE_TILE / 64 + 64];
     constexpr int       HC = 4, HS = 256 + 16;  // histogram copies (lane & 3), 16 banks apart: output bytes are skewed
     __shared__ uint32_t h[HC * HS];
@@ -504,14 +409,14 @@ __global__ void __launch_bounds__(TPB) k_rle_write(const uint8_t* __restrict__ i
             h[c * HS + threadIdx.x] = 0;
         TileThread T;
         tile_load(in, P, T);
-        uint32_t nl, rs, clen[PT];
-        tile_runs(T, K.left, K.right, tmp[0], nl, rs, clen);
+        const RunCls   C      = tile_cls(T, K.left, K.right, tmp[0]);
+        const uint32_t nl     = C.nl;
         const uint32_t GSprev = block_scan_excl<true>(nl ? T.base + hi_bit(nl) + 1 : 0u, 0u, 0u, OpMax(), tmp[1]);
         const uint32_t GEnext = block_scan_excl<false>(nl ? T.base + lo_bit(nl) : T.n, T.n, T.n, OpMin(), tmp[1]);
-        const uint32_t by     = tile_emit<false>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, nullptr, 0);
+        const uint32_t by     = out_bytes(C, T.nt, T.base, GSprev, O.g_in);
         uint32_t       total;
         const uint32_t pos = block256_exclusive_sum(by, tmp[1], &total);
-        tile_emit<true>(T, nl, rs, clen, GSprev, GEnext, O.g_in, O.rem_after, stage, pos);
+        stage_out(T.w, T.bm, C, T.nt, T.base, T.n, GSprev, GEnext, O.g_in, O.rem_after, stage, pos);
         __syncthreads();
         uint8_t*       dst = out + rle_base[P.block] + O.out_off;
         const uint32_t cp  = (uint32_t) (lane_id() & (HC - 1)) * HS;
