@@ -559,7 +559,7 @@ class BlockCodec:
              "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",
              "chunks.frame", "chunks.crc",
              "dec.huffman", "dec.rle", "dec.mtf", "dec.ibwt",
-             "dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk")
+             "dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk", "dec.ib_pair")
     DECODE_KERNELS = ("dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk")
 
     @classmethod

@@ -50,7 +50,7 @@ const char* prof_name(int slot)
         "huf.build", "huf.offsets", "huf.tilebits", "huf.tilescan", "huf.zero", "huf.pack",
         "chunks.frame", "chunks.crc",
         "dec.huffman", "dec.rle", "dec.mtf", "dec.ibwt",
-        "dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk"};
+        "dec.hd_trans", "dec.rled", "dec.mtf_local", "dec.ib_walk", "dec.ib_pair"};
     return (slot >= 0 && slot < P_NSLOT) ? names[slot] : "";
 }
 

@@ -9,11 +9,14 @@ struct IbwtWorkspace
 {
     Tiling    tiling;
     uint32_t* T        = nullptr;  // transform, block-local indices
+    uint64_t* T2       = nullptr;  // main path: two transform steps per entry (k_ib_pair)
+    uint64_t  cap_n2   = 0;
     uint32_t* th       = nullptr;
     uint32_t* hop_next = nullptr;
     uint32_t* hop_len  = nullptr;
     uint32_t* start    = nullptr;
     uint32_t* cyc      = nullptr;
+    uint32_t* nopair   = nullptr;  // blocks unsuited to the two-step walk (k_ib_scan)
     uint64_t  cap_n    = 0;
     uint32_t  cap_t = 0, cap_b = 0;
     // main path (ibwt.hip): block records, splitter prefix, control words, hops, staging
@@ -24,6 +27,7 @@ struct IbwtWorkspace
     uint32_t *             m_order = nullptr, *m_cnt = nullptr;  // hops in output order, chain hops per block
     uint8_t *              slot = nullptr, *pool = nullptr;
     uint32_t               cap_mb = 0, cap_ms = 0, pool_cap = 0, G = 0, walk_wg = 384;
+    bool                   pair = false;  // two-step walk (k_ib_pair)
     uint64_t               cap_slot = 0;
     std::vector<uint64_t>  h_blk;
     std::vector<uint32_t>  h_ctl;

@@ -8,10 +8,15 @@
 // Main path (blocks < 2^24 bytes):
 //   k_ib_hist / k_ib_scan / k_ib_scatter2 + 3  TL[k] = transform[k] | L[transform[k]] << 24, so one
 //        4-byte load per step gives both the next index and the output byte;
+//   k_ib_pair    TL2[k] = two steps from k in one 8-byte entry: T[T[k]], both output bytes and the
+//        intermediate index T[k] (for the splitter test).  Its gathers are parallel and nearly
+//        ordered (T is increasing inside every byte bucket, so the k of one bucket read TL at
+//        increasing positions), unlike the walk's dependent loads, which it halves;
 //   k_ib_walk3   persistent waves claim splitters from per-XCD queues (each XCD works through its
-//        own range of blocks, so the random loads of an XCD stay in few blocks' TL); a lane walks
-//        from its splitter to the next one, staging the bytes 16 at a time into the splitter's slot
-//        (4 S bytes; longer hops continue in 256-byte chunks from a pool) and records the hop;
+//        own range of blocks, so the random loads of an XCD stay in few blocks' TL2); a lane walks
+//        from its splitter to the next one two steps per load, staging the bytes 16 at a time into
+//        the splitter's slot (4 S bytes; longer hops continue in 256-byte chunks from a pool) and
+//        records the hop;
 //        lanes that finish claim the next splitter at once, so no lane idles on a long hop;
 //   k_ib_chain3  one workgroup per block ranks the splitter list from the primary splitter by
 //        pointer jumping in LDS -> output offset of every hop (and the primary cycle's length);
@@ -23,6 +28,7 @@
 #include "ibwt.h"
 #include "prof.h"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace bra {
@@ -111,9 +117,13 @@ __global__ void __launch_bounds__(TPB) k_ib_hist(const uint8_t* __restrict__ L, 
     }
 }
 
-// per block: tile offsets per byte = first[c] + sum over earlier tiles
+// per block: tile offsets per byte = first[c] + sum over earlier tiles; *nopair counts the blocks
+// that do not suit the two-step walk (k_ib_pair's gathers read TL at increasing positions inside a
+// byte's bucket, 4 / frequency bytes apart: a byte rarer than 1/32 makes one 128-byte line per
+// element, so a block where such bytes hold a quarter of the positions or more -- e.g. uniform
+// random data -- is walked one step at a time, and with it the batch)
 __global__ void __launch_bounds__(TPB) k_ib_scan(const uint32_t* __restrict__ first, const uint32_t* __restrict__ count, uint32_t nblocks,
-                                                 uint32_t* __restrict__ th)
+                                                 uint32_t* __restrict__ th, uint32_t* __restrict__ nopair)
 {
     __shared__ uint32_t tmp[8];
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
@@ -133,7 +143,15 @@ __global__ void __launch_bounds__(TPB) k_ib_scan(const uint32_t* __restrict__ fi
         }
         for (; i < nt; ++i)
             tot += th[(size_t) (t0 + i) * 256 + c];
-        uint32_t run = block256_exclusive_sum(tot, tmp);
+        uint32_t n;
+        uint32_t run = block256_exclusive_sum(tot, tmp, &n);
+        {
+            uint32_t rare;
+            __syncthreads();
+            block256_exclusive_sum(32ull * tot <= n ? tot : 0u, tmp, &rare);
+            if (c == 0 && nopair && 4ull * rare >= n)
+                atomicAdd(nopair, 1u);
+        }
         for (i = 0; i + 16 <= nt; i += 16)
         {
             uint32_t h[16];
@@ -514,6 +532,46 @@ __global__ void __launch_bounds__(64 * IBS_WAVES) k_ib_scatter3(const uint8_t* _
     }
 }
 
+// TL2[k] = T[T[k]] | L[T[k]] << 24 | L[T[T[k]]] << 32 | T[k] << 40 (block-local indices < 2^24):
+// the byte of step 1, the byte of step 2, the index after step 2 and, for the splitter test, the
+// index between them.  One workgroup per tile, tiles XCD-major (an XCD's gathers stay in its
+// contiguous range of blocks), 16 positions per thread with all their gathers in flight.
+__global__ void __launch_bounds__(TPB) k_ib_pair(const Piece* __restrict__ tiles, uint32_t ntiles, const BlockDesc* __restrict__ blocks,
+                                                 const uint32_t* __restrict__ nopair, const uint32_t* __restrict__ TL, uint64_t* __restrict__ TL2)
+{
+    if (*nopair)
+        return;  // the batch walks one step at a time
+    constexpr int  PT = ITILE / TPB;
+    const XcdTiles X  = xcd_tiles(ntiles);
+    for (uint32_t t = X.t; t < X.end; t += X.step)
+    {
+        const Piece     P    = tiles[t];
+        const uint32_t* tl   = TL + blocks[P.block].off;
+        const uint64_t  o    = blocks[P.block].off + P.start;
+        uint32_t        v1[PT], v2[PT];
+#pragma unroll
+        for (int j = 0; j < PT; ++j)
+        {
+            const uint32_t i = j * TPB + threadIdx.x;
+            v1[j]            = i < P.len ? TL[o + i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j)
+        {
+            const uint32_t i = j * TPB + threadIdx.x;
+            v2[j]            = i < P.len ? tl[v1[j] & 0xFFFFFFu] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j)
+        {
+            const uint32_t i = j * TPB + threadIdx.x;
+            if (i < P.len)
+                TL2[o + i] = (uint64_t) (v2[j] & 0xFFFFFFu) | ((uint64_t) (v1[j] >> 24) << 24) | ((uint64_t) (v2[j] >> 24) << 32) |
+                             ((uint64_t) (v1[j] & 0xFFFFFFu) << 40);
+        }
+    }
+}
+
 // Hardware id (0-7) of the XCD the calling wave runs on (placement only: correctness never
 // depends on it, every wave drains all eight queues).
 __device__ __forceinline__ uint32_t xcd_id()
@@ -531,6 +589,8 @@ struct WalkArgs
     const uint32_t* xr;    // XCD x serves blocks [xr[x], xr[x+1])
     uint32_t*       qc;    // claim counters, one per XCD (32-word stride)
     const uint32_t* TL;
+    const uint64_t* TL2;     // PAIR walks, unless *nopair
+    const uint32_t* nopair;
     uint8_t*        slot;  // splitter slots
     uint8_t*        pool;  // overflow chunks of IB_CHUNK bytes
     uint32_t*       pool_ctr;
@@ -549,6 +609,17 @@ constexpr uint32_t IB_CHUNK = 256;
 // per XCD: 3 MB of TL), 512 3.18, 768 3.59, 1024 3.88, 2048 4.29, 4096 4.31; 32 x 8 MiB 16-symbol
 // blocks (S = 512, scripts/gpu_r4aq.sh): 128 WGs 7.95 ms, 192 6.66, 256 6.49, 384 6.74.
 __host__ inline uint32_t walk_grid(uint32_t max_shift) { return max_shift <= 6 ? 384u : 256u; }
+
+// Walk two steps per load (k_ib_pair first) unless k_ib_scan counts a block that does not suit it?  Building TL2 writes 8
+// bytes per element, more HBM time than the halved walk saves on blocks of up to 1 MiB (their TL
+// fits an XCD's L2, so the one-step walk's loads hit it); BRA_IB_PAIR=0/1 overrides (measurement).
+__host__ inline bool pair_walk(uint32_t max_shift)
+{
+    static const char* e = getenv("BRA_IB_PAIR");
+    if (e && *e)
+        return *e == '1';
+    return max_shift > 6;
+}
 
 __device__ __forceinline__ uint8_t* walk_dst(const WalkArgs& a, uint8_t* slot, uint32_t cap, uint32_t o, uint32_t& chunk, uint32_t g)
 {
@@ -572,8 +643,20 @@ __device__ __forceinline__ uint8_t* walk_dst(const WalkArgs& a, uint8_t* slot, u
     return chunk == 0xFFFFFFFFu ? nullptr : a.pool + (size_t) chunk * IB_CHUNK + (r & (IB_CHUNK - 1));
 }
 
+// WM_ONE: one step per load; WM_PAIR / WM_ONE_IF: two / one step per load if the batch suits /
+// does not suit two-step walking (*nopair), else the kernel exits at once -- both are launched and
+// one of them walks (a kernel holding both loops walked 9 % slower in pair mode).
+enum WalkMode
+{
+    WM_ONE,
+    WM_PAIR,
+    WM_ONE_IF
+};
+template <int MODE>
 __global__ void __launch_bounds__(256) k_ib_walk3(WalkArgs a)
 {
+    if (MODE != WM_ONE && (*a.nopair == 0) != (MODE == WM_PAIR))
+        return;
     const int      lane = lane_id();
     const uint32_t x0   = xcd_id();
     uint32_t       t    = 0;  // queues tried: (x0 + t) & 7
@@ -649,15 +732,45 @@ __global__ void __launch_bounds__(256) k_ib_walk3(WalkArgs a)
         }
         if (act)
         {
+            constexpr bool PAIR = MODE == WM_PAIR;
 #pragma unroll 1
-            for (int st = 0; st < 32; ++st)
+            for (int st = 0; st < (PAIR ? 16 : 32); ++st)
             {
-                const uint32_t v = a.TL[boff + y];
-                y                = v & 0xFFFFFFu;
-                lo               = (lo >> 8) | (hi << 56);
-                hi               = (hi >> 8) | ((uint64_t) (v >> 24) << 56);
-                ++j;
-                const bool split = (y & mask) == 0 || y == p;
+                bool split;
+                if constexpr (PAIR)
+                {
+                    // two steps per load; the hop ends at the intermediate index when that is a
+                    // splitter (one byte), else after both (j stays even until then, so the 16-byte
+                    // flushes fall on whole registers)
+                    const uint64_t v  = a.TL2[boff + y];
+                    const uint32_t y1 = (uint32_t) (v >> 40), y2 = (uint32_t) v & 0xFFFFFFu;
+                    const uint64_t b1 = (v >> 24) & 0xFFu, b2 = (v >> 32) & 0xFFu;
+                    const bool     s1 = (y1 & mask) == 0 || y1 == p;
+                    if (s1)
+                    {
+                        lo = (lo >> 8) | (hi << 56);
+                        hi = (hi >> 8) | (b1 << 56);
+                        j += 1;
+                        y = y1;
+                    }
+                    else
+                    {
+                        lo = (lo >> 16) | (hi << 48);
+                        hi = (hi >> 16) | (b1 << 48) | (b2 << 56);
+                        j += 2;
+                        y = y2;
+                    }
+                    split = s1 || (y2 & mask) == 0 || y2 == p;
+                }
+                else
+                {
+                    const uint32_t v = a.TL[boff + y];
+                    y                = v & 0xFFFFFFu;
+                    lo               = (lo >> 8) | (hi << 56);
+                    hi               = (hi >> 8) | ((uint64_t) (v >> 24) << 56);
+                    ++j;
+                    split = (y & mask) == 0 || y == p;
+                }
                 if ((j & 15) == 0 || split)
                 {
                     const uint32_t nb = ((j - 1) & 15) + 1;  // staged bytes (the top nb of the register)
@@ -883,7 +996,7 @@ bool IbwtWorkspace::reserve(uint64_t n, uint32_t nblocks, uint32_t ntiles)
         cap_b            = 0;
         const uint32_t c = nblocks + 8;
         if (!dev_alloc(hop_next, (uint64_t) c * (MAX_SPLIT + 1)) || !dev_alloc(hop_len, (uint64_t) c * (MAX_SPLIT + 1)) ||
-            !dev_alloc(start, (uint64_t) c * (MAX_SPLIT + 1)) || !dev_alloc(cyc, c))
+            !dev_alloc(start, (uint64_t) c * (MAX_SPLIT + 1)) || !dev_alloc(cyc, c) || (!nopair && !dev_alloc(nopair, 1)))
             return false;
         cap_b = c;
     }
@@ -894,11 +1007,13 @@ void IbwtWorkspace::release()
 {
     tiling.release();
     (void) hipFree(T);
+    (void) hipFree(T2);
     (void) hipFree(th);
     (void) hipFree(hop_next);
     (void) hipFree(hop_len);
     (void) hipFree(start);
     (void) hipFree(cyc);
+    (void) hipFree(nopair);
     for (void* p : {(void*) blk, (void*) cum, (void*) ctl, (void*) m_next, (void*) m_len, (void*) m_ovf, (void*) m_start, (void*) ovl_next,
                     (void*) slot, (void*) pool, (void*) m_order, (void*) m_cnt})
         (void) hipFree(p);
@@ -971,7 +1086,9 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
         return false;
     uint8_t* runny = reinterpret_cast<uint8_t*>(w.th + (size_t) w.cap_t * 256);  // per tile: k_ib_scatter2 (1) or k_ib_scatter3 (0)
     hipLaunchKernelGGL(k_ib_hist, dim3(std::min<uint32_t>(nt, 8192)), dim3(TPB), 0, s, d_L, w.tiling.d_pieces, nt, w.th, runny);
-    hipLaunchKernelGGL(k_ib_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, w.th);
+    BRA_HIP_CHECK(hipMemsetAsync(w.nopair, 0, 4, s));
+    hipLaunchKernelGGL(k_ib_scan, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(TPB), 0, s, w.tiling.d_first, w.tiling.d_count, nblocks, w.th,
+                       w.nopair);
     if (!main_path)
         return ibwt_two_walk(w, d_L, d_pi, d_blocks, nblocks, d_out, s);
 
@@ -999,11 +1116,19 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
         }
         cum[nblocks] = G;
         w.walk_wg    = walk_grid(max_shift);
+        w.pair       = pair_walk(max_shift);
         // XCD x serves blocks [xr[x], xr[x+1]): contiguous eighths of the batch
         for (uint32_t x = 0; x <= 8; ++x)
             ctl[256 + x] = (uint32_t) ((uint64_t) nblocks * x / 8);
         if (!w.reserve_main(nblocks, G, slot))
             return false;
+        if (w.pair && N > w.cap_n2)
+        {
+            w.cap_n2 = 0;
+            if (!dev_alloc(w.T2, N + N / 8 + 4096))
+                return false;
+            w.cap_n2 = N + N / 8 + 4096;
+        }
         w.G = G;
         w.h_key.clear();
         BRA_HIP_CHECK(hipMemcpyAsync(w.blk, w.h_blk.data(), (size_t) nblocks * sizeof(IbBlk), hipMemcpyHostToDevice, s));
@@ -1022,17 +1147,30 @@ bool ibwt_device(IbwtWorkspace& w, const uint8_t* d_L, const uint32_t* d_pi, con
     // k_ib_scatter2's and this launch only reads the flags)
     hipLaunchKernelGGL(k_ib_scatter3, dim3(std::min<uint32_t>(nt, 1024)), dim3(64 * IBS_WAVES), 0, s, d_L, w.tiling.d_pieces, nt, w.th, d_blocks,
                        w.T, runny);
-    WalkArgs a{blk, d_pi, w.cum, w.ctl + 256, w.ctl, w.T, w.slot, w.pool, w.ctl + 300, w.pool_cap, w.ovl_next, w.m_next, w.m_len, w.m_ovf};
+    if (w.pair)
+    {
+        BRA_PROF(P_DEC_IB_PAIR, s);
+        hipLaunchKernelGGL(k_ib_pair, dim3(xcd_grid(std::min<uint32_t>(nt, 8192))), dim3(TPB), 0, s, w.tiling.d_pieces, nt, d_blocks, w.nopair, w.T,
+                           w.T2);
+    }
+    WalkArgs a{blk, d_pi, w.cum, w.ctl + 256, w.ctl, w.T, w.T2, w.nopair, w.slot, w.pool, w.ctl + 300, w.pool_cap, w.ovl_next, w.m_next, w.m_len, w.m_ovf};
     {
         BRA_PROF(P_DEC_IB_WALK, s);
         if (g_prof)
         {
-            double n = 0;  // algorithmic bytes: one 4-byte TL entry read and one output byte per element
+            double n = 0;  // algorithmic bytes per element: one output byte and a 4-byte TL entry (PAIR: half an 8-byte TL2 entry)
             for (uint32_t b = 0; b < nblocks; ++b)
                 n += h_blocks[b].len;
             prof_bytes(P_DEC_IB_WALK, 5.0 * n);
+            prof_bytes(P_DEC_IB_PAIR, 16.0 * n);  // TL read twice, TL2 written
         }
-        hipLaunchKernelGGL(k_ib_walk3, dim3(w.walk_wg), dim3(256), 0, s, a);
+        if (w.pair)
+        {
+            hipLaunchKernelGGL(k_ib_walk3<WM_PAIR>, dim3(w.walk_wg), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_ib_walk3<WM_ONE_IF>, dim3(w.walk_wg), dim3(256), 0, s, a);
+        }
+        else
+            hipLaunchKernelGGL(k_ib_walk3<WM_ONE>, dim3(w.walk_wg), dim3(256), 0, s, a);
     }
     hipLaunchKernelGGL(k_ib_chain3, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(IB_CH_TPB), 0, s, blk, d_pi, w.cum, nblocks, w.m_next,
                        w.m_len, w.m_start, w.cyc, w.m_order, w.m_cnt);

@@ -20,6 +20,7 @@ enum ProfSlot : int
     P_FRAME, P_CRC,
     P_DEC_HUF, P_DEC_RLE, P_DEC_MTF, P_DEC_IBWT,       // decode stages
     P_DEC_HD_TRANS, P_DEC_RLED, P_DEC_MTF_LOCAL, P_DEC_IB_WALK,  // their largest kernels
+    P_DEC_IB_PAIR,
     P_NSLOT
 };
 
