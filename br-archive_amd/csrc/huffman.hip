@@ -96,37 +96,67 @@ __global__ void __launch_bounds__(64) k_huff_build(const uint32_t* __restrict__ 
             }
             return c;
         };
-        // leaves in symbol order (:140-153): position 0 if the head's frequency is larger, else
-        // max(1, entries with a smaller frequency) (:90-118); entries from p on move up by one
-        for (uint32_t id = 0; id < leaves; ++id)
+        // Leaves in symbol order (:140-153): position 0 if the head's frequency is larger, else
+        // max(1, entries with a smaller frequency) (:90-118).  The list stays sorted by frequency,
+        // so the insertions have a closed form, computed for all leaves at once instead of one
+        // insertion (ballots + lane shifts) per leaf: a leaf's position = the leaves of smaller
+        // frequency + its rank among its equals.  Equals go in front of each other (lower bound),
+        // except while their frequency is the smallest seen so far (no earlier symbol is rarer):
+        // those land at position 1, right behind the group's first leaf.  With the group's members
+        // x1..xm in symbol order and x1..xk inserted in that regime the group reads
+        // xm .. x(k+1), x1, xk .. x2 (k = 0: xm .. x1).
         {
-            const uint32_t f     = S.node_f[id];
-            const uint32_t headf = __builtin_amdgcn_readlane(LF[0], 0);
-            const uint32_t lt    = lt_count(f, 0);
-            const uint32_t p     = (len == 0 || headf > f) ? 0u : (lt > 1u ? lt : 1u);
-            uint32_t       uF[4], uI[4], cF[4], cI[4];
-            const int      nr = (int) (len / 64u) + 1;  // registers holding the list after the insert
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
+            uint32_t less[4] = {0, 0, 0, 0}, eq[4] = {0, 0, 0, 0}, eqb[4] = {0, 0, 0, 0}, lessb[4] = {0, 0, 0, 0}, lid[4];
             {
-                if (r >= nr)
-                    break;
-                uF[r] = wave_shr1(LF[r]);
-                uI[r] = wave_shr1(LI[r]);
-                cF[r] = r ? (uint32_t) __builtin_amdgcn_readlane(LF[r > 0 ? r - 1 : 0], 63) : 0u;
-                cI[r] = r ? (uint32_t) __builtin_amdgcn_readlane(LI[r > 0 ? r - 1 : 0], 63) : 0u;
+                uint32_t id = ex;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    lid[r] = h[r] ? id++ : 0xFFFFFFFFu;
+            }
+            for (uint32_t q = 0; q < leaves; ++q)
+            {
+                const uint32_t fq = S.node_f[q];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    less[r] += fq < h[r] ? 1u : 0u;
+                    eq[r] += fq == h[r] ? 1u : 0u;
+                    eqb[r] += (fq == h[r] && q < lid[r]) ? 1u : 0u;
+                    lessb[r] += (fq < h[r] && q < lid[r]) ? 1u : 0u;
+                }
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r)
+                if (h[r])
+                    S.next[lid[r]] = lessb[r] == 0 ? 1u : 0u;  // inserted while the smallest so far
+            __syncthreads();
+            uint32_t kmin[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < leaves; ++q)
             {
-                if (r >= nr)
-                    break;
-                const uint32_t j  = 64u * r + lane;
-                const uint32_t sF = lane ? uF[r] : cF[r], sI = lane ? uI[r] : cI[r];
-                LF[r]             = j > p ? sF : (j == p ? f : LF[r]);
-                LI[r]             = j > p ? sI : (j == p ? id : LI[r]);
+                const uint32_t fq = S.node_f[q], mq = S.next[q];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    kmin[r] += (fq == h[r] && mq) ? 1u : 0u;
             }
-            ++len;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (h[r])
+                {
+                    const uint32_t m = eq[r], i = eqb[r] + 1, k = kmin[r];
+                    const uint32_t rank = k == 0 ? m - i : (i == 1 ? m - k : (i <= k ? m - i + 1 : m - i));
+                    S.cnt[less[r] + rank]   = h[r];            // (cnt / len_s: free until the lengths)
+                    S.len_s[less[r] + rank] = (uint8_t) lid[r];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const uint32_t j = 64u * r + lane;
+                LF[r]            = j < leaves ? S.cnt[j] : 0u;
+                LI[r]            = j < leaves ? (uint32_t) S.len_s[j] : 0u;
+            }
+            len = leaves;
+            __syncthreads();
         }
         // merges (:158-175): pop the two head entries, insert their sum by the same rule
         uint32_t nodes = leaves;

@@ -608,7 +608,13 @@ constexpr uint32_t IB_CHUNK = 256;
 // latency.  256 x 1 MiB text (S = 64, scripts/gpu_r4v.sh): 256 WGs 3.55 ms, 384 3.07 (12 K lanes
 // per XCD: 3 MB of TL), 512 3.18, 768 3.59, 1024 3.88, 2048 4.29, 4096 4.31; 32 x 8 MiB 16-symbol
 // blocks (S = 512, scripts/gpu_r4aq.sh): 128 WGs 7.95 ms, 192 6.66, 256 6.49, 384 6.74.
-__host__ inline uint32_t walk_grid(uint32_t max_shift) { return max_shift <= 6 ? 384u : 256u; }
+__host__ inline uint32_t walk_grid(uint32_t max_shift)
+{
+    static const char* e = getenv("BRA_IB_WALKWG");  // measurement override
+    if (e && *e)
+        return (uint32_t) atoi(e);
+    return max_shift <= 6 ? 384u : 256u;
+}
 
 // Walk two steps per load (k_ib_pair first) unless k_ib_scan counts a block that does not suit it?  Building TL2 writes 8
 // bytes per element, more HBM time than the halved walk saves on blocks of up to 1 MiB (their TL
