@@ -103,21 +103,29 @@ __global__ void __launch_bounds__(TPB) k_mtf_alpha(const uint32_t* __restrict__ 
 // 4-byte load per thread was bound by its load -> atomics -> barrier -> store latency chain.)
 // Position-table blocks: the lanes of each half segment (lanes 0-31: bytes 0-511) update their own
 // row, and the segment's state is two compact rows, [256 s + 32 h + a] = last occurrence of the
-// block's a-th value in half h (-1: none; a >= the block's alphabet: -1).
+// block's a-th value in half h (-1: none; a >= the block's alphabet: -1).  Their values are below
+// 127 and few, so many lanes of one atomic instruction hit the same entry (same-address atomics
+// serialise: half the kernel's time on text): each half keeps LO_NC copies of its row (copy = lane
+// mod LO_NC, LO_CS words apart so one value's copies sit in different banks), merged at the end.
+constexpr int LO_NC = 4, LO_CS = 132;
 __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__ in, const Piece* __restrict__ segs, uint32_t nseg,
                                                      int32_t* __restrict__ state, const uint32_t* __restrict__ amode,
                                                      const uint32_t* __restrict__ nsym, const uint8_t* __restrict__ ainv)
 {
-    __shared__ int32_t lo_s[TPB / 64][2][256];
-    const int      lane = lane_id();
-    const uint32_t wave = threadIdx.x >> 6;
+    constexpr int      ROW = 2 * LO_NC * LO_CS;  // >= 256: the full row of other blocks
+    __shared__ __attribute__((aligned(16))) int32_t lo_s[TPB / 64][ROW];
+    const int          lane = lane_id();
+    const uint32_t     wave = threadIdx.x >> 6;
     for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
     {
         const Piece    P    = segs[s];
         const bool     half = amode[P.block] != 0;
-        int32_t*       lo   = lo_s[wave][half ? (lane >> 5) : 0];
-        reinterpret_cast<int4*>(lo_s[wave][0])[lane] = make_int4(-1, -1, -1, -1);
-        reinterpret_cast<int4*>(lo_s[wave][1])[lane] = make_int4(-1, -1, -1, -1);
+        int32_t*       lo   = half ? lo_s[wave] + ((lane >> 5) * LO_NC + (lane & (LO_NC - 1))) * LO_CS : lo_s[wave];
+        if (half)
+            for (int i = lane; i < ROW / 4; i += 64)
+                reinterpret_cast<int4*>(lo_s[wave])[i] = make_int4(-1, -1, -1, -1);
+        else
+            reinterpret_cast<int4*>(lo_s[wave])[lane] = make_int4(-1, -1, -1, -1);
         const uint8_t* p    = in + P.off;
         const uint32_t i0   = (uint32_t) lane * 16;
         uint32_t       w[4] = {0, 0, 0, 0};
@@ -144,7 +152,14 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
         if (half)
         {
             const uint32_t a = (uint32_t) lane & 31u;
-            const int32_t  v = a < nsym[P.block] ? lo_s[wave][lane >> 5][ainv[(size_t) P.block * 32 + a]] : -1;
+            int32_t        v = -1;
+            if (a < nsym[P.block])
+            {
+                const int32_t* row = lo_s[wave] + (lane >> 5) * LO_NC * LO_CS + ainv[(size_t) P.block * 32 + a];
+#pragma unroll
+                for (int k = 0; k < LO_NC; ++k)
+                    v = max(v, row[k * LO_CS]);
+            }
             state[(size_t) s * 256 + lane] = v >= 0 ? st + v : -1;
         }
         else
