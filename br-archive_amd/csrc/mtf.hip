@@ -255,6 +255,8 @@ __global__ void __launch_bounds__(TPB) k_mtf_pt_tables(int32_t* __restrict__ sta
 {
     const uint32_t a = threadIdx.x & 31u, hb = (uint32_t) lane_id() & 32u;
     uint8_t*       pt = reinterpret_cast<uint8_t*>(state);
+    __shared__ __attribute__((aligned(16))) int32_t tt_s[TPB / 32][32];  // per half wave: the 32 last occurrences
+    int32_t*       tts = tt_s[threadIdx.x >> 5];
     for (uint32_t c = blockIdx.x * (TPB / 32) + (threadIdx.x >> 5); c < g.nchunks; c += gridDim.x * (TPB / 32))
     {
         const uint32_t b = g.chunk_blk[c];  // uniform per half wave
@@ -278,9 +280,17 @@ __global__ void __launch_bounds__(TPB) k_mtf_pt_tables(int32_t* __restrict__ sta
             const bool     seen = a < na && tt >= 0;
             const uint32_t mk   = (uint32_t) (__builtin_amdgcn_ballot_w64(seen) >> hb);
             uint32_t       later = 0;
-#pragma unroll 8
-            for (uint32_t j = 0; j < 32; ++j)
-                later += __shfl(tt, (int) (hb + j), 64) > tt ? 1u : 0u;
+            // the half wave's 32 values through LDS, 4 per broadcast read (32 lane permutes per
+            // half segment bounded the kernel)
+            tts[a] = tt;
+            wave_barrier_lds();
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j)
+            {
+                const int4 q = reinterpret_cast<const int4*>(tts)[j];
+                later += (q.x > tt ? 1u : 0u) + (q.y > tt ? 1u : 0u) + (q.z > tt ? 1u : 0u) + (q.w > tt ? 1u : 0u);
+            }
+            wave_barrier_lds();
             const uint32_t pos = seen ? later : (uint32_t) __popc(mk) + val - (uint32_t) __popc(mk & ((1u << a) - 1u));
             pt[(size_t) (s0 + (h >> 1)) * 1024 + 512 + (h & 1) * 32 + a] = a < na ? (uint8_t) (0x80u | pos) : (uint8_t) 0xFF;
         }
