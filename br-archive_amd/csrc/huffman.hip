@@ -478,8 +478,7 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
                                                    const uint32_t* __restrict__ tbits, const uint64_t* __restrict__ tbit0,
                                                    uint32_t* __restrict__ out_words)
 {
-    __shared__ uint8_t  L[256];
-    __shared__ uint32_t C[256];
+    __shared__ uint2    LC[256];  // (code, length) per symbol: one LDS read per symbol
     __shared__ uint32_t tmp[8];
     __shared__ uint32_t img[PACK_WORDS];
     constexpr int       PT = RLE_TILE / TPB;
@@ -491,8 +490,7 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
             continue;  // uniform
         const Piece    P  = tiles[t];
         const uint32_t rs = meta[P.block].orig_size;
-        L[threadIdx.x]    = meta[P.block].lengths[threadIdx.x];
-        C[threadIdx.x]    = codes[(size_t) P.block * 256 + threadIdx.x];
+        LC[threadIdx.x]   = make_uint2(codes[(size_t) P.block * 256 + threadIdx.x], meta[P.block].lengths[threadIdx.x]);
         const uint32_t cnt = min(P.len, rs - P.start);
         const uint64_t g0  = tbit0[t];
         const uint32_t sh  = (uint32_t) (g0 & 31);
@@ -506,11 +504,15 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
         static_assert(PT == 16, "16 symbols per thread");
         const uint32_t i0 = threadIdx.x * PT;
         uint8_t        sym[PT];
+        uint2          e[PT];  // code, length of each symbol (read once, kept across the scan's barrier)
         uint32_t       mybits = 0;
         load_syms(rle + P.off, cnt, i0, sym);
 #pragma unroll
         for (int k = 0; k < PT; ++k)
-            mybits += (i0 + k < cnt) ? L[sym[k]] : 0;
+        {
+            e[k] = (i0 + k < cnt) ? LC[sym[k]] : make_uint2(0, 0);
+            mybits += e[k].y;
+        }
         if (!lds)
         {
             // global path (codes > 32 bits make the tile image too large for LDS): the words strictly
@@ -549,15 +551,15 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
             for (int k = 0; k < PT; ++k)
             {
                 if (i0 + k >= cnt)
-                    break;
-                uint32_t nb = L[sym[k]];
+                    continue;  // (not break: the loop must unroll fully to keep e[] in registers)
+                uint32_t nb = e[k].y;
                 if (nb > 32)
                 {
                     nacc += nb - 32;  // leading zero bits of a wrapped long code
                     flush();
                     nb = 32;
                 }
-                acc |= ((uint64_t) C[sym[k]] << (64 - nb)) >> nacc;
+                acc |= ((uint64_t) e[k].x << (64 - nb)) >> nacc;
                 nacc += nb;
                 flush();
             }
@@ -570,9 +572,9 @@ __global__ void __launch_bounds__(TPB) k_huff_pack(const uint8_t* __restrict__ r
             for (int k = 0; k < PT; ++k)
             {
                 if (i0 + k >= cnt)
-                    break;
-                uint32_t       nb = L[sym[k]];
-                const uint32_t c  = C[sym[k]];
+                    continue;
+                uint32_t       nb = e[k].y;
+                const uint32_t c  = e[k].x;
                 if (nb > 32)
                 {
                     pos += nb - 32;  // leading zero bits of a wrapped long code
