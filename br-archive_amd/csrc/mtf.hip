@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_presence(const uint8_t* __restrict_
 
 // One workgroup per block, thread c = byte value c: the block's alphabet from its presence mask.
 // amap[b][c] = rank of c among the present values (0xFF: absent), ainv[b][a] = the a-th present
-// value (a < 32), amode[b] = 4 / 8 position-table dwords when the block has at most 16 / 32
+// value (a < 32), amode[b] = the position-table dwords (4 for at most 16 values, else ceil(values / 4) up to 32
 // distinct values, all below 127 (every MTF position then stays below 127), else 0.
 __global__ void __launch_bounds__(TPB) k_mtf_alpha(const uint32_t* __restrict__ amask, uint32_t nblocks, uint32_t* __restrict__ nsym,
                                                    uint8_t* __restrict__ amap, uint8_t* __restrict__ ainv, uint32_t* __restrict__ amode)
@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_alpha(const uint32_t* __restrict__ 
         if (c == 0)
         {
             nsym[b]  = (uint32_t) n;
-            amode[b] = high ? 0u : (n <= 16 ? 4u : (n <= 32 ? 8u : 0u));
+            amode[b] = (high || n > 32) ? 0u : (n <= 16 ? 4u : (uint32_t) (n + 3) / 4);  // table dwords (4..8)
         }
         __syncthreads();
     }
@@ -582,15 +582,19 @@ __device__ __forceinline__ uint32_t mtf_step_pos(uint32_t (&R)[NP], uint32_t a)
     for (int k = 0; k < NP; ++k)
         v[k] = op(R[k]);
     uint32_t x;
-    if constexpr (NP == 8)
+    if constexpr (NP > 4)
     {
-        const uint32_t x0 = (q & 1) ? v[1] : v[0], x1 = (q & 1) ? v[3] : v[2], x2 = (q & 1) ? v[5] : v[4], x3 = (q & 1) ? v[7] : v[6];
-        const uint32_t y0 = (q & 2) ? x1 : x0, y1 = (q & 2) ? x3 : x2;
+        // 5..8 dwords (17..32 values): a three-level tree, missing leaves never selected
+        constexpr int  i5 = NP > 5 ? 5 : NP - 1, i6 = NP > 6 ? 6 : NP - 1, i7 = NP > 7 ? 7 : NP - 1;
+        const uint32_t x0 = (q & 1) ? v[1] : v[0], x1 = (q & 1) ? v[3] : v[2];
+        const uint32_t x2 = NP > 5 ? ((q & 1) ? v[i5] : v[4]) : v[4];
+        const uint32_t x3 = NP > 7 ? ((q & 1) ? v[i7] : v[i6]) : v[i6];
+        const uint32_t y0 = (q & 2) ? x1 : x0, y1 = NP > 6 ? ((q & 2) ? x3 : x2) : x2;
         x = (q & 4) ? y1 : y0;
     }
     else
     {
-        static_assert(NP == 4, "4 or 8 table dwords");
+        static_assert(NP == 4, "4 to 8 table dwords");
         const uint32_t x0 = (q & 1) ? v[1] : v[0], x1 = (q & 1) ? v[3] : v[2];
         x = (q & 2) ? x1 : x0;
     }
@@ -732,12 +736,12 @@ __device__ __forceinline__ void encode_pos_wg(const uint8_t* __restrict__ in, ui
     if (len)
     {
         const uint4* pt = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(state) + (size_t) s * 1024 + 512 + half * 32);
+        const uint4  v0 = pt[0];
+        const uint4  v1 = NP > 4 ? pt[1] : v0;
+        const uint32_t t8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-        for (int q = 0; q < NP / 4; ++q)
-        {
-            const uint4 v = pt[q];
-            R[4 * q] = v.x, R[4 * q + 1] = v.y, R[4 * q + 2] = v.z, R[4 * q + 3] = v.w;
-        }
+        for (int k = 0; k < NP; ++k)
+            R[k] = t8[k];
     }
     mtf_code_rounds<NP, true>(in, out, R, io, s_off, s_len, map_s, [](uint32_t (&T)[NP], uint32_t a) { return mtf_step_pos<NP>(T, a); });
 }
@@ -774,10 +778,14 @@ __global__ void __launch_bounds__(TPB, 8) k_mtf_encode_pos(const uint8_t* __rest
         s_len[t] = len;
         map_s[t] = amap[(size_t) b * 256 + t];
         __syncthreads();
-        if (mode == 4)
-            encode_pos_wg<4>(in, out, state, s, half, len, io, s_off, s_len, map_s);
-        else
-            encode_pos_wg<8>(in, out, state, s, half, len, io, s_off, s_len, map_s);
+        switch (mode)  // table dwords: ceil(values / 4), uniform per block
+        {
+        case 4: encode_pos_wg<4>(in, out, state, s, half, len, io, s_off, s_len, map_s); break;
+        case 5: encode_pos_wg<5>(in, out, state, s, half, len, io, s_off, s_len, map_s); break;
+        case 6: encode_pos_wg<6>(in, out, state, s, half, len, io, s_off, s_len, map_s); break;
+        case 7: encode_pos_wg<7>(in, out, state, s, half, len, io, s_off, s_len, map_s); break;
+        default: encode_pos_wg<8>(in, out, state, s, half, len, io, s_off, s_len, map_s); break;
+        }
         __syncthreads();
     }
 }

@@ -326,6 +326,19 @@ def test_batch_alphabets(bra, codec, orc, bs):
     _encode_check(bra, codec, orc, data, bs)
 
 
+def test_batch_position_table_widths(bra, codec, orc):
+    """MTF position tables (csrc/mtf.hip mtf_step_pos): blocks of 1..32 distinct values all below 127
+    take tables of ceil(values / 4) dwords (4 for up to 16) -- every width from 4 to 8 on both sides
+    of its limit, values spread over 0..126 or packed at its top, against the oracle."""
+    rng = np.random.default_rng(0x7AB1E)
+    bs = 65536
+    blocks = []
+    for k in [1, 15, 16, 17, 20, 21, 24, 25, 28, 29, 31, 32]:
+        blocks.append(_alphabet_block(rng, bs, np.sort(rng.choice(127, k, replace=False))))
+        blocks.append(_alphabet_block(rng, bs, np.arange(127 - k, 127)))
+    _encode_check(bra, codec, orc, np.concatenate(blocks), bs)
+
+
 def test_config1_tiled_block(bra, codec, golden):
     import torch
 
