@@ -37,6 +37,7 @@ ABI_SYMBOLS = (
     "bra_gpu_encode_blocks", "bra_gpu_decode_blocks", "bra_gpu_stage_ptr", "bra_gpu_version", "bra_gpu_selftest",
     "bra_gpu_prof_enable", "bra_gpu_prof_reset", "bra_gpu_prof_read",
     "bra_gpu_crc32c", "bra_gpu_chunks_crc32c", "bra_gpu_crc32c_combine", "bra_gpu_entry_crc32c", "bra_gpu_chunks_bound",
+    "bra_gpu_pipe_records_bound",
     "bra_gpu_frame_chunks", "bra_gpu_unframe_chunks", "bra_gpu_compress_chunks", "bra_gpu_decompress_chunks",
     "bra_gpu_compress_chunks_host", "bra_gpu_decompress_chunks_host",
     "bra_gpu_chunks_crc32c_shard", "bra_gpu_assemble_shards",
@@ -141,6 +142,8 @@ def _load() -> C.CDLL:
     lib.bra_gpu_entry_crc32c.restype = C.c_uint32
     lib.bra_gpu_chunks_bound.argtypes = [C.c_uint64, C.c_uint32]
     lib.bra_gpu_chunks_bound.restype = C.c_uint64
+    lib.bra_gpu_pipe_records_bound.argtypes = [C.c_uint64, C.c_uint32]
+    lib.bra_gpu_pipe_records_bound.restype = C.c_uint64
     lib.bra_gpu_frame_chunks.argtypes = [vp, vp, vp, vp, C.c_uint32, vp, C.c_uint64, u64p, vp]
     lib.bra_gpu_frame_chunks.restype = C.c_int
     lib.bra_gpu_unframe_chunks.argtypes = [vp, vp, C.c_uint64, C.c_uint32, vp, vp, u32p, vp]
@@ -421,7 +424,7 @@ class BlockCodec:
         total = int(data_np.size)
         bb = max(block_size, batch_bytes // block_size * block_size)
         spans = [(o, min(total, o + bb)) for o in range(0, total, bb)]
-        cap = lib.bra_gpu_chunks_bound(bb, block_size)
+        cap = lib.bra_gpu_pipe_records_bound(bb, block_size)
         hin = [lib.bra_gpu_host_alloc(self.ctx, bb) for _ in range(2)]
         hout = lib.bra_gpu_host_alloc(self.ctx, cap)
         if not all(hin) or not hout:
@@ -468,6 +471,10 @@ class BlockCodec:
                         submit(k + 1)
                     collect(k)
         finally:
+            # after a failure part way a slot may still hold a submitted batch or a staged copy:
+            # drain both (a no-op on a free slot) so later pipelined calls find them free
+            for q in range(2):
+                lib.bra_gpu_compress_chunks_collect(self.ctx, q, None, 0, None, None)
             for p in (*hin, hout):
                 lib.bra_gpu_host_free(self.ctx, p)
         return res

@@ -32,8 +32,9 @@ bool bwt_encode_enqueue(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d
 bool bwt_encode_finish(BwtWorkspace* w, const uint8_t* d_in, const BlockDesc* d_blocks, const BlockDesc* h_blocks, uint32_t nblocks,
                        uint8_t* d_L, uint32_t* d_pi, hipStream_t s, bool* fallback_ran);
 
-// BWT of one block of any length >= 1 (bwt_large.hip: prefix doubling with rocPRIM radix sorts), used
-// by the single-block C-ABI for blocks of 2^24 bytes or more; synchronises the stream.
+// BWT of one block of any length >= 1 (bwt_large.hip: prefix doubling over cyclic rotations, the
+// (key, index) pairs sorted by a hand-written stable LSD radix sort), used by the single-block C-ABI
+// for blocks of 2^24 bytes or more; synchronises the stream.
 bool bwt_encode_large(const uint8_t* d_in, uint32_t n, uint8_t* d_L, uint32_t* d_pi, hipStream_t s);
 
 }  // namespace bra

@@ -219,6 +219,8 @@ struct bra_gpu_ctx_s
     uint64_t*      d_enc_rle_base = nullptr;
     uint64_t       cap_eb = 0, cap_erb = 0;
     hipEvent_t     null_ev = nullptr;  // CallStream: the null stream's position at a NULL-stream call
+    hipEvent_t     caller_ev = nullptr;  // CallStream: the end of the last call on a caller-supplied stream
+    bool           caller_pending = false;
     Prof           prof;
     // pipelined host-buffer chunk compression (bra_gpu_compress_chunks_submit / _collect)
     struct PipeSlot
@@ -284,6 +286,8 @@ static void ctx_free(bra_gpu_ctx_s* c)
         (void) hipStreamDestroy(c->stream);
     if (c->null_ev)
         (void) hipEventDestroy(c->null_ev);
+    if (c->caller_ev)
+        (void) hipEventDestroy(c->caller_ev);
 }
 
 // The stream a batch call runs on (include/bra_hip.h, Part 2/3).  An explicit stream orders the
@@ -293,31 +297,53 @@ static void ctx_free(bra_gpu_ctx_s* c)
 // non-blocking: without the two joins a NULL-stream caller could read the results before the
 // call's last kernels had written them -- the encode chain queues MTF / RLE / Huffman after its
 // last host wait -- or the call could read inputs still in flight on the null stream.)
+// A pipelined batch (bra_gpu_compress_chunks_submit) leaves its MTF / RLE / Huffman, framing and
+// CRC queued on the context stream, and they use the context-wide work buffers; a call on a
+// caller-supplied stream made before that batch is collected waits for the batch's end (the slot's
+// ev_done), and the next submit waits for the last caller-stream call (caller_ev), so the two never
+// share the buffers at the same time.
 struct CallStream
 {
-    hipStream_t s;
-    bool        own;
-    CallStream(bra_gpu_ctx_s* c, void* stream) : s(stream ? (hipStream_t) stream : c->stream), own(stream == nullptr)
+    bra_gpu_ctx_s* c;
+    hipStream_t    s;
+    bool           own;
+    CallStream(bra_gpu_ctx_s* ctx, void* stream) : c(ctx), s(stream ? (hipStream_t) stream : ctx->stream), own(stream == nullptr)
     {
         if (own && hipEventRecord(c->null_ev, nullptr) == hipSuccess)
             (void) hipStreamWaitEvent(s, c->null_ev, 0);
+        if (!own)
+            for (auto& ps : c->pipe)
+                if (ps.state == 1)
+                    (void) hipStreamWaitEvent(s, ps.ev_done, 0);
+    }
+    void mark()
+    {
+        if (own || (!c->caller_ev && hipEventCreateWithFlags(&c->caller_ev, hipEventDisableTiming) != hipSuccess))
+            return;
+        if (hipEventRecord(c->caller_ev, s) == hipSuccess)
+            c->caller_pending = true;
     }
     // The call's result folded with the completion of a NULL-stream call: a kernel of the chain
     // that failed after the last host wait shows only at this synchronisation.
     int finish(int rc)
     {
+        mark();
         if (own)
         {
             own = false;
             if (hipStreamSynchronize(s) != hipSuccess && rc >= 0)
                 rc = -1;
         }
+        else
+            s = nullptr;  // marked
         return rc;
     }
     ~CallStream()
     {
         if (own)  // an early (error) return: still leave nothing queued behind the caller
             (void) hipStreamSynchronize(s);
+        else if (s)
+            mark();
     }
     operator hipStream_t() const { return s; }
 };
@@ -944,6 +970,11 @@ static uint64_t pipe_records_bound(const std::vector<BlockDesc>& hb)
     return r;
 }
 
+uint64_t bra_gpu_pipe_records_bound(uint64_t total, uint32_t block_size)
+{
+    return (total && block_size) ? pipe_records_bound(geometry(total, block_size)) : 0;
+}
+
 void* bra_gpu_host_alloc(bra_gpu_ctx_t* c, uint64_t bytes)
 {
     if (!c || !bytes)
@@ -1038,7 +1069,8 @@ int bra_gpu_compress_chunks_submit(bra_gpu_ctx_t* c, int slot, const uint8_t* h_
     if (!grow(ps.d_out, ps.cap_out, rb + 16) || !grow(c->d_hdr, c->cap_hdr, nb) || !grow(c->d_off, c->cap_off, nb + 1) ||
         !grow(c->d_pay, c->cap_pay, rb) || !grow(c->d_word, c->cap_word, 4))
         return -1;
-    if ((!staged && !pipe_copy_in(c, ps, h_in, data_size)) || hipStreamWaitEvent(s, ps.ev_in, 0) != hipSuccess)
+    if ((!staged && !pipe_copy_in(c, ps, h_in, data_size)) || hipStreamWaitEvent(s, ps.ev_in, 0) != hipSuccess ||
+        (c->caller_pending && hipStreamWaitEvent(s, c->caller_ev, 0) != hipSuccess))
         return -1;
     g_prof = c->prof.mask ? &c->prof : nullptr;
     int rc = encode_impl(c, ps.d_in, hb, c->d_hdr, c->d_off, c->d_pay, c->cap_pay, s, nullptr);
@@ -1081,17 +1113,22 @@ int bra_gpu_compress_chunks_collect(bra_gpu_ctx_t* c, int slot, uint8_t* h_out, 
     }
     if (ps.state != 1)
         return -1;
-    ps.state = 0;
     if (hipEventSynchronize(ps.ev_done) != hipSuccess)
+    {
+        ps.state = 0;
         return -1;
+    }
     const uint64_t* mail = c->h_pipe_mail + 2 * slot;
     const uint64_t  need = mail[0] + (uint64_t) CHUNK_HDR_DISK * ps.nb;
     if (out_size)
         *out_size = need;
     if (chunks_crc)
         *chunks_crc = (uint32_t) mail[1];
-    if (need > out_cap || !h_out)
-        return need > out_cap ? -2 : -1;
+    if (h_out && need > out_cap)
+        return -2;  // the batch stays in the slot: collect again with a larger buffer (or drain it)
+    ps.state = 0;
+    if (!h_out)
+        return -1;
     if (hipMemcpyAsync(h_out, ps.d_out, need, hipMemcpyDeviceToHost, c->copy_out) != hipSuccess || hipStreamSynchronize(c->copy_out) != hipSuccess)
         return -1;
     return need < ps.data_size ? 1 : 0;  // 0: not smaller than the input -> STORED (lib_bra_io_file_chunks.c:274-278)

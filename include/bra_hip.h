@@ -151,6 +151,9 @@ uint32_t bra_gpu_entry_crc32c(uint32_t me_crc, uint64_t chunks_size, uint32_t ch
 
 /* Output capacity for bra_gpu_compress_chunks: payload bound + 267 bytes per chunk. */
 uint64_t bra_gpu_chunks_bound(uint64_t total, uint32_t block_size);
+/* Output capacity for bra_gpu_compress_chunks_collect of one batch of total bytes: the chunk records
+ * the pipelined API can return (RLE-capacity payloads + 267 bytes per chunk), about 1.01x total. */
+uint64_t bra_gpu_pipe_records_bound(uint64_t total, uint32_t block_size);
 
 /*
  * Write the .BRa chunk records of nblocks encoded blocks (bra_gpu_encode_blocks output) back to
@@ -217,9 +220,13 @@ int bra_gpu_decompress_chunks_host(bra_gpu_ctx_t* ctx, const uint8_t* h_stream, 
  * jobs are done, with the rest of the batch still queued; h_in may be refilled from then on.
  * bra_gpu_compress_chunks_collect waits for the slot's batch, copies its chunk records into h_out on
  * the output-copy stream and returns what bra_gpu_compress_chunks_host returns (1 smaller than the
- * input, 0 not smaller, -2 out_cap too small: *out_size = the bytes needed, -1 error); a slot is
+ * input, 0 not smaller, -2 out_cap too small: *out_size = the bytes needed and the batch stays in
+ * the slot, so a second collect with a larger buffer returns it; -1 error); a slot is
  * collected before it is submitted again.  Collect with h_out NULL drains the slot: it waits for the
- * submitted batch and drops it, and drops a staged copy.  The overlapped order: stage(k + 1) before submit(k)
+ * submitted batch and drops it, and drops a staged copy.  Other calls on the context may be made
+ * while a batch is in flight: a call on a caller-supplied stream waits on the device for the
+ * in-flight batches, and the next submit for the last such call (they share the context's work
+ * buffers).  The overlapped order: stage(k + 1) before submit(k)
  * (batch k + 1's input arrives while batch k's kernels run), then collect(k - 1) (its records return
  * under batch k's kernels).  Host buffers from bra_gpu_host_alloc (pinned) make the copies
  * asynchronous; bra_gpu_host_free releases them.

@@ -24,7 +24,7 @@ def test_library_loads_and_exports_header_symbols():
     out = subprocess.check_output(["nm", "-D", "--defined-only", bra.LIB_PATH], text=True)
     exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
     declared = _header_functions()
-    assert len(declared) == 46
+    assert len(declared) == 47
     missing = [f for f in declared if f not in exported]
     assert not missing, missing
     assert sorted(bra.ABI_SYMBOLS) == declared
