@@ -634,7 +634,12 @@ static bool decode_records_serial(bra_io_file_t* dst, const char* fn, const uint
 {
     const uint64_t hsz = BRA_BWT_INDEX_BYTES + sizeof(bra_huffman_t);
     uint64_t       p   = 0;
-    for (uint32_t r = 0; r < recs; ++r)
+    // the reference contract of bra_bwt_decode2 asks for a transform buffer (bra_bwt.c:137)
+    bra_bwt_index_t* trans = (bra_bwt_index_t*) malloc(CHUNK_SIZE * sizeof(bra_bwt_index_t));
+    if (trans == NULL)
+        return false;
+    bool ok = true;
+    for (uint32_t r = 0; ok && r < recs; ++r)
     {
         bra_io_chunk_header_t h = {.primary_index = 0};
         h.primary_index         = (bra_bwt_index_t) stream[p] | (bra_bwt_index_t) stream[p + 1] << 8 | (bra_bwt_index_t) stream[p + 2] << 16;
@@ -644,7 +649,8 @@ static bool decode_records_serial(bra_io_file_t* dst, const char* fn, const uint
         if (huf == NULL)
         {
             bra_log_error("unable to decode huffman file: %s ", fn);
-            return false;
+            ok = false;
+            break;
         }
         uint8_t*   rle = NULL;
         size_t     s   = 0;
@@ -653,7 +659,8 @@ static bool decode_records_serial(bra_io_file_t* dst, const char* fn, const uint
         if (!rok)
         {
             bra_log_error("unable to decode RLE in %s", fn);
-            return false;
+            ok = false;
+            break;
         }
         *orig += s;
         if (s > CHUNK_SIZE)
@@ -662,24 +669,30 @@ static bool decode_records_serial(bra_io_file_t* dst, const char* fn, const uint
             // check; here it protects the tmp buffer
             bra_log_error("decoded chunk size %zu exceeds BRA_MAX_CHUNK_SIZE in %s", s, fn);
             free(rle);
-            return false;
+            ok = false;
+            break;
         }
         if (h.primary_index >= s)
         {
             bra_log_error("invalid primary index (%u) for chunk size %zu in %s", h.primary_index, s, fn);
             free(rle);
-            return false;
+            ok = false;
+            break;
         }
         bra_mtf_decode2(rle, s, tmp);
         free(rle);
-        bra_bwt_decode2(tmp, (bra_bwt_index_t) s, h.primary_index, NULL, tmp + CHUNK_SIZE);
+        bra_bwt_decode2(tmp, (bra_bwt_index_t) s, h.primary_index, trans, tmp + CHUNK_SIZE);
         me->crc32 = bra_crc32c(&h, sizeof(bra_io_chunk_header_t), me->crc32);
         me->crc32 = bra_crc32c(tmp + CHUNK_SIZE, s, me->crc32);
         if (dst != NULL && !bra_io_file_write(dst, tmp + CHUNK_SIZE, s))
-            return false;
+        {
+            ok = false;
+            break;
+        }
         p += hsz + h.huffman.encoded_size;
     }
-    return true;
+    free(trans);
+    return ok;
 }
 
 /* The decoded output of batch k is written to dst on a helper thread while batch k + 1 is read and

@@ -19,6 +19,9 @@ import os
 from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# BRA_ORACLE_DIR: load liboracle.so / libbraref.so / libbralib.so from another build of them (the
+# host-sanitizer build, oracle/_ref/asan, `make -C oracle asan`; tests/test_asan.py)
+_ALT = os.environ.get("BRA_ORACLE_DIR")
 _libc = C.CDLL(None)
 _libc.free.argtypes = [C.c_void_p]
 
@@ -67,7 +70,7 @@ class Oracle:
     """The restatement (bra_oracle.c).  Method names follow the reference encoder API."""
 
     def __init__(self, path: str | None = None):
-        path = path or os.path.join(_HERE, "liboracle.so")
+        path = path or os.path.join(_ALT or _HERE, "liboracle.so")
         self.lib = L = C.CDLL(path)
         u8p, u32p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint32)
         L.orc_bwt_encode.argtypes = [u8p, C.c_uint32, u32p, u8p, u32p]
@@ -208,7 +211,7 @@ class Oracle:
 # --------------------------------------------------------------------------------------------
 # Reference encoders compiled from /root/reference (oracle/_ref/libbraref.so)
 # --------------------------------------------------------------------------------------------
-REF_PATH = os.path.join(_HERE, "_ref", "libbraref.so")
+REF_PATH = os.path.join(_ALT or os.path.join(_HERE, "_ref"), "libbraref.so")
 
 
 def have_ref() -> bool:
@@ -323,7 +326,7 @@ class Reference:
 # --------------------------------------------------------------------------------------------
 # The whole reference lib_bra (oracle/_ref/libbralib.so): CRC32C and the chunk loop
 # --------------------------------------------------------------------------------------------
-LIB_PATH = os.path.join(_HERE, "_ref", "libbralib.so")
+LIB_PATH = os.path.join(_ALT or os.path.join(_HERE, "_ref"), "libbralib.so")
 
 
 def have_reflib() -> bool:
