@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--profile-all", action="store_true", help="time every kernel during the timed steps")
     ap.add_argument("--no-secondary", action="store_true", help="skip the decode and PCIe-inclusive measurements")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--gather-mode", default="exact", choices=["exact", "bound"],
+                    help="N > 1: payloads gathered at their exact sizes (one size all_gather per step) or at the geometry's bound")
     ap.add_argument("--pcie-batches", type=int, default=4, help="batches of the split transfer-inclusive encode (two contexts)")
     ap.add_argument("--pcie-stream", type=int, default=4, help="batches of the streamed transfer-inclusive encode (pipelined API)")
     return ap.parse_args()
@@ -473,9 +475,14 @@ def main():
     per_batch = max(1, args.batch_bytes // bs)
     batches = [(b0, min(nb, b0 + per_batch)) for b0 in range(0, nb, per_batch)]
     off_b = torch.empty((per_batch + 1,), dtype=torch.int64, device=dev)
-    # sizes from the geometry: the payloads travel at their bound, no rank waits on the host for the
-    # others' encodes (unmeasured on hardware until a driver SCALE record exists)
-    gather = dmod.ChunkGather(dist, rank, world, geometry=(global_total, bs)) if world > 1 else None
+    # exact sizes (default): one all_gather of (payload bytes, block count) per step, then each rank's
+    # compressed bytes only.  The host waits for that all_gather, but the gather of step k is issued
+    # after step k + 1's encode has been queued, so the GPU is never idle for it.  "bound": the sizes
+    # follow from the geometry and the payloads travel at their bound (about 1.0x the shard's input
+    # instead of its compressed size), no host wait.  (Unmeasured on hardware until a driver SCALE
+    # record exists.)
+    geo = (global_total, bs) if args.gather_mode == "bound" else None
+    gather = dmod.ChunkGather(dist, rank, world, geometry=geo) if world > 1 else None
     work_stream = torch.cuda.Stream()
     gather_stream = torch.cuda.Stream() if world > 1 else None
     result = {}
@@ -652,7 +659,7 @@ def main():
                 "global_bytes": global_total,
                 "batches_per_rank": len(batches),
                 "parallelism": f"dp{world}: block b on GPU b mod {world} (round robin)"
-                               + ((", RCCL gather of compressed chunks + CRC shares to rank 0" if args.backend == "nccl" else
+                               + ((f", RCCL gather of compressed chunks + CRC shares to rank 0 ({args.gather_mode} sizes)" if args.backend == "nccl" else
                                   f", {args.backend} gather through host copies (ranks sharing a GPU: rehearsal, not a scaling number)")
                                  if world > 1 else ""),
             },
@@ -681,6 +688,11 @@ def main():
             "secondary": secondary,
             "cpu_baseline": None,
         }
+        if world > 1:
+            # bytes that crossed to rank 0 per step (the last gather: headers, offsets, CRC shares,
+            # payloads at their exact sizes or at the geometry's bound, --gather-mode)
+            line["gather_bytes_per_step"] = int(gather.last_bytes)
+            line["gather_mode"] = args.gather_mode
         if args.profile_all:
             line["kernels"] = {k: {"ms": round(v[0] / max(1, v[1]), 4), "launches": v[1], "GBps": round(v[2] / max(v[0], 1e-9) / 1e6, 1)}
                                for k, v in prof.items() if v[1]}

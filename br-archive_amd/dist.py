@@ -69,6 +69,7 @@ class ChunkGather:
         self.dist, self.rank, self.world = dist, rank, world
         self.bufs: dict[int, tuple] = {}
         self.bounds = None
+        self.last_bytes = 0
         if geometry is not None:
             total, bs = geometry
             nb = num_blocks(total, bs)
@@ -126,6 +127,8 @@ class ChunkGather:
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        # bytes that crossed to rank 0 in this call (headers, offsets, CRC shares, payloads)
+        self.last_bytes = sum(nbs[r] * HEADER_BYTES + (nbs[r] + 1) * 8 + 4 + sizes[r] for r in range(1, world))
         if rank != 0:
             return None
         parts = [(hdr, off, pay[: sizes[0]], crc)]
