@@ -712,11 +712,11 @@ def main():
                     line["roofline"]["traffic"] = k.get("hbm_bytes_per_launch")
                     line["roofline"]["traffic_source"] = f"profiles/pmc_summary.json workloads.{args.kind}_{bs} ({wl.get('source', '?')})"
                 # the compute side of the job kernels (sorting networks and string compares, not HBM
-                # bound): VALU issue fraction of the chip and VALU instructions per input byte of the
-                # launch (one launch covers the whole batch), from the SQ / GRBM passes
-                # (valu_frac = 4 x SQ_ACTIVE_INST_VALU quad-cycles / the chip's VALU issue cycles: about 1
-                # means VALU-issue saturated; valu_insts_per_element = lane instructions per element the
-                # launch covers: the job slots' 11 algorithmic bytes per element, else the batch)
+                # bound): the fraction of the chip's calibrated VALU issue ceiling the launch used
+                # (valu_frac = SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs x 0.380 wave-instructions
+                # per SIMD per cycle, the rate scripts/micro/valu_cal.hip reaches: profiles/
+                # r06_valu_calibration.json) and VALU lane instructions per element the launch covers
+                # (the job slots: their 11 algorithmic bytes per element; else the batch)
                 valu = {}
                 for slot in dict.fromkeys((dominant, "bwt.jobs", "bwt.mjobs")):
                     e = wl.get("kernels", {}).get(slot, {})
@@ -727,6 +727,10 @@ def main():
                                       "valu_insts_per_element": round(e.get("valu_insts_per_launch", 0) * 64 / max(1.0, elems), 1)}
                 if dominant in valu:
                     line["roofline"].update(valu[dominant])
+                    if "jobs" in dominant and valu[dominant]["valu_frac"] > line["roofline"]["frac"]:
+                        # the job kernels: VALU issue, not HBM, is the resource they use most of;
+                        # achieved / peak / frac stay the HBM figures
+                        line["roofline"]["bound"] = "valu"
                 if valu:
                     line["roofline"]["valu"] = valu
             except (OSError, ValueError, AttributeError):

@@ -14,7 +14,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_summary import main as summarize  # noqa: E402
+from pmc_summary import main as summarize, valu_frac  # noqa: E402
 
 SLOTS = {
     "bwt.pack": ["k_alpha", "k_pack_desc", "k_pack"],
@@ -48,10 +48,9 @@ if __name__ == "__main__":
         if all("valu_insts_per_launch" in e for e in have):
             ks["valu_insts_per_launch"] = int(sum(e["valu_insts_per_launch"] for e in have))
         if all("valu_frac" in e for e in have):
-            quads = sum(e["active_valu_quads_per_launch"] for e in have)
-            cyc = sum(e["gui_active_per_launch"] for e in have) / 8
-            ks["valu_frac"] = round(4 * quads / (cyc * 1024), 4)
+            ks["valu_frac"] = valu_frac(sum(e["valu_insts_per_launch"] for e in have), sum(e["gui_active_per_launch"] for e in have))
     res["workloads"][key] = entry
+    res["valu_frac_basis"] = "SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs x 0.380): profiles/r06_valu_calibration.json"
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for s_, e in entry["kernels"].items():
         print(f"{key} {s_:14s} {e['hbm_bytes_per_launch'] / 1e6:10.1f} MB per launch")

@@ -3,11 +3,13 @@
 usage: pmc_summary.py <run_dir>  -- reads <run_dir>/{fetch,write,sq1,grbm}/run_counter_collection.csv.
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950 FETCH_SIZE reports half of the bytes of
 wide coalesced reads (MI355X_MICROARCH.md, HBM section), so hbm_bytes = 2 * FETCH + WRITE.
-VALU: SQ_INSTS_VALU = wave-level VALU instructions issued; SQ_ACTIVE_INST_VALU counts quad-cycles
-(MI355X_MICROARCH.md, "s_memtime tick vs SQ PMC units") over all waves; GRBM_GUI_ACTIVE is summed
-over the 8 XCDs, so a dispatch lasts GRBM_GUI_ACTIVE / 8 cycles and the chip has 256 CUs x 4 SIMDs
-= 1024 VALU issue ports: valu_frac = 4 * SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 * 1024), the
-fraction of the chip's VALU issue cycles the dispatch used.
+VALU: SQ_INSTS_VALU = wave-level VALU instructions issued; GRBM_GUI_ACTIVE is summed over the 8 XCDs,
+so a dispatch lasts GRBM_GUI_ACTIVE / 8 cycles on 256 CUs x 4 SIMDs = 1024 VALU issue ports.
+valu_frac = SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 * 1024 * R_MAX), where R_MAX is the issue rate a
+VALU-only kernel at full occupancy reaches (scripts/micro/valu_cal.hip, profiles/r06_valu_calibration.json:
+0.380 wave-instructions per SIMD per cycle): 1.0 = the calibrated VALU issue ceiling.  (Round 5 used
+4 * SQ_ACTIVE_INST_VALU / (cycles * 1024), which reads 1.52 on the calibration kernel: SQ_ACTIVE_INST_VALU
+equals SQ_INSTS_VALU there, one count per wave-instruction.)
 """
 import collections
 import csv
@@ -17,6 +19,19 @@ import re
 import sys
 
 N_SIMD = 256 * 4  # VALU issue ports: 256 CUs x 4 SIMDs
+
+
+def valu_rate_max():
+    """Calibrated VALU issue ceiling (wave-instructions per SIMD per cycle)."""
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r06_valu_calibration.json")
+    try:
+        return float(json.load(open(p))["valu_wave_insts_per_simd_per_cycle_max"])
+    except (OSError, KeyError, ValueError):
+        return 0.3804
+
+
+def valu_frac(insts, gui_active):
+    return round(insts / (gui_active / 8 * N_SIMD * valu_rate_max()), 4)
 
 
 def short(name):
@@ -55,8 +70,8 @@ def main(d):
         g = gr.get(k)
         if g and g.get("GRBM_GUI_ACTIVE"):
             e["gui_active_per_launch"] = sum(g["GRBM_GUI_ACTIVE"]) / len(g["GRBM_GUI_ACTIVE"])
-            if "active_valu_quads_per_launch" in e:
-                e["valu_frac"] = round(4 * e["active_valu_quads_per_launch"] / (e["gui_active_per_launch"] / 8 * N_SIMD), 4)
+            if "valu_insts_per_launch" in e:
+                e["valu_frac"] = valu_frac(e["valu_insts_per_launch"], e["gui_active_per_launch"])
         out[k] = e
     return out
 
