@@ -41,6 +41,9 @@ constexpr uint32_t RD_WIN   = RD_WAVES * RD_SUB;    // 16 KiB window
 constexpr uint32_t RD_HALO  = 256;                  // a literal's payload runs up to 128 bytes past its window
 constexpr uint32_t RD_LOAD  = (RD_WIN + RD_HALO) / 16;  // 16-byte loads per window (<= 2 per thread)
 constexpr uint32_t RD_NENT  = 129;                  // entry offsets into a segment: [0, 128]
+constexpr uint32_t PK_SH    = 11;                   // PK word: position (< RD_SUB + 129 < 2^11) | output bytes << 11
+constexpr uint32_t PK_POS   = (1u << PK_SH) - 1u;
+static_assert(RD_SUB + 129 <= PK_POS + 1 && (RD_SUB / 2 * 128 + 129) < (1u << (32 - PK_SH)), "PK fields");
 typedef uint4 __attribute__((aligned(1))) u128_u;
 
 __device__ __forceinline__ void wave_lds_sync()
@@ -82,8 +85,11 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                                                  uint32_t* __restrict__ out_size, RledSeg sg)
 {
     __shared__ uint4    win4[1 + (RD_WIN + RD_HALO) / 16];  // one 16-byte pad in front: unaligned output reads start up to 15 bytes early
-    __shared__ uint16_t NX[RD_WAVES][RD_SUB];  // successor (sub-window position; >= len: exit) / later: chain positions
-    __shared__ uint32_t SM[RD_WAVES][RD_SUB];  // output bytes to the exit / later: output offsets of the chain
+    // Per sub-window position: successor (sub-window position, >= len: the exit; < 2^11) | output
+    // bytes to the exit << 11 (< 2^17: at most 128 per two stream bytes); later the chain's controls:
+    // position | output offset << 11.  One word per position: a pointer-jumping round is one LDS read
+    // and one write per position (two of each with separate successor / count arrays).
+    __shared__ uint32_t PK[RD_WAVES][RD_SUB];
     __shared__ uint32_t sub_entry[RD_WAVES], sub_out[RD_WAVES], sub_tot[RD_WAVES];
     __shared__ uint32_t sh_E, sh_O;
     const uint8_t*  win   = reinterpret_cast<const uint8_t*>(win4 + 1);
@@ -143,36 +149,30 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             const uint32_t sb  = k * RD_SUB;
             const uint32_t rem = size - w0;
             const uint32_t len = rem > sb ? min(RD_SUB, rem - sb) : 0u;
-            uint32_t       nx0[RD_PER], nx[RD_PER], sm[RD_PER];
+            uint32_t       nx0[RD_PER], v[RD_PER];
 #pragma unroll
             for (int m = 0; m < (int) RD_PER; ++m)
             {
                 const uint32_t p = m * 64 + lane;
                 const uint32_t c = win[sb + p];
                 nx0[m]           = p + ctl_step(c);
-                nx[m]            = nx0[m];
-                sm[m]            = ctl_prod(c);
+                v[m]             = nx0[m] | ctl_prod(c) << PK_SH;
                 if (p < len)
-                {
-                    NX[k][p] = (uint16_t) nx[m];
-                    SM[k][p] = sm[m];
-                }
+                    PK[k][p] = v[m];
             }
             wave_lds_sync();
             while (true)
             {
                 bool     act = false;
-                uint32_t nn[RD_PER], ss[RD_PER];
+                uint32_t nn[RD_PER];
 #pragma unroll
                 for (int m = 0; m < (int) RD_PER; ++m)
                 {
-                    const uint32_t p = m * 64 + lane;
-                    nn[m]            = nx[m];
-                    ss[m]            = 0;
-                    if (p < len && nx[m] < len)
+                    const uint32_t p = m * 64 + lane, nx = v[m] & PK_POS;
+                    nn[m]            = v[m];
+                    if (p < len && nx < len)
                     {
-                        nn[m] = NX[k][nx[m]];
-                        ss[m] = SM[k][nx[m]];
+                        nn[m] = (v[m] & ~PK_POS) + PK[k][nx];  // successor's successor, counts added
                         act   = true;
                     }
                 }
@@ -183,12 +183,10 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                 for (int m = 0; m < (int) RD_PER; ++m)
                 {
                     const uint32_t p = m * 64 + lane;
-                    if (p < len && nx[m] < len)
+                    if (p < len && (v[m] & PK_POS) < len)
                     {
-                        nx[m] = nn[m];
-                        sm[m] += ss[m];
-                        NX[k][p] = (uint16_t) nx[m];
-                        SM[k][p] = sm[m];
+                        v[m]     = nn[m];
+                        PK[k][p] = v[m];
                     }
                 }
                 wave_lds_sync();
@@ -208,8 +206,9 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                         const uint32_t ql = rem > qb ? min(RD_SUB, rem - qb) : 0u;
                         if (e - qb < ql)
                         {
-                            mo += SM[q][e - qb];
-                            e = qb + NX[q][e - qb];
+                            const uint32_t x = PK[q][e - qb];
+                            mo += x >> PK_SH;
+                            e = qb + (x & PK_POS);
                         }
                     }
                     me = e - RD_WIN;
@@ -228,9 +227,9 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                     uint32_t t        = 0;
                     if (e - qb < ql)
                     {
-                        const uint32_t el = e - qb;
-                        t                 = SM[q][el];
-                        e                 = qb + NX[q][el];
+                        const uint32_t x = PK[q][e - qb];
+                        t                = x >> PK_SH;
+                        e                = qb + (x & PK_POS);
                     }
                     sub_tot[q] = t;
                     o += t;
@@ -247,8 +246,8 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             uint32_t       ncon = 0;
             if (ent < len)
             {
-                const uint32_t sm_entry = SM[k][ent];
-                wave_lds_sync();  // everyone read SM[k][ent] before the compaction overwrites it
+                const uint32_t sm_entry = PK[k][ent] >> PK_SH;
+                wave_lds_sync();  // everyone read PK[k][ent] before the compaction overwrites it
                 uint32_t e = ent;
 #pragma unroll
                 for (int m = 0; m < (int) RD_PER; ++m)
@@ -264,8 +263,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                     if ((on >> lane) & 1)
                     {
                         const uint32_t idx = ncon + (uint32_t) __popcll(on & below);
-                        NX[k][idx]         = (uint16_t) (m * 64 + lane);
-                        SM[k][idx]         = sm_entry - sm[m];  // output offset inside the sub-window's range
+                        PK[k][idx]         = (m * 64 + lane) | (sm_entry - (v[m] >> PK_SH)) << PK_SH;  // position | output offset inside the sub-window's range
                     }
                     ncon += (uint32_t) __popcll(on);
                 }
@@ -282,13 +280,13 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                     while (lo < hi)
                     {
                         const uint32_t mid = (lo + hi + 1) >> 1;
-                        if (SM[k][mid] <= o0)
+                        if ((PK[k][mid] >> PK_SH) <= o0)
                             lo = mid;
                         else
                             hi = mid - 1;
                     }
-                    uint32_t idx = lo, d = SM[k][idx], p = NX[k][idx];
-                    uint32_t dn = idx + 1 < ncon ? SM[k][idx + 1] : 0xFFFFFFFFu;
+                    uint32_t idx = lo, d = PK[k][idx] >> PK_SH, p = PK[k][idx] & PK_POS;
+                    uint32_t dn = idx + 1 < ncon ? PK[k][idx + 1] >> PK_SH : 0xFFFFFFFFu;
                     uint32_t wv[4] = {0, 0, 0, 0};
                     const uint32_t nb = min(16u, tot - o0);
                     // one piece per control covering part of the lane's 16 bytes: a run fills its
@@ -302,8 +300,8 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                         {
                             ++idx;
                             d  = dn;
-                            p  = NX[k][idx];
-                            dn = idx + 1 < ncon ? SM[k][idx + 1] : 0xFFFFFFFFu;
+                            p  = PK[k][idx] & PK_POS;
+                            dn = idx + 1 < ncon ? PK[k][idx + 1] >> PK_SH : 0xFFFFFFFFu;
                         }
                         const uint32_t at = sb + p;
                         const uint32_t c  = win[at];

@@ -99,3 +99,35 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def tie_stats(kind="text", bs=1 << 20):
+    """Round-1 ties of the wave / workgroup jobs for a key of K rotation bits after the job depth."""
+    kid = {"text": bra.SYNTH_TEXT, "random": bra.SYNTH_RANDOM, "sym16": bra.SYNTH_SYM16}[kind]
+    blk = bra.synth_fill(kid, bs, bs)
+    keys, b = packed_bytes(blk)
+    order = np.lexsort(keys.T[::-1])
+    jobs, k = jobs_of(keys, order)
+    for bits in (24, 32, 48, 56):
+        nb = bits // 8
+        tied = tot = 0
+        gsz = []
+        for s, e, d in jobs:
+            if d + nb > NB:
+                continue
+            sub = k[s:e, d:d + nb]
+            # rows equal to a neighbour (sorted order): tied after a round-1 key of `bits` bits
+            eq = np.all(sub[1:] == sub[:-1], axis=1)
+            t = np.zeros(e - s, bool)
+            t[1:] |= eq
+            t[:-1] |= eq
+            tied += int(t.sum())
+            tot += e - s
+            # group sizes
+            heads = np.concatenate([[True], ~eq])
+            ids = np.cumsum(heads)
+            cnt = np.bincount(ids)[1:]
+            gsz.extend(cnt[cnt > 1].tolist())
+        g = np.array(gsz) if gsz else np.array([0])
+        print(f"{kind}: round-1 key of {bits} bits: tied {tied / max(1, tot):.1%} of {tot} job elements; tied groups {len(gsz)}, "
+              f"mean size {g.mean():.1f}, p90 {np.percentile(g, 90):.0f}, max {g.max()}, elements in groups > 64: {g[g > 64].sum() / max(1, tot):.1%}")
