@@ -78,6 +78,14 @@ struct RledSeg
     uint2*   state;  // [b * nseg + j] = (entry offset, block output offset) (k_rled_link)
 };
 
+#ifdef BRA_RLED_TIMING
+// measurement build only: shader clocks of wave 0 per phase, summed over the windows (load + 1, 2, 3)
+__device__ unsigned long long g_rled_t[4];
+#define RT_NOW() (threadIdx.x == 0 ? (unsigned long long) clock64() : 0ull)
+#else
+#define RT_NOW() 0ull
+#endif
+
 template <bool MAP>
 __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_base,
                                                  const uint32_t* __restrict__ in_size, uint32_t nblocks, uint8_t* __restrict__ out,
@@ -90,7 +98,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
     // position | output offset << 11.  One word per position: a pointer-jumping round is one LDS read
     // and one write per position (two of each with separate successor / count arrays).
     __shared__ uint32_t PK[RD_WAVES][RD_SUB];
-    __shared__ uint32_t sub_entry[RD_WAVES], sub_out[RD_WAVES], sub_tot[RD_WAVES];
+    __shared__ uint32_t sub_entry[RD_WAVES], sub_out[RD_WAVES], sub_tot[RD_WAVES], sub_ncon[RD_WAVES];
     __shared__ uint32_t sh_E, sh_O;
     const uint8_t*  win   = reinterpret_cast<const uint8_t*>(win4 + 1);
     const uint32_t* win32 = reinterpret_cast<const uint32_t*>(win4 + 1);
@@ -125,6 +133,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
             const uint32_t t = threadIdx.x + h * RD_TPB;
             pf[h]            = t < RD_LOAD ? load16(src, size, seg0 + t * 16) : make_uint4(0, 0, 0, 0);
         }
+        [[maybe_unused]] unsigned long long rt[4] = {0, 0, 0, 0}, rc = RT_NOW();
         for (uint32_t w0 = seg0; w0 < seg1; w0 += RD_WIN)
         {
             __syncthreads();  // previous window fully consumed
@@ -161,6 +170,13 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                     PK[k][p] = v[m];
             }
             wave_lds_sync();
+#ifdef BRA_RLED_TIMING
+            {
+                const unsigned long long t = RT_NOW();
+                rt[0] += t - rc;
+                rc = t;
+            }
+#endif
             while (true)
             {
                 bool     act = false;
@@ -192,6 +208,13 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                 wave_lds_sync();
             }
             __syncthreads();
+#ifdef BRA_RLED_TIMING
+            {
+                const unsigned long long t = RT_NOW();
+                rt[1] += t - rc;
+                rc = t;
+            }
+#endif
 
             // ---- 2. entries and output offsets of the sub-windows ----
             if (MAP)
@@ -238,11 +261,16 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                 sh_O = o;
             }
             __syncthreads();
+#ifdef BRA_RLED_TIMING
+            {
+                const unsigned long long t = RT_NOW();
+                rt[2] += t - rc;
+                rc = t;
+            }
+#endif
 
             // ---- 3. walk the chain through this sub-window, compact it, write the output ----
-            const uint32_t ent = sub_entry[k];
-            const uint32_t tot = sub_tot[k];
-            const uint32_t ob0 = sub_out[k];
+            const uint32_t ent  = sub_entry[k];
             uint32_t       ncon = 0;
             if (ent < len)
             {
@@ -269,41 +297,69 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                 }
                 wave_lds_sync();
             }
-            // output bytes [ob0, ob0 + tot) of the block: 16 per lane per round
-            for (uint32_t r0 = 0; r0 < tot; r0 += 64 * 16)
+            if (lane == 0)
+                sub_ncon[k] = ncon;
+            __syncthreads();  // every sub-window's control list is compacted
+            // Output bytes of the whole window, [sub_out[0], sh_O), 16 per thread per round over the
+            // workgroup (a run-dense sub-window decodes to up to 64 KiB, a literal-dense one to about
+            // 1 KiB: writing each sub-window's range with its own wave left the workgroup waiting for
+            // its heaviest wave at the next barrier).  A thread's 16 bytes start in the last
+            // sub-window holding output at or before them and may continue into the next ones.
+            const uint32_t ow0 = sub_out[0], otot = sh_O - ow0;
+            for (uint32_t r0 = 0; r0 < otot; r0 += RD_TPB * 16)
             {
-                const uint32_t o0 = r0 + lane * 16;  // relative to ob0
-                if (o0 < tot)
+                const uint32_t o0 = r0 + threadIdx.x * 16;  // relative to ow0
+                if (o0 < otot)
                 {
-                    // last control with offset <= o0
-                    uint32_t lo = 0, hi = ncon - 1;
+                    uint32_t kk = 0;
+#pragma unroll
+                    for (uint32_t q = 1; q < RD_WAVES; ++q)
+                        if (sub_out[q] - ow0 <= o0 && sub_tot[q] > 0)
+                            kk = q;
+                    uint32_t base = sub_out[kk] - ow0, nk = sub_ncon[kk], tk = sub_tot[kk];
+                    // last control of sub-window kk with offset <= o0 - base
+                    uint32_t lo = 0, hi = nk - 1;
                     while (lo < hi)
                     {
                         const uint32_t mid = (lo + hi + 1) >> 1;
-                        if ((PK[k][mid] >> PK_SH) <= o0)
+                        if ((PK[kk][mid] >> PK_SH) <= o0 - base)
                             lo = mid;
                         else
                             hi = mid - 1;
                     }
-                    uint32_t idx = lo, d = PK[k][idx] >> PK_SH, p = PK[k][idx] & PK_POS;
-                    uint32_t dn = idx + 1 < ncon ? PK[k][idx + 1] >> PK_SH : 0xFFFFFFFFu;
+                    uint32_t idx = lo, d = PK[kk][idx] >> PK_SH, p = PK[kk][idx] & PK_POS;
+                    uint32_t dn = idx + 1 < nk ? PK[kk][idx + 1] >> PK_SH : tk;
                     uint32_t wv[4] = {0, 0, 0, 0};
-                    const uint32_t nb = min(16u, tot - o0);
-                    // one piece per control covering part of the lane's 16 bytes: a run fills its
+                    const uint32_t nb = min(16u, otot - o0);
+                    // one piece per control covering part of the thread's 16 bytes: a run fills its
                     // bytes with one value, a literal copies a 16-byte unaligned LDS read (5 dwords
                     // + alignbyte) positioned so that byte j of it is output byte j; bytes outside
                     // [j, j + n) are kept by a bitfield insert
                     for (uint32_t j = 0; j < nb;)
                     {
-                        const uint32_t o = o0 + j;
+                        uint32_t o = o0 + j - base;  // relative to sub-window kk's output
                         while (o >= dn)
                         {
-                            ++idx;
-                            d  = dn;
-                            p  = PK[k][idx] & PK_POS;
-                            dn = idx + 1 < ncon ? PK[k][idx + 1] >> PK_SH : 0xFFFFFFFFu;
+                            if (idx + 1 < nk)
+                            {
+                                ++idx;
+                                d  = dn;
+                                p  = PK[kk][idx] & PK_POS;
+                                dn = idx + 1 < nk ? PK[kk][idx + 1] >> PK_SH : tk;
+                            }
+                            else
+                            {
+                                // past sub-window kk's output: the next one holding output
+                                do
+                                    ++kk;
+                                while (sub_tot[kk] == 0);
+                                base = sub_out[kk] - ow0, nk = sub_ncon[kk], tk = sub_tot[kk];
+                                o    = o0 + j - base;
+                                idx = 0, d = 0, p = PK[kk][0] & PK_POS;
+                                dn = nk > 1 ? PK[kk][1] >> PK_SH : tk;
+                            }
                         }
-                        const uint32_t at = sb + p;
+                        const uint32_t at = kk * RD_SUB + p;
                         const uint32_t c  = win[at];
                         const uint32_t n  = min(dn - o, nb - j);
                         uint32_t       v[4];
@@ -314,9 +370,9 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                         }
                         else
                         {
-                            const int32_t  base = (int32_t) (at + 1 + (o - d)) - (int32_t) j;  // >= -15
-                            const int32_t  a4   = (base >> 2);                               // floor
-                            const uint32_t sh   = (uint32_t) base & 3u;
+                            const int32_t  base4 = (int32_t) (at + 1 + (o - d)) - (int32_t) j;  // >= -15
+                            const int32_t  a4    = (base4 >> 2);                               // floor
+                            const uint32_t sh    = (uint32_t) base4 & 3u;
                             uint32_t       W[5];
 #pragma unroll
                             for (int i = 0; i < 5; ++i)
@@ -336,7 +392,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                         }
                         j += n;
                     }
-                    const uint64_t a = (uint64_t) ob0 + o0;  // block output offset
+                    const uint64_t a = (uint64_t) ow0 + o0;  // block output offset
                     uint8_t*       q = dst + a;
                     if (nb == 16 && a + 16 <= cap)  // one (unaligned) 16-byte store: the output offsets have any alignment
                         *reinterpret_cast<u128_u*>(q) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
@@ -346,7 +402,19 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
                                 q[j] = (uint8_t) (wv[j >> 2] >> (8 * (j & 3)));
                 }
             }
+#ifdef BRA_RLED_TIMING
+            {
+                const unsigned long long t = RT_NOW();
+                rt[3] += t - rc;
+                rc = t;
+            }
+#endif
         }
+#ifdef BRA_RLED_TIMING
+        if (threadIdx.x == 0)
+            for (int i = 0; i < 4; ++i)
+                atomicAdd(&g_rled_t[i], rt[i]);
+#endif
         __syncthreads();
         if (MAP)
         {
@@ -442,6 +510,15 @@ bool rle_decode_device(RleWorkspace& w, const uint32_t* h_in_size, const uint8_t
         hipLaunchKernelGGL(k_rled<false>, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(RD_TPB), 0, s, d_in, d_in_base, d_in_size, nblocks,
                            d_out, d_out_base, d_out_cap, d_out_size, sg);
     BRA_HIP_CHECK(hipGetLastError());
+#ifdef BRA_RLED_TIMING
+    {
+        unsigned long long t[4] = {0, 0, 0, 0}, z[4] = {0, 0, 0, 0};
+        if (hipStreamSynchronize(s) == hipSuccess && hipMemcpyFromSymbol(t, HIP_SYMBOL(g_rled_t), sizeof t) == hipSuccess)
+            fprintf(stderr, "rled clocks (wave 0, summed): load+ptr-init %llu  pointer-jumping %llu  entries %llu  walk+write %llu\n", t[0], t[1], t[2],
+                    t[3]);
+        (void) hipMemcpyToSymbol(HIP_SYMBOL(g_rled_t), z, sizeof z);
+    }
+#endif
     return true;
 }
 
