@@ -77,6 +77,14 @@ struct BlockDesc
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// The wave's index in its workgroup, wave-uniform to the compiler: threadIdx.x >> 6 is not (the
+// compiler treats it as per-lane), so loops and branches on it ran under exec masks with VALU
+// compares and readfirstlanes; through readfirstlane they run on scalar registers.  Round 6, one
+// box, two A/B pairs: wave jobs 1.82 -> 1.73 ms (k_jobs 73 -> 55 VGPRs), MTF last occurrences
+// 0.139 -> 0.124 ms, the RLE decode's chain walk a 5-instruction scalar loop (it was 12 with
+// exec-mask juggling and s_nops).
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
 {
     uint32_t lo = (uint32_t) v, hi = (uint32_t) (v >> 32);

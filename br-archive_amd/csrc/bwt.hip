@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(TPB) k_hist(const Bucket* __restrict__ buckets
         // share a digit hit HIST_NC different banks (skewed digits: few lanes per address), and the
         // read-back of a lane's 4 digits is 4 x HIST_NC contiguous words.
         __shared__ __attribute__((aligned(16))) uint32_t hw[TPB / 64][256 * HIST_NC];
-        const uint32_t      wv = threadIdx.x >> 6, lane = (uint32_t) lane_id();
+        const uint32_t      wv = wave_id(), lane = (uint32_t) lane_id();
         uint32_t* const     hc = hw[wv];
         const uint32_t      cp = lane & (HIST_NC - 1);
         uint32_t            p  = tile_pos_wave(to, 0, ntiles, wv, TPB / 64);
@@ -759,7 +759,7 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
     __shared__ uint8_t        nx_s[SCAN_WAVES][256];
     __shared__ ScanWaveCounts cnt_s[SCAN_WAVES];
     __shared__ uint32_t       base_s[SCAN_WAVES][5];  // jobs, mjobs, big, tiles, groups
-    const int                 lane = lane_id(), w = threadIdx.x >> 6;
+    const int                 lane = lane_id(), w = (int) wave_id();
     const uint32_t            nbuckets = a.lin ? dev_count(&a.lin->n_big) : a.nbuckets;
     const uint32_t            bstride  = gridDim.x * SCAN_WAVES;
     for (uint32_t b0 = blockIdx.x * SCAN_WAVES; b0 < nbuckets; b0 += bstride)
@@ -1654,7 +1654,16 @@ template <int W>
 struct JobLds
 {
     static constexpr int KD = JobGeom<W>::KD;
-    uint64_t kh[256 * W];   // neighbour keys, merge levels, compaction scratch
+#ifdef BRA_JOB_AUDIT
+    static constexpr int KH = 256 * W;  // the audit keeps a sort's output here
+#else
+    // Wave jobs use kh only for the small sorts (<= 128 keys) and as 32-bit compaction scratch, so
+    // 1 KiB instead of 2: 4.6 KiB per wave fits 8 four-wave workgroups per CU (8 waves per SIMD)
+    // where 5.6 KiB fitted 7.  (Measured equal, round 6: 1.744 / 1.746 vs 1.749 / 1.740 ms -- the
+    // seventh wave already hides what occupancy can.)
+    static constexpr int KH = (W == 1) ? 128 : 256 * W;
+#endif
+    uint64_t kh[KH];        // neighbour keys, merge levels, small sorts; as uint32_t: compaction scratch
     uint64_t wx[256 * W];   // STRING: the 64 rotation bits after each element's round-1 key (the round-2 key bits)
     uint32_t v[256 * W];    // payload of every slot of the current round (the keys carry the slot)
     uint32_t nx[W];         // group-end scratch (the first head of each wave)
@@ -2560,7 +2569,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
                 {
                     const uint32_t c = wj * 256 + lane * 4 + r;
                     S.v[cx[r]]       = v[r];
-                    S.kh[cx[r]]      = ((uint64_t) (cx[r] - (c - g[r])) << 16) | pos[r];  // new group head | position
+                    reinterpret_cast<uint32_t*>(S.kh)[cx[r]] = ((cx[r] - (c - g[r])) << 16) | pos[r];  // new group head | position
                     if (round == 1)
                         S.wx[cx[r]] = key[r];
                 }
@@ -2626,7 +2635,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
             pos[r]           = c;
             if (c < T)
             {
-                const uint64_t gp = S.kh[c];
+                const uint32_t gp = reinterpret_cast<const uint32_t*>(S.kh)[c];
                 pos[r]            = (uint32_t) (gp & 0xFFFF);
                 key[r]            = make_key<W>((uint32_t) (gp >> 16), c, key[r]);
             }
@@ -2670,7 +2679,7 @@ __global__ void __launch_bounds__(256, JOB_MIN_WAVES) k_jobs(JobArgs a)
     __shared__ JobLds<1> lds[4];
     __shared__ uint32_t  xs[9];
     load_xseg(a, xs);
-    const int      wl  = threadIdx.x >> 6;
+    const int      wl  = (int) wave_id();
     const bool     dyn = a.xcd_major && a.jq;
     const JobRange R   = job_range(a, xs, wl, 4);
     JobClaim       c{xcc_id(), 0};
@@ -2736,7 +2745,7 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_mjobs(JobArgs a)
         __syncthreads();
         return __builtin_amdgcn_readfirstlane(claim[(k++) & 1]);
     };
-    const int wj = threadIdx.x >> 6;
+    const int wj = (int) wave_id();
     JT_INIT();
     [[maybe_unused]] unsigned long long tc = JT_NOW();
     uint32_t j = dyn ? next(0) : (R.first < R.end ? R.first : ~0u);
@@ -2801,7 +2810,7 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_sortnet_test(uint32_
         for (int r = 0; r < 4; ++r)
         {
             const uint32_t c = wj * 256 + lane * 4 + r;
-            S.kh[c]          = key[r];
+            S.wx[c]          = key[r];  // (wx: kh holds fewer slots in wave jobs)
             if (c < T)
                 atomicAdd(&S.v[(uint32_t) (key[r] & G::SMASK) & (256u * W - 1)], 1u);
         }
@@ -2812,7 +2821,7 @@ __global__ void __launch_bounds__(64 * W, MJOB_MIN_WAVES) k_sortnet_test(uint32_
         {
             const uint32_t c = wj * 256 + lane * 4 + r;
             if (c < T)
-                b |= (S.v[c] != 1u) || (c + 1 < T && S.kh[c] >= S.kh[c + 1]) || (c + 1 == T && T < 256u * W && S.kh[c + 1] != ~0ull);
+                b |= (S.v[c] != 1u) || (c + 1 < T && S.wx[c] >= S.wx[c + 1]) || (c + 1 == T && T < 256u * W && S.wx[c + 1] != ~0ull);
         }
         bad += __syncthreads_or(b) ? 1u : 0u;
     }

@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(64 * IBS_WAVES) k_ib_scatter3(const uint8_t* _
     __shared__ uint32_t sval[ITILE], sdst[ITILE];
     __shared__ uint32_t tmp[8];
     const uint8_t* tb   = reinterpret_cast<const uint8_t*>(tb4);
-    const uint32_t lane = (uint32_t) lane_id(), w = threadIdx.x >> 6;
+    const uint32_t lane = (uint32_t) lane_id(), w = wave_id();
     const uint64_t lt   = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
     {

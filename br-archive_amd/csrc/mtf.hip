@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_presence(const uint8_t* __restrict_
                                                       uint32_t* __restrict__ amask)
 {
     const int      lane = lane_id();
-    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t wave = wave_id();
     for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
     {
         const Piece P = segs[s];
@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_lastocc(const uint8_t* __restrict__
     constexpr int      ROW = 2 * LO_NC * LO_CS;  // >= 256: the full row of other blocks
     __shared__ __attribute__((aligned(16))) int32_t lo_s[TPB / 64][ROW];
     const int          lane = lane_id();
-    const uint32_t     wave = threadIdx.x >> 6;
+    const uint32_t     wave = wave_id();
     for (uint32_t s = blockIdx.x * (TPB / 64) + wave; s < nseg; s += gridDim.x * (TPB / 64))
     {
         const Piece    P    = segs[s];
@@ -907,7 +907,7 @@ __global__ void __launch_bounds__(TPB) k_mtf_encode_wave(const uint8_t* __restri
     __shared__ uint32_t mark_s[TPB / 64][64];  // byte p != 0: position p holds a symbol of the chunk
     __shared__ uint4    buf_s[TPB / 64][64];   // the segment: symbols, overwritten by their ranks
     const int      lane  = lane_id();
-    const uint32_t wave  = threadIdx.x >> 6;
+    const uint32_t wave  = wave_id();
     uint8_t*       pos   = reinterpret_cast<uint8_t*>(pos_s[wave]);
     uint8_t*       list  = reinterpret_cast<uint8_t*>(list_s[wave]);
     uint8_t*       mark  = reinterpret_cast<uint8_t*>(mark_s[wave]);

@@ -54,7 +54,7 @@ struct TileOff
 template <bool FWD, typename Op>
 __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t seed, uint32_t id, Op op, uint32_t* tmp, uint32_t* total = nullptr)
 {
-    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    const int      lane = lane_id(), w = (int) wave_id();
     uint32_t       ex;  // scan of the lanes before this one in scan order (id at the wave's first lane)
     const uint32_t inc = wave_scan<FWD>(v, id, op, &ex);
     if (lane == (FWD ? 63 : 0))
@@ -84,7 +84,7 @@ template <bool F1, bool F2, typename O1, typename O2>
 __device__ __forceinline__ void block_scan_pair(uint32_t v1, uint32_t seed1, uint32_t id1, O1 op1, uint32_t& ex1, uint32_t& all1, uint32_t v2,
                                                 uint32_t seed2, uint32_t id2, O2 op2, uint32_t& ex2, uint32_t& all2, uint32_t* tmp)
 {
-    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    const int      lane = lane_id(), w = (int) wave_id();
     uint32_t       e1, e2;
     const uint32_t i1 = wave_scan<F1>(v1, id1, op1, &e1);
     const uint32_t i2 = wave_scan<F2>(v2, id2, op2, &e2);
@@ -115,7 +115,7 @@ __device__ __forceinline__ void block_scan_pair(uint32_t v1, uint32_t seed1, uin
 // Exclusive sum over the workgroup with one barrier (tmp as in block_scan_pair: 4 dwords).
 __device__ __forceinline__ uint32_t block_sum_excl1(uint32_t v, uint32_t* tmp, uint32_t& total)
 {
-    const int      lane = lane_id(), w = threadIdx.x >> 6;
+    const int      lane = lane_id(), w = (int) wave_id();
     const uint32_t x    = wave_scan<true>(v, 0u, OpAdd());
     if (lane == 63)
         tmp[w] = x;

@@ -103,7 +103,7 @@ __global__ void __launch_bounds__(RD_TPB) k_rled(const uint8_t* __restrict__ in,
     const uint8_t*  win   = reinterpret_cast<const uint8_t*>(win4 + 1);
     const uint32_t* win32 = reinterpret_cast<const uint32_t*>(win4 + 1);
     const int      lane = lane_id();
-    const uint32_t k    = threadIdx.x >> 6;  // this wave's sub-window
+    const uint32_t k    = wave_id();  // this wave's sub-window (wave-uniform: its loops run on scalar registers)
     const uint64_t below = (1ull << lane) - 1ull;
     const uint64_t nunits = (uint64_t) nblocks * sg.nseg;
     for (uint64_t u = blockIdx.x; u < nunits; u += gridDim.x)
