@@ -3684,12 +3684,32 @@ static bool run_jobs(BwtWorkspace& w, const JobPhase& ph, hipStream_t s)
 // stop: it enqueues up to `lookahead` levels beyond the last slot it has read; once a read slot is
 // empty, the levels already enqueued after it find nothing to do and return at once.
 // Sub-buckets become jobs / fallback groups (appended to the call-wide lists, slot 0).
+// Workgroups of a level's scan; BRA_SCAN_GRID overrides (measurement).
+static uint32_t scan_grid_setting(uint32_t dflt)
+{
+    static const uint32_t v = [dflt] {
+        const char* e = getenv("BRA_SCAN_GRID");
+        return e ? std::max<uint32_t>(64u, (uint32_t) atoi(e)) : dflt;
+    }();
+    return v;
+}
+
+// Workgroups of the level kernels (histogram, scatter); BRA_LEVEL_GRID overrides (measurement).
+static int level_grid(int dflt)
+{
+    static const int v = [dflt] {
+        const char* e = getenv("BRA_LEVEL_GRID");
+        return e ? std::max(64, atoi(e)) : dflt;
+    }();
+    return v;
+}
+
 template <uint32_t MODE>
 static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_blocks, int cur, Group* groups_out, hipStream_t s,
                        uint32_t first_seq)
 {
     const size_t   lds    = tile_stage_bytes();
-    const int      grid   = w.grid;
+    const int      grid   = level_grid(w.grid);
     const uint32_t max_lv = (MODE == MODE_STRING) ? DCAP_BIG : RANK_KEYBYTES;  // the scans emit no bucket deeper than this
     uint32_t       seqs[MAX_LEVELS + 1] = {};
     seqs[1]                             = first_seq;
@@ -3740,7 +3760,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
 };
             {
                 BRA_PROF(P_BWT_SCAN, s);
-                hipLaunchKernelGGL(k_scan<MODE>, dim3(w.scan_grid), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
+                hipLaunchKernelGGL(k_scan<MODE>, dim3(scan_grid_setting(w.scan_grid)), dim3(64 * SCAN_WAVES), 0, s, a); BRA_DSYNC(s);
             }
             {
                 BRA_PROF(P_BWT_SCATTER, s);

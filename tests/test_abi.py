@@ -91,3 +91,21 @@ def test_lib_bra_links_against_gpu_library(lib):
         assert {"bra_bwt_encode2", "bra_mtf_encode2", "bra_rle_encode", "bra_huffman_encode", "bra_huffman_chunk_free"} <= need
     else:  # the batched front end calls the batch ABI
         assert {"bra_gpu_compress_chunks_stage", "bra_gpu_compress_chunks_submit", "bra_gpu_compress_chunks_collect", "bra_gpu_decompress_chunks_host"} <= need
+
+
+def test_pipe_records_bound_covers_every_chunk():
+    """bra_gpu_pipe_records_bound (host arithmetic, no device): at least the on-disk record of every
+    chunk at its RLE capacity (n + ceil(n / 128) + 16 payload bytes + 267 header bytes) and at most
+    about 1.01x the batch plus the headers."""
+    bra = importlib.import_module("br-archive_amd")
+    lib = bra.lib
+    cs = bra.MAX_CHUNK_SIZE
+    for total in (1, 100, cs - 1, cs, cs + 1, 3 * cs + 7, 256 * cs):
+        b = lib.bra_gpu_pipe_records_bound(total, cs)
+        need, o = 0, 0
+        while o < total:
+            n = min(cs, total - o)
+            need += n + (n + 127) // 128 + 16 + 267
+            o += n
+        assert need <= b <= need + 4096 + 64 * (total // cs + 1)
+    assert lib.bra_gpu_pipe_records_bound(0, cs) == 0

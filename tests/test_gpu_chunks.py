@@ -363,3 +363,63 @@ def test_pipelined_stage_protocol(bra):
         for p in (*h, out):
             lib.bra_gpu_host_free(c.ctx, p)
         c.close()
+
+
+@pytest.mark.gpu
+def test_pipelined_batch_beside_caller_stream_calls(bra, codec):
+    """A call on a caller-supplied stream while a pipelined batch is in flight, and a submit right
+    after such a call, share the context's work buffers: both results must be exact (the call waits
+    on the device for the batch, the submit for the call).  A collect with too small a buffer
+    returns -2 with the size needed and keeps the batch for a retry."""
+    import ctypes as C
+
+    import torch
+
+    lib = bra.lib
+    a = bra.synth_fill(0, 4 * CS + 11, CS)
+    b = bra.synth_fill(2, 3 * CS + 5, CS, first_block=9)
+    want_a = codec.compress_chunks(torch.from_numpy(a).cuda(), CS)[0].cpu().numpy().tobytes()
+    wh, wo, wp = codec.encode(torch.from_numpy(b).cuda(), CS)
+    torch.cuda.synchronize()
+    nb = wh.shape[0]
+    want_b = (wh.cpu(), wo.cpu(), wp[: int(wo[nb].item())].cpu())
+
+    def check_b(H, O, P):
+        assert torch.equal(H.cpu(), want_b[0]) and torch.equal(O.cpu(), want_b[1])
+        assert torch.equal(P[: int(O[nb].item())].cpu(), want_b[2])
+
+    c = bra.BlockCodec(0)
+    n = a.size
+    h = lib.bra_gpu_host_alloc(c.ctx, n)
+    cap = lib.bra_gpu_pipe_records_bound(n, CS)
+    out = lib.bra_gpu_host_alloc(c.ctx, cap)
+    s = torch.cuda.Stream()
+    db = torch.from_numpy(b).cuda()
+    s.wait_stream(torch.cuda.current_stream())
+    try:
+        C.memmove(h, a.ctypes.data, n)
+        size, crc = C.c_uint64(), C.c_uint32()
+        # 1. a caller-stream encode while the batch is in flight
+        assert lib.bra_gpu_compress_chunks_submit(c.ctx, 0, h, n, CS) == 0
+        with torch.cuda.stream(s):
+            H, O, P = c.encode(db, CS, stream=s)
+        s.synchronize()
+        check_b(H, O, P)
+        assert lib.bra_gpu_compress_chunks_collect(c.ctx, 0, out, 16, C.byref(size), C.byref(crc)) == -2
+        assert size.value == len(want_a)
+        assert lib.bra_gpu_compress_chunks_collect(c.ctx, 0, out, cap, C.byref(size), C.byref(crc)) == 1
+        assert C.string_at(out, size.value) == want_a
+        # 2. a submit right after a caller-stream encode that is still queued
+        with torch.cuda.stream(s):
+            H, O, P = c.encode(db, CS, stream=s)
+        assert lib.bra_gpu_compress_chunks_submit(c.ctx, 1, h, n, CS) == 0
+        assert lib.bra_gpu_compress_chunks_collect(c.ctx, 1, out, cap, C.byref(size), C.byref(crc)) == 1
+        assert C.string_at(out, size.value) == want_a
+        s.synchronize()
+        check_b(H, O, P)
+    finally:
+        for q in range(2):
+            lib.bra_gpu_compress_chunks_collect(c.ctx, q, None, 0, None, None)
+        for p in (h, out):
+            lib.bra_gpu_host_free(c.ctx, p)
+        c.close()
