@@ -854,9 +854,8 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
         }
         const uint32_t nd     = B.d + 1;
         const uint32_t obuf   = (B.buf == 2u) ? 0u : (nomove ? B.buf : 1u - B.buf);  // buf 2 = level-0 input
-        if (active && lane == 0)
-            a.nomove[bi] = nomove ? (nm_next ? 2 : 1) : 0;
         bool big[4], med[4], fin[4], nbn[4];
+        bool nm_fin = false;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
@@ -864,7 +863,13 @@ __global__ void __launch_bounds__(64 * SCAN_WAVES) k_scan(ScanArgs a)
             med[r] = tot[r] > JOB_MAX && !big[r];
             fin[r] = big[r] && ((MODE == MODE_STRING) ? nd >= a.dcap : nd >= RANK_KEYBYTES);
             nbn[r] = big[r] && !fin[r];
+            nm_fin |= tot[r] == B.len && fin[r];
         }
+        // STRING: a bucket that stays in place as one fallback group (code 3) has its payloads' low
+        // words copied to p32 by the scatter, where the group flush reads them
+        nm_fin = MODE == MODE_STRING && nomove && __any(nm_fin);
+        if (active && lane == 0)
+            a.nomove[bi] = nomove ? (nm_fin ? 3 : (nm_next ? 2 : 1)) : 0;
         // ---- wave jobs: greedy packing of consecutive sub-buckets of <= JOB_MAX elements ----
         // The non-empty sub-buckets form a list in digit order; a wave-job sub-bucket weighs its
         // size, a larger one JOB_MAX + 1 (it never shares a job).  A job starting at entry i takes
@@ -1306,7 +1311,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                                                     const uint8_t* __restrict__ packed, const BlockDesc* __restrict__ blocks,
                                                     const PackDesc* __restrict__ pkd, const L0Tile* __restrict__ tiles, uint32_t ntiles,
                                                     const uint32_t* __restrict__ tile_off, const uint32_t* __restrict__ l0base,
-                                                    uint64_t* __restrict__ opay, uint8_t* __restrict__ odig)
+                                                    uint64_t* __restrict__ opay, uint8_t* __restrict__ odig, uint32_t* __restrict__ p32)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageL0& S   = *reinterpret_cast<TileStageL0*>(smem);
@@ -1329,7 +1334,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
         const uint32_t  cnt = min((uint32_t) TILE, B.len - T.start);
         load_window(packed + P.poff, T.start, cnt, P.b, win);
         stage_zero(S);
-        S.goff[threadIdx.x] = (tile_off[(size_t) t * 256 + threadIdx.x] + l0base[(size_t) T.block * 256 + threadIdx.x]) & ~NEXT_FLAG;
+        S.goff[threadIdx.x] = tile_off[(size_t) t * 256 + threadIdx.x] + l0base[(size_t) T.block * 256 + threadIdx.x];  // (bit 31: next-level bucket)
         {
             // alphabet rank -> byte value (the packing's map, inverted): thread v = byte value v
             const uint32_t  vv = threadIdx.x;
@@ -1360,7 +1365,8 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
             {
                 const uint32_t vv   = (uint32_t) S.pay[q];
                 const uint32_t dd   = vv >> 24, e = vv & 0xFFFFFFu;
-                const uint32_t slot = S.goff[dd] + (q - S.base[dd]);
+                const uint32_t g    = S.goff[dd];
+                const uint32_t slot = (g & ~NEXT_FLAG) + (q - S.base[dd]);
                 const uint64_t kk   = win_bits64(win, e * P.b);  // virtual bytes 0..7: keep bytes 1..CARRY
                 const uint32_t pos  = T.start + e;
                 // the output byte: the character before the element in the packed window, mapped
@@ -1368,8 +1374,13 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
                 const uint32_t lb = e ? inv_s[(uint32_t) (win_bits64(win, (e - 1) * P.b) >> (64 - P.b))] : prev_s;
                 if (BRA_DCHECK(slot >= B.off && slot < B.off + B.len, "l0 scatter slot %u outside block %u", slot, T.block))
                 {
-                    opay[slot] = ((kk << 8) & 0xFFFFFFFF00000000ull) | ((uint64_t) lb << 24) | pos;
-                    odig[slot] = (uint8_t) (kk >> 48);  // virtual byte 1: the level-1 digit
+                    if (g & NEXT_FLAG)
+                    {
+                        opay[slot] = ((kk << 8) & 0xFFFFFFFF00000000ull) | ((uint64_t) lb << 24) | pos;
+                        odig[slot] = (uint8_t) (kk >> 48);  // virtual byte 1: the level-1 digit
+                    }
+                    else
+                        p32[slot] = (lb << 24) | pos;  // a job's element: the job reads only the low word
                 }
             }
         }
@@ -1385,7 +1396,7 @@ __global__ void __launch_bounds__(TPB) k_l0_scatter(const uint8_t* __restrict__ 
 __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict__ packed, const uint8_t* __restrict__ nomove,
                                                    const uint32_t* __restrict__ tile_off, uint64_t* __restrict__ pay0,
                                                    uint64_t* __restrict__ pay1, const Counters* __restrict__ lv, TileOrder to,
-                                                   uint8_t* __restrict__ dig0, uint8_t* __restrict__ dig1)
+                                                   uint8_t* __restrict__ dig0, uint8_t* __restrict__ dig1, uint32_t* __restrict__ p32)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     TileStageS&    S      = *reinterpret_cast<TileStageS*>(smem);
@@ -1399,6 +1410,14 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
         const uint32_t nm = nomove[D.bi];
         if (nm == 1)
             continue;  // uniform per workgroup: the bucket stays as it is (the next level reads its digits from the payloads)
+        if (nm == 3)
+        {
+            // the bucket stays where it is as one fallback group: its payloads' low words to p32
+            const uint64_t* ip = (D.buf ? pay1 : pay0) + D.s0;
+            for (uint32_t e = threadIdx.x; e < D.cnt; e += TPB)
+                p32[D.s0 + e] = (uint32_t) ip[e];
+            continue;
+        }
         const uint32_t t   = D.t;
         const uint8_t* pk  = packed + D.poff;
         const uint32_t cnt = D.cnt;
@@ -1468,9 +1487,13 @@ __global__ void __launch_bounds__(TPB, 4) k_scatter_p(const uint8_t* __restrict_
                 }
                 if (BRA_DCHECK(slot >= B.start && slot < B.start + B.len, "scatter slot %u outside [%u, +%u)", slot, B.start, B.len))
                 {
-                    op[slot] = nv;
-                    if (g & NEXT_FLAG)  // the next level's digit, for its histogram
-                        od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));
+                    if (g & NEXT_FLAG)
+                    {
+                        op[slot] = nv;
+                        od[slot] = (uint8_t) (rg ? p_digit(nv, 0) : p_digit(vv, j + 1));  // the next level's digit, for its histogram
+                    }
+                    else
+                        p32[slot] = (uint32_t) vv;  // a job's or fallback group's element: only the low word is read again
                 }
             }
         }
@@ -1563,6 +1586,7 @@ struct JobArgs
     uint32_t         jq_chunk; // jobs a wave claims at once
     const uint8_t*   packed;   // STRING: packed key strings (keys are gathered from them)
     const PackDesc*  pk;
+    const uint32_t*  p32;      // STRING: the job elements' payload low words (BWT byte << 24 | rotation), by slot
 };
 
 // Hardware id (0-7) of the XCD the calling wave runs on.  Speed only: the job queues below stay
@@ -2474,7 +2498,7 @@ __device__ __forceinline__ void job_run(const JobArgs& a, const Job& J, const Bl
         for (int r = 0; r < 4; ++r)
         {
             const uint32_t c = wj * 256 + lane * 4 + r;
-            pay[r]           = c < T ? (uint32_t) K[J.start + c] : 0u;
+            pay[r]           = c < T ? a.p32[J.start + c] : 0u;
         }
         job_gather1<W>(a, J, BD, PK, pay, wj, gl);
     }
@@ -2861,9 +2885,8 @@ __global__ void k_audit_cover(const Job* __restrict__ jobs, const uint32_t* __re
             atomicAdd(&cnt[J.start + c], 1u);
     }
 }
-__global__ void k_audit_check(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t kind, const uint64_t* __restrict__ key0,
-                              const uint64_t* __restrict__ key1, const uint32_t* __restrict__ fsa, const uint32_t* __restrict__ cnt,
-                              const BlockDesc* __restrict__ blocks)
+__global__ void k_audit_check(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t kind, const uint32_t* __restrict__ p32,
+                              const uint32_t* __restrict__ fsa, const uint32_t* __restrict__ cnt, const BlockDesc* __restrict__ blocks)
 {
     __shared__ uint32_t s_in, s_out, x_in, x_out, over;
     const uint32_t n = dev_count(pn);
@@ -2872,11 +2895,10 @@ __global__ void k_audit_check(const Job* __restrict__ jobs, const uint32_t* __re
         if (threadIdx.x == 0)
             s_in = s_out = x_in = x_out = over = 0;
         __syncthreads();
-        const Job       J = jobs[j];
-        const uint64_t* K = J.buf ? key1 : key0;
+        const Job J = jobs[j];
         for (uint32_t c = threadIdx.x; c < J.len; c += blockDim.x)
         {
-            const uint32_t a = (uint32_t) K[J.start + c] & 0xFFFFFFu, b = fsa[J.start + c];
+            const uint32_t a = p32[J.start + c] & 0xFFFFFFu, b = fsa[J.start + c];
             atomicAdd(&s_in, a);
             atomicAdd(&s_out, b);
             atomicXor(&x_in, a);
@@ -2910,16 +2932,16 @@ __device__ __forceinline__ uint32_t au_hash(uint32_t x)
     x ^= x >> 16;
     return x;
 }
-__global__ void __launch_bounds__(1024) k_audit_shuffle(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint64_t* __restrict__ key0,
-                                                        uint64_t* __restrict__ key1, uint32_t seed)
+__global__ void __launch_bounds__(1024) k_audit_shuffle(const Job* __restrict__ jobs, const uint32_t* __restrict__ pn, uint32_t* __restrict__ p32,
+                                                        uint32_t seed)
 {
-    __shared__ uint64_t pl[1024];
+    __shared__ uint32_t pl[1024];
     __shared__ uint32_t hk[1024];
     const uint32_t n = dev_count(pn);
     for (uint32_t j = blockIdx.x; j < n; j += gridDim.x)
     {
         const Job J   = jobs[j];
-        uint64_t* K   = J.buf ? key1 : key0;
+        uint32_t* K   = p32;
         const uint32_t len = min(J.len, 1024u), t = threadIdx.x;
         if (t < len)
         {
@@ -2939,7 +2961,7 @@ __global__ void __launch_bounds__(1024) k_audit_shuffle(const Job* __restrict__ 
             for (uint32_t i = 0; i < len; ++i)
                 dst += hk[i] < hc || (hk[i] == hc && i < cr);
         }
-        const uint64_t mine = t < len ? pl[t] : 0;
+        const uint32_t mine = t < len ? pl[t] : 0;
         __syncthreads();
         if (t < len)
             K[J.start + dst] = mine;
@@ -3185,17 +3207,16 @@ __global__ void __launch_bounds__(256) k_tile_scatter(const Bucket* __restrict__
 // fallback (prefix doubling on ranks) helpers
 // -------------------------------------------------------------------------------------------------
 // Copy the members of fallback groups that still live in a KV buffer into fsa.
-__global__ void k_group_flush(const Group* __restrict__ groups, uint32_t ng, const uint64_t* __restrict__ pay0,
-                              const uint64_t* __restrict__ pay1, uint32_t* __restrict__ fsa)
+__global__ void k_group_flush(const Group* __restrict__ groups, uint32_t ng, const uint32_t* __restrict__ p32, uint32_t* __restrict__ fsa)
 {
+    // (the MSD scatters leave a fallback group's payload low words in p32, by slot)
     for (uint32_t gi = blockIdx.x; gi < ng; gi += gridDim.x)
     {
         const Group G = groups[gi];
         if (G.block & (1u << 30))
             continue;
-        const uint64_t* p = (G.block >> 31) ? pay1 : pay0;
         for (uint32_t i = threadIdx.x; i < G.len; i += blockDim.x)
-            fsa[G.start + i] = (uint32_t) p[G.start + i] & 0xFFFFFFu;
+            fsa[G.start + i] = p32[G.start + i] & 0xFFFFFFu;
     }
 }
 
@@ -3371,6 +3392,7 @@ struct BwtWorkspace
     uint64_t  cap_n          = 0;
     uint32_t  cap_blocks     = 0;
     uint64_t* key[2]         = {nullptr, nullptr};
+    uint32_t* p32            = nullptr;  // STRING: payload low words of the elements that leave the levels for jobs / fallback groups
     uint32_t* pay[2]         = {nullptr, nullptr};
     uint32_t* fsa            = nullptr;
     uint32_t* isa            = nullptr;
@@ -3557,7 +3579,7 @@ static void ws_free(BwtWorkspace& w)
         (void) hipFree(w.tdesc[i]);
         (void) hipFree(w.dig[i]);
     }
-    void* dev[] = {w.fsa,      w.isa,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
+    void* dev[] = {w.fsa,      w.isa,   w.p32,   w.tile_hist, w.tile_off, w.nomove, w.flag, w.jobs, w.mjobs, w.jobs_sorted, w.mjobs_sorted,
                    w.job_cnt,  w.jseg,  w.tile_cnt,  w.tile_order, w.ctr,  w.jobq,  w.l0tiles, w.l0b, w.packed, w.pkd, w.amask, w.tmask, w.l0tot, w.l0base,
                    w.audit_cnt};
     for (void* p : dev)
@@ -3617,7 +3639,7 @@ static bool ws_reserve(BwtWorkspace& w, uint64_t n, uint32_t nblocks)
              dev_alloc(w.tile_bucket[i], w.cap_tiles) && dev_alloc(w.tdesc[i], w.cap_tiles) && dev_alloc(w.dig[i], N + 16);
     const uint32_t tmax  = std::max(w.cap_tiles, w.cap_l0);
     const size_t   nkeys = 8 * (size_t) div_up(B, 8);
-    ok = ok && dev_alloc(w.fsa, N) && dev_alloc(w.isa, N) && dev_alloc(w.tile_hist, (uint64_t) tmax * 256) &&
+    ok = ok && dev_alloc(w.fsa, N) && dev_alloc(w.isa, N) && dev_alloc(w.p32, N) && dev_alloc(w.tile_hist, (uint64_t) tmax * 256) &&
          dev_alloc(w.tile_off, (uint64_t) tmax * 256) && dev_alloc(w.nomove, std::max<uint32_t>(w.cap_big, B)) && dev_alloc(w.flag, B) &&
          dev_alloc(w.jobs, w.cap_jobs) && dev_alloc(w.mjobs, w.cap_mjobs) && dev_alloc(w.jobs_sorted, cap_sorted) &&
          dev_alloc(w.mjobs_sorted, w.cap_mjobs) && dev_alloc(w.job_cnt, 4 * MJ_CLASSES * nkeys) && dev_alloc(w.jseg, (1 + MJ_CLASSES) * 16) &&
@@ -3766,7 +3788,7 @@ static bool run_levels(BwtWorkspace& w, const uint8_t* d_in, const BlockDesc* d_
                 BRA_PROF(P_BWT_SCATTER, s);
                 if (MODE == MODE_STRING)
                     hipLaunchKernelGGL(k_scatter_p, dim3(grid), dim3(TPB), sizeof(TileStageS), s, w.packed, w.nomove, w.tile_off, w.key[0],
-                                       w.key[1], lin, to, w.dig[0], w.dig[1]);
+                                       w.key[1], lin, to, w.dig[0], w.dig[1], w.p32);
                 else
                     hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(TPB), lds, s, w.big[cur], w.nomove, w.tile_bucket[cur], lin, w.tile_off,
                                        w.key[0], w.key[1], w.pay[0], w.pay[1], MODE);
@@ -3801,7 +3823,8 @@ static bool account_levels(BwtWorkspace& w, hipStream_t s)
     const uint32_t ns = std::min<uint32_t>(w.levels + 2, MAX_LEVELS);
     BRA_HIP_CHECK(hipMemcpyAsync(w.h_ctr, w.ctr, ns * sizeof(Counters), hipMemcpyDeviceToHost, s));
     BRA_HIP_CHECK(hipStreamSynchronize(s));
-    // STRING: 8-byte payloads moved (+ the next digit gathered for elements that stay in big buckets)
+    // STRING: 8-byte payloads moved (+ the next digit gathered for elements that stay in big buckets);
+    // elements leaving for a job write a 4-byte word instead, so this is an upper estimate
     const double eb = 8.0, mb = (MODE == MODE_STRING) ? 16.0 + 8.0 / CARRY : 24.0;
     for (uint32_t k = 1; k + 1 < ns; ++k)
     {
@@ -3838,8 +3861,8 @@ static int audit_jobs(BwtWorkspace& w, uint64_t N, const BlockDesc* d_blocks, hi
         return -1;
     hipLaunchKernelGGL(k_audit_cover, dim3(4096), dim3(256), 0, s, w.jobs, &w.ctr[0].n_jobs, cnt);
     hipLaunchKernelGGL(k_audit_cover, dim3(4096), dim3(256), 0, s, w.mjobs, &w.ctr[0].n_mjobs, cnt);
-    hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.jobs, &w.ctr[0].n_jobs, 0u, w.key[0], w.key[1], w.fsa, cnt, d_blocks);
-    hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.mjobs, &w.ctr[0].n_mjobs, 1u, w.key[0], w.key[1], w.fsa, cnt, d_blocks);
+    hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.jobs, &w.ctr[0].n_jobs, 0u, w.p32, w.fsa, cnt, d_blocks);
+    hipLaunchKernelGGL(k_audit_check, dim3(4096), dim3(256), 0, s, w.mjobs, &w.ctr[0].n_mjobs, 1u, w.p32, w.fsa, cnt, d_blocks);
     if (hipStreamSynchronize(s) != hipSuccess || hipMemcpyFromSymbol(&fails, HIP_SYMBOL(g_audit_fail), 4) != hipSuccess)
         return -1;
 #ifdef BRA_JOB_AUDIT
@@ -3895,8 +3918,8 @@ int bwt_debug_rerun_jobs(BwtWorkspace* wp, int reps, hipStream_t s, uint32_t see
     {
         if (seed)
         {
-            hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->jobs, &wp->ctr[0].n_jobs, wp->key[0], wp->key[1], seed + (uint32_t) r);
-            hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->mjobs, &wp->ctr[0].n_mjobs, wp->key[0], wp->key[1], seed + (uint32_t) r);
+            hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->jobs, &wp->ctr[0].n_jobs, wp->p32, seed + (uint32_t) r);
+            hipLaunchKernelGGL(k_audit_shuffle, dim3(4096), dim3(1024), 0, s, wp->mjobs, &wp->ctr[0].n_mjobs, wp->p32, seed + (uint32_t) r);
         }
         if (!run_jobs(*wp, wp->last_ph, s))
             return -1;
@@ -4021,7 +4044,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     {
         BRA_PROF(P_BWT_L0SCATTER, s);
         hipLaunchKernelGGL(k_l0_scatter, dim3(nt0 >= 8 ? std::min<uint32_t>(nt0, grid) & ~7u : nt0), dim3(TPB), sizeof(TileStageL0) + TILE + 64, s, d_in, w.amask, w.packed, d_blocks,
-                           w.pkd, w.l0tiles, nt0, w.tile_off, w.l0base, w.key[0], w.dig[0]); BRA_DSYNC(s);
+                           w.pkd, w.l0tiles, nt0, w.tile_off, w.l0base, w.key[0], w.dig[0], w.p32); BRA_DSYNC(s);
     }
     BRA_HIP_CHECK(hipGetLastError());
     prof_bytes(P_BWT_PACK, 3.0 * (double) N);  // input read twice, packed string written (<= N)
@@ -4033,6 +4056,7 @@ bool bwt_encode_enqueue(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* 
     JobPhase ph;
     ph.ja = JobArgs{w.jobs,  0,     d_in,        d_blocks, w.key[0], w.key[1], w.pay[0], w.pay[1], w.fsa, d_L, d_pi,
                     w.isa,   w.groups[0], w.cap_groups, w.ctr,  DCAP_JOB, 0, 0, {}, nullptr, nullptr, 0, w.packed, w.pkd};
+    ph.ja.p32  = w.p32;
     ph.jm      = ph.ja;
     ph.jm.jobs = w.mjobs;
     ph.nblocks = nblocks;
@@ -4118,7 +4142,7 @@ bool bwt_encode_finish(BwtWorkspace* wp, const uint8_t* d_in, const BlockDesc* d
     int gcur = 0;
     hipLaunchKernelGGL(k_group_depth_chars, dim3(std::min<uint32_t>(div_up(ng, 256), 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.pkd);
     BRA_DSYNC(s);
-    hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.key[0], w.key[1], w.fsa); BRA_DSYNC(s);
+    hipLaunchKernelGGL(k_group_flush, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, w.p32, w.fsa); BRA_DSYNC(s);
     // mark blocks, build ranks: singletons rank = own slot, group members = group start
     hipLaunchKernelGGL(k_group_mark, dim3(std::min<uint32_t>(ng, 4096u)), dim3(256), 0, s, w.groups[gcur], ng, d_blocks, w.fsa, w.isa,
                        w.flag); BRA_DSYNC(s);  // sets the flags (its rank writes are redone below)
