@@ -1034,11 +1034,17 @@ __global__ void k_hd_tail(const HuffMetaRec* __restrict__ meta, uint32_t nblocks
 // k_hd_trans walks the entries > 0 two at a time (one at a time, or 3 or 4 in lockstep, measured slower)
 constexpr uint32_t HD2_SEG   = 2048;  // bits per segment
 constexpr uint32_t HD2_LMAX  = 30;
-constexpr uint32_t HD2_TPB   = 256;
+constexpr uint32_t HD2_TPB   = 256;   // k_hd_trans: a lane per segment, HD2_TPB segments per task
+constexpr uint32_t HD2_WTPB  = 4 * HD2_TPB;  // k_hd_write2: four lanes per segment
 constexpr uint32_t HD2_REFB  = 512;   // boundary bitmap of the reference path (bits from the segment start;
                                       // 64 / 128 / 256 / 512 / 1024: text decode 14.9 / 16.3 / 17.9 / 19.5 / 18.5 GB/s)
 constexpr uint32_t HD2_STRD  = 32;    // transfer words per segment
 constexpr uint32_t HD2_TAB   = 2304;  // u32 words per block table
+constexpr uint32_t HD2_SUB   = HD2_SEG / 4;  // k_hd_write2: four lanes per segment, from sub records
+                                             // every HD2_SUB bits of the entry-0 path
+static_assert(HD2_REFB <= HD2_SUB, "a path joins the entry-0 path before the first sub record");
+static_assert(HD2_LMAX + 2 <= HD2_STRD, "the sub records follow the entries' transfer words");
+static_assert(HD2_SEG <= 2048 && HD2_LMAX < 32, "ranks and offsets of the sub records fit 11 + 5 bits");
 
 // table layout (u32 words)
 constexpr uint32_t T_LUT = 0, T_LIM = 2048, T_FIRST = 2112, T_IDX = 2144, T_PERM = 2176, T_INFO = 2240;  // info: lmax, clean
@@ -1284,6 +1290,10 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
             bm[i] = 0;
         W.init(s);
         uint32_t p = s, c = 0, bad = 0, len, sym;
+        // the path's first codeword at or after bits HD2_SUB, 2 HD2_SUB, 3 HD2_SUB: (offset past the
+        // mark << 11) | rank, 0xFFFF when the path ends before (k_hd_write2 starts its sub-segment
+        // lanes there)
+        uint32_t mark = HD2_SUB, sub1 = 0xFFFFu, sub2 = 0xFFFFu, sub3 = 0xFFFFu;
         while (p < stop)
         {
             const uint32_t d = p - s;
@@ -1294,6 +1304,14 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
                     if ((d >> 5) == (uint32_t) i)
                         bm[i] |= 1u << (d & 31);
             }
+            if (d >= mark)
+            {
+                const uint32_t rec = ((d - mark) << 11) | c;
+                sub1 = mark == HD2_SUB ? rec : sub1;
+                sub2 = mark == 2 * HD2_SUB ? rec : sub2;
+                sub3 = mark == 3 * HD2_SUB ? rec : sub3;
+                mark += HD2_SUB;
+            }
             if (!hd2_dec(L, W.peek(p), len, sym) || len > nbits - p)
             {
                 bad = 1;
@@ -1302,8 +1320,11 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
             p += len;
             ++c;
         }
-        const uint32_t c0 = c, r0 = (bad << 31) | (((p - stop) & 31u) << 16);
+        // bit 30: the path joins the entry-0 path (so k_hd_write2 may split it at the sub records)
+        const uint32_t c0 = c, r0 = (bad << 31) | (1u << 30) | (((p - stop) & 31u) << 16);
         out[0]               = r0 | c0;
+        out[HD2_STRD - 2]    = sub1 | sub2 << 16;
+        out[HD2_STRD - 1]    = sub3;
         // the other entries two at a time in lockstep: both paths' window loads and LUT reads are
         // issued before either result is used (one path's step is a dependent load chain)
         for (uint32_t e = 1; e < nent; e += 2)
@@ -1374,27 +1395,103 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
     }
 }
 
-// Per block: the true path from segment to segment.
-__global__ void __launch_bounds__(64) k_hd_chain(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint32_t* __restrict__ seg_base,
-                                                 const uint32_t* __restrict__ trans, uint32_t* __restrict__ seg_info, uint32_t* __restrict__ status)
+// Per block: the true path from segment to segment, 256 segments at a time.  Guess: segment k is
+// entered where the entry-0 path of segment k - 1 leaves it.  That holds whenever the true path of
+// k - 1 joined its entry-0 path (bit 30), so if every guessed word of the chunk has bit 30 (the
+// chunk's first segment is entered where the chunk before left), the guesses are the true path by
+// induction and the chunk's offsets are one prefix sum -- Huffman codes of unequal lengths
+// resynchronise within a few codewords, so text and skewed data take this path.  Otherwise (codes
+// of near-equal lengths keep separate phases) one lane walks the chunk serially.  Either way the
+// result is the reference's sequential walk: offsets up to orig_size, nothing after the first
+// death, fail when the path dies before symbol orig_size.
+constexpr uint32_t HD2_CTPB = 256;
+__global__ void __launch_bounds__(HD2_CTPB) k_hd_chain(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint32_t* __restrict__ seg_base,
+                                                       const uint32_t* __restrict__ trans, uint32_t* __restrict__ seg_info, uint32_t* __restrict__ status)
 {
-    __shared__ uint32_t rows[64 * HD2_STRD];
-    const int           lane = lane_id();
+    __shared__ uint32_t rows[HD2_CTPB * HD2_STRD];
+    __shared__ uint32_t wsum[HD2_CTPB / 64], wdead[HD2_CTPB / 64], sh_e, sh_acc, sh_done, sh_fail, sh_all;
+    const uint32_t      t = threadIdx.x, lane = t & 63u, wv = wave_id();
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
         const uint32_t g0 = seg_base[b], ns = seg_base[b + 1] - g0, osz = meta[b].orig_size;
-        uint32_t       e = 0, acc = 0, fail = 0, done = 0;
-        for (uint32_t c0 = 0; c0 < ns; c0 += 64)
+        __syncthreads();
+        if (t == 0)
         {
-            const uint32_t nr = min(64u, ns - c0);
+            sh_e = 0, sh_acc = 0, sh_done = 0, sh_fail = 0;
+        }
+        for (uint32_t c0 = 0; c0 < ns; c0 += HD2_CTPB)
+        {
+            const uint32_t nr = min(HD2_CTPB, ns - c0);
             __syncthreads();
-            for (uint32_t i = lane; i < nr * HD2_STRD; i += 64)
+            for (uint32_t i = t; i < nr * HD2_STRD; i += HD2_CTPB)
                 rows[i] = trans[(size_t) (g0 + c0) * HD2_STRD + i];
+            if (t == 0)
+                sh_all = 1;
             __syncthreads();
-            if (lane == 0)
+            const uint32_t e0 = sh_e, acc0 = sh_acc, done0 = sh_done;
+            // the guessed entry and word of segment c0 + t
+            uint32_t g = 0, word = 0, cnt = 0;
+            if (t < nr)
+            {
+                g    = t == 0 ? e0 : (rows[(t - 1) * HD2_STRD] >> 16) & 31u;
+                word = rows[t * HD2_STRD + g];
+                cnt  = word & 0xFFFFu;
+                if (!((word >> 30) & 1u))
+                    sh_all = 0;  // benign race: every writer stores 0
+            }
+            // inclusive prefix of the counts and of the death flags over the chunk
+            uint32_t inc = cnt, dead = (t < nr) ? (word >> 31) : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1)
+            {
+                const uint32_t o = (uint32_t) __shfl_up((int) inc, d, 64), od = (uint32_t) __shfl_up((int) dead, d, 64);
+                if ((int) lane >= d)
+                    inc += o, dead += od;
+            }
+            if (lane == 63)
+                wsum[wv] = inc, wdead[wv] = dead;
+            __syncthreads();
+            if (done0)
+            {
+                if (t < nr)
+                    seg_info[g0 + c0 + t] = 0xFFFFFFFFu;  // the path died in an earlier chunk
+                continue;
+            }
+            if (sh_all)
+            {
+                uint32_t wb = 0, db = 0;
+                for (uint32_t i = 0; i < wv; ++i)
+                    wb += wsum[i], db += wdead[i];
+                inc += wb, dead += db;
+                // segment t is walked iff no death strictly before it: deaths up to t minus its own
+                const uint32_t before = dead - ((t < nr) ? (word >> 31) : 0u), acc = acc0 + inc - cnt;
+                if (t < nr)
+                {
+                    uint32_t info = 0xFFFFFFFFu;
+                    if (before == 0 && acc < osz)
+                    {
+                        info = (g << 27) | acc;
+                        if (word >> 31)
+                        {
+                            sh_done = 1;  // the one segment with the first death
+                            if (acc + cnt < osz)
+                                sh_fail = 1;
+                        }
+                    }
+                    seg_info[g0 + c0 + t] = info;
+                }
+                if (t == nr - 1)
+                {
+                    sh_acc = acc0 + inc;  // past orig_size or past a death, the sum no longer matters
+                    sh_e   = (word >> 16) & 31u;
+                }
+            }
+            else if (t == 0)
+            {
+                uint32_t e = e0, acc = acc0, done = 0, fail = 0;
                 for (uint32_t k = 0; k < nr; ++k)
                 {
-                    uint32_t info = 0xFFFFFFFFu;  // (entry << 27) | output offset; all ones: nothing to write
+                    uint32_t info = 0xFFFFFFFFu;
                     if (!done && acc < osz)
                     {
                         const uint32_t r = rows[k * HD2_STRD + e], cnt = r & 0xFFFFu;
@@ -1410,28 +1507,72 @@ __global__ void __launch_bounds__(64) k_hd_chain(const HuffMetaRec* __restrict__
                     }
                     seg_info[g0 + c0 + k] = info;
                 }
+                sh_e = e, sh_acc = acc, sh_done = done;
+                if (fail)
+                    sh_fail = 1;
+            }
         }
-        if (lane == 0)
-            status[b] = (fail || acc < osz) ? 1u : 0u;
+        __syncthreads();
+        if (t == 0)
+            status[b] = (sh_fail || sh_acc < osz) ? 1u : 0u;
     }
 }
 
-// Per segment: decode the true path into out[off, off + n).
-__global__ void __launch_bounds__(HD2_TPB) k_hd_write2(const HuffMetaRec* __restrict__ meta, const uint8_t* __restrict__ payload,
-                                                       const uint64_t* __restrict__ payload_off, const uint32_t* __restrict__ tab,
-                                                       const Hd2Task* __restrict__ tasks, uint32_t ntasks, const uint32_t* __restrict__ seg_base,
-                                                       const uint32_t* __restrict__ trans, const uint32_t* __restrict__ seg_info,
-                                                       const uint32_t* __restrict__ status, uint8_t* __restrict__ out,
-                                                       const uint64_t* __restrict__ out_base, uint64_t* __restrict__ end_pos)
+// Symbols [0, n) of the path from bit p into dst (a lane writes its own range: 16 bytes per store
+// once dst is aligned, dword stores would cost a request per 4 bytes); returns the bit after them.
+__device__ __forceinline__ uint32_t hd2_write_run(const Hd2Lds& L, BitWin& W, uint32_t p, uint8_t* dst, uint32_t n)
+{
+    uint32_t len = 0, sym = 0, i = 0;
+    for (; i < n && (((uintptr_t) (dst + i)) & 15); ++i)
+    {
+        (void) hd2_dec(L, W.peek(p), len, sym);
+        p += len;
+        dst[i] = (uint8_t) sym;
+    }
+    for (; i + 16 <= n; i += 16)
+    {
+        uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+        {
+            (void) hd2_dec(L, W.peek(p), len, sym);
+            p += len;
+            wv[k >> 2] |= sym << (8 * (k & 3));
+        }
+        *reinterpret_cast<uint4*>(dst + i) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    }
+    for (; i < n; ++i)
+    {
+        (void) hd2_dec(L, W.peek(p), len, sym);
+        p += len;
+        dst[i] = (uint8_t) sym;
+    }
+    return p;
+}
+
+// Per segment: decode the true path into out[off, off + n), four lanes per segment.  A true path
+// that joined the entry-0 path (bit 30 of its transfer word; it joins within the first HD2_REFB
+// bits) passes through the entry-0 path's codeword starts recorded after every HD2_SUB bits, so
+// lane k > 0 decodes from the k-th record to the next and lane 0 from the entry to the first; a
+// path that did not join (codes of near-equal lengths) is decoded by lane 0 alone.  The decode is
+// a dependent chain per lane (window bits -> LUT read -> length), so four lanes on a quarter each
+// hide its latency four times better.
+__global__ void __launch_bounds__(HD2_WTPB) k_hd_write2(const HuffMetaRec* __restrict__ meta, const uint8_t* __restrict__ payload,
+                                                        const uint64_t* __restrict__ payload_off, const uint32_t* __restrict__ tab,
+                                                        const Hd2Task* __restrict__ tasks, uint32_t ntasks, const uint32_t* __restrict__ seg_base,
+                                                        const uint32_t* __restrict__ trans, const uint32_t* __restrict__ seg_info,
+                                                        const uint32_t* __restrict__ status, uint8_t* __restrict__ out,
+                                                        const uint64_t* __restrict__ out_base, uint64_t* __restrict__ end_pos)
 {
     __shared__ Hd2Lds L;
+    const uint32_t    k = threadIdx.x & 3u;
     for (uint32_t tk = blockIdx.x; tk < ntasks; tk += gridDim.x)
     {
         const Hd2Task  K = tasks[tk];
         const uint32_t b = K.block;
         __syncthreads();
         hd2_load_tables(tab + (size_t) b * HD2_TAB, L);
-        const uint32_t j = K.seg0 + threadIdx.x, g0 = seg_base[b], ns = seg_base[b + 1] - g0;
+        const uint32_t j = K.seg0 + (threadIdx.x >> 2), g0 = seg_base[b], ns = seg_base[b + 1] - g0;
         if (j >= ns || status[b])
             continue;
         const uint32_t info = seg_info[g0 + j];
@@ -1441,41 +1582,38 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_write2(const HuffMetaRec* __rest
         const uint32_t e = info >> 27, off = info & 0x7FFFFFFu;
         if (off >= osz)
             continue;
-        const uint32_t cnt = trans[(size_t) (g0 + j) * HD2_STRD + e] & 0xFFFFu;
-        const uint32_t n   = min(cnt, osz - off);
-        const uint32_t nbytes = meta[b].encoded_size;
-        BitWin         W      = hd2_win(payload, payload_off[b], nbytes);
-        uint32_t       p      = j * HD2_SEG + e, len = 0, sym = 0;
-        W.init(p);
-        uint8_t* dst = out + out_base[b] + off;
-        // bytes until dst is 16-byte aligned, then 16 bytes per store (a lane writes its own
-        // range: dword stores cost a request per 4 bytes), then the rest
-        uint32_t i = 0;
-        for (; i < n && (((uintptr_t) (dst + i)) & 15); ++i)
+        const uint32_t* tr  = trans + (size_t) (g0 + j) * HD2_STRD;
+        const uint32_t  r   = tr[e], cnt = r & 0xFFFFu;
+        const uint32_t  n   = min(cnt, osz - off);
+        // this lane's symbols [i0, i1) of the segment's cnt, from bit p
+        uint32_t i0 = 0, i1 = cnt, p = j * HD2_SEG + e;
+        if ((r >> 30) & 1u)
         {
-            (void) hd2_dec(L, W.peek(p), len, sym);
-            p += len;
-            dst[i] = (uint8_t) sym;
-        }
-        for (; i + 16 <= n; i += 16)
-        {
-            uint32_t wv[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
+            const uint32_t c0 = tr[0] & 0xFFFFu, s12 = tr[HD2_STRD - 2], s3 = tr[HD2_STRD - 1];
+            // records: rank in bits 0-10, offset past the mark above; once one is missing (the
+            // path ended before its mark) so are the later ones.  The entry-0 path's codeword of
+            // rank x is symbol cnt - c0 + x of the true path.
+            const uint32_t mine = k == 1 ? (s12 & 0xFFFFu) : k == 2 ? (s12 >> 16) : s3;
+            const uint32_t next = k == 0 ? (s12 & 0xFFFFu) : k == 1 ? (s12 >> 16) : k == 2 ? s3 : 0xFFFFu;
+            if (k > 0)
             {
-                (void) hd2_dec(L, W.peek(p), len, sym);
-                p += len;
-                wv[k >> 2] |= sym << (8 * (k & 3));
+                if (mine == 0xFFFFu)
+                    continue;  // the lane before runs to the end
+                i0 = cnt - c0 + (mine & 0x7FFu);
+                p  = j * HD2_SEG + k * HD2_SUB + (mine >> 11);
             }
-            *reinterpret_cast<uint4*>(dst + i) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+            if (next != 0xFFFFu)
+                i1 = cnt - c0 + (next & 0x7FFu);
         }
-        for (; i < n; ++i)
-        {
-            (void) hd2_dec(L, W.peek(p), len, sym);
-            p += len;
-            dst[i] = (uint8_t) sym;
-        }
-        if (off + n == osz)
+        else if (k > 0)
+            continue;
+        const uint32_t z = min(i1, n);
+        if (i0 >= z)
+            continue;
+        BitWin W = hd2_win(payload, payload_off[b], meta[b].encoded_size);
+        W.init(p);
+        p = hd2_write_run(L, W, p, out + out_base[b] + off + i0, z - i0);
+        if (off + n == osz && z == n)
             end_pos[b] = p;
     }
 }
@@ -1783,10 +1921,10 @@ bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint3
         hipLaunchKernelGGL(k_hd_trans, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
                            w.seg_base, w.trans);
     }
-    hipLaunchKernelGGL(k_hd_chain, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(64), 0, s, d_meta, nblocks, w.seg_base, w.trans, w.seg_info,
+    hipLaunchKernelGGL(k_hd_chain, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(HD2_CTPB), 0, s, d_meta, nblocks, w.seg_base, w.trans, w.seg_info,
                        d_status);
     if (nt)
-        hipLaunchKernelGGL(k_hd_write2, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
+        hipLaunchKernelGGL(k_hd_write2, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_WTPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
                            w.seg_base, w.trans, w.seg_info, d_status, d_out, d_out_base, w.end_pos);
     hipLaunchKernelGGL(k_hd_tail2, dim3(div_up(nblocks, 64)), dim3(64), 0, s, d_meta, nblocks, d_payload, d_payload_off, w.tab, w.end_pos,
                        d_status);

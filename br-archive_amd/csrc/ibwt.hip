@@ -905,6 +905,38 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
 // text).  The hop's last partial dword goes byte by byte (the next hop owns the bytes after it).
 typedef uint32_t __attribute__((aligned(1))) u32_u;
 typedef uint4 __attribute__((aligned(1))) u128_u;
+typedef uint64_t __attribute__((aligned(1))) u64_u;
+typedef uint16_t __attribute__((aligned(1))) u16_u;
+constexpr uint32_t CP_BATCH = 8;
+
+// the first k (1..16) bytes of v to dst (unaligned): one 16-byte store, or at most four narrower
+// ones for the partial tail of a hop (the bytes after it belong to the next hop)
+__device__ __forceinline__ void store_head(uint8_t* dst, uint4 v, uint32_t k)
+{
+    if (k == 16)
+    {
+        *reinterpret_cast<u128_u*>(dst) = v;
+        return;
+    }
+    uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
+    if (k & 8)
+    {
+        *reinterpret_cast<u64_u*>(dst) = (uint64_t) w0 | (uint64_t) w1 << 32;
+        dst += 8, w0 = w2, w1 = v.w;
+    }
+    if (k & 4)
+    {
+        *reinterpret_cast<u32_u*>(dst) = w0;
+        dst += 4, w0 = w1;
+    }
+    if (k & 2)
+    {
+        *reinterpret_cast<u16_u*>(dst) = (uint16_t) w0;
+        dst += 2, w0 >>= 16;
+    }
+    if (k & 1)
+        *dst = (uint8_t) w0;
+}
 
 __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk, const uint32_t* __restrict__ cum, const uint32_t* __restrict__ cnt,
                                                    const uint32_t* __restrict__ order, uint32_t nblocks,
@@ -934,6 +966,7 @@ __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk
                 if (st < B.len)
                     len = min(hop_len[base + q], B.len - st);
             }
+#ifdef BRA_EXP_OLDCOPY
             for (uint32_t h = 0; h < 16; ++h)
             {
                 const uint32_t hq = (uint32_t) __shfl((int) q, (int) (g0 + h), 64);
@@ -953,6 +986,45 @@ __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk
                         for (uint32_t t = 0; o + t < m; ++t)
                             dst[o + t] = (uint8_t) (v >> (8 * t));
                 }
+#else
+            for (uint32_t h0 = 0; h0 < 16; h0 += CP_BATCH)
+            {
+                // the first 256 bytes of CP_BATCH hops (a whole slot when S = 64): all loads in
+                // flight before the first store
+                uint4 v[CP_BATCH];
+#pragma unroll
+                for (uint32_t i = 0; i < CP_BATCH; ++i)
+                {
+                    const uint32_t hq = (uint32_t) __shfl((int) q, (int) (g0 + h0 + i), 64);
+                    const uint32_t hl = (uint32_t) __shfl((int) len, (int) (g0 + h0 + i), 64);
+                    v[i]              = make_uint4(0, 0, 0, 0);
+                    if (16 * l < min(hl, cap))
+                        v[i] = reinterpret_cast<const uint4*>(slots + B.tslot + (size_t) hq * cap)[l];
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < CP_BATCH; ++i)
+                {
+                    const uint32_t hs = (uint32_t) __shfl((int) st, (int) (g0 + h0 + i), 64);
+                    const uint32_t hl = (uint32_t) __shfl((int) len, (int) (g0 + h0 + i), 64);
+                    const uint32_t m  = min(hl, cap), o = 16 * l;
+                    if (hs < B.len && o < m)
+                        store_head(ob + hs + o, v[i], min(m - o, 16u));
+                }
+            }
+            for (uint32_t h = 0; h < 16; ++h)
+            {
+                const uint32_t hq = (uint32_t) __shfl((int) q, (int) (g0 + h), 64);
+                const uint32_t hs = (uint32_t) __shfl((int) st, (int) (g0 + h), 64);
+                const uint32_t hl = (uint32_t) __shfl((int) len, (int) (g0 + h), 64);
+                if (hs >= B.len || hl <= 256)
+                    continue;
+                // the rest of a slot of more than 256 bytes (S > 64), then the overflow chunks
+                const uint8_t* src = slots + B.tslot + (size_t) hq * cap;
+                const uint32_t m   = min(hl, cap);
+                uint8_t*       dst = ob + hs;
+                for (uint32_t o = 256 + 16 * l; o < m; o += 256)
+                    store_head(dst + o, *reinterpret_cast<const uint4*>(src + o), min(m - o, 16u));
+#endif
                 uint32_t c = hl > cap ? hop_ovf[base + hq] : 0xFFFFFFFFu;
                 for (uint32_t o0 = cap; o0 < hl && c < pool_cap; o0 += IB_CHUNK)
                 {
@@ -960,15 +1032,7 @@ __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk
                     const uint32_t mm = min(IB_CHUNK, hl - o0);
                     for (uint32_t o = 16 * l; o < mm; o += 256)
                     {
-                        const uint4 v = *reinterpret_cast<const uint4*>(cs + o);
-                        if (o + 16 <= mm)
-                            *reinterpret_cast<u128_u*>(dst + o0 + o) = v;
-                        else
-                        {
-                            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-                            for (uint32_t t = 0; o + t < mm; ++t)
-                                dst[o0 + o + t] = (uint8_t) (w[t >> 2] >> (8 * (t & 3)));
-                        }
+                        store_head(dst + o0 + o, *reinterpret_cast<const uint4*>(cs + o), min(mm - o, 16u));
                     }
                     c = ovl_next[c];
                 }

@@ -377,6 +377,39 @@ def test_huffman_decode_malformed(bra, orc):
         assert bra.huffman_decode(lens, osz, esz, pay) == orc.huffman_decode(lens, osz, esz, pay), (osz, esz)
 
 
+def _large_huffman_streams(orc, seed=11):
+    """Streams of many 2048-bit decode segments (more than one 256-segment chain chunk): skewed data
+    (paths rejoin: the chain's parallel chunks, the four-lane segment writes), uniform bytes (equal
+    code lengths keep separate phases: the serial chunks) and both in one stream (the entry carried
+    between the two kinds of chunk), valid and mutated (bit flips in later chunks, truncation,
+    orig_size off by a few)."""
+    rng = np.random.default_rng(seed)
+    skew = rng.geometric(0.18, 700_000).clip(1, 60).astype(np.uint8) + 40
+    unif = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    mixed = np.concatenate([skew[:250_000], unif[:120_000], skew[250_000:500_000]])
+    out = []
+    for data in (skew, unif, mixed):
+        lens, osz, esz, pay = orc.huffman_encode(data.tobytes())
+        assert esz * 8 > 3 * 256 * 2048  # several chain chunks
+        out.append((lens, osz, esz, pay))
+        for frac in (0.1, 0.45, 0.8, 0.97):
+            b = bytearray(pay)
+            k = int(esz * frac)
+            b[k] ^= 1 << int(rng.integers(8))
+            out.append((lens, osz, esz, bytes(b)))
+        out.append((lens, osz, esz // 2, pay[: esz // 2]))
+        out.append((lens, osz + 3, esz, pay))
+        out.append((lens, osz - 1, esz, pay))
+        out.append((lens, osz // 3, esz, pay))
+    return out
+
+
+def test_huffman_decode_large_streams(bra, orc):
+    """Multi-chunk streams, valid and malformed: accept/reject and output as the oracle."""
+    for lens, osz, esz, pay in _large_huffman_streams(orc):
+        assert bra.huffman_decode(lens, osz, esz, pay) == orc.huffman_decode(lens, osz, esz, pay), (osz, esz)
+
+
 @pytest.mark.gpu
 def test_batch_decode_rejects_corruption(bra, codec):
     """A corrupted payload in one block makes the batch decode fail (no silent garbage)."""
