@@ -898,11 +898,13 @@ __global__ void __launch_bounds__(IB_CH_TPB) k_ib_chain3(const IbBlk* __restrict
     }
 }
 
-// Sixteen lanes per hop, four hops per wave: lane l copies source dwords l, l + 16, ... of its
-// hop's slot to the output with unaligned dword stores, so one store instruction writes four
-// contiguous 64-byte stretches (the round-4 lane-per-hop copy stored 4 bytes to each of 64 lines per
-// instruction: bound by the L2 request rate, not by bytes; iBWT 4.86 -> 4.72 ms on 256 x 1 MiB
-// text).  The hop's last partial dword goes byte by byte (the next hop owns the bytes after it).
+// Sixteen lanes per hop, four hops per wave: lane l copies source bytes 16 l, 16 l + 256, ... of
+// its hop's slot to the output with unaligned 16-byte stores, so one store instruction writes four
+// contiguous stretches (the round-4 lane-per-hop copy stored 4 bytes to each of 64 lines per
+// instruction: bound by the L2 request rate, not by bytes).  The first 256 bytes of 8 hops are
+// loaded before any of them is stored (a hop-by-hop loop left every hop's load latency exposed:
+// 0.50 -> 0.28 ms on 256 x 1 MiB text); a hop's partial last 16 bytes go out as at most four
+// narrower stores (the next hop owns the bytes after it).
 typedef uint32_t __attribute__((aligned(1))) u32_u;
 typedef uint4 __attribute__((aligned(1))) u128_u;
 typedef uint64_t __attribute__((aligned(1))) u64_u;
@@ -966,27 +968,6 @@ __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk
                 if (st < B.len)
                     len = min(hop_len[base + q], B.len - st);
             }
-#ifdef BRA_EXP_OLDCOPY
-            for (uint32_t h = 0; h < 16; ++h)
-            {
-                const uint32_t hq = (uint32_t) __shfl((int) q, (int) (g0 + h), 64);
-                const uint32_t hs = (uint32_t) __shfl((int) st, (int) (g0 + h), 64);
-                const uint32_t hl = (uint32_t) __shfl((int) len, (int) (g0 + h), 64);
-                if (hs == 0xFFFFFFFFu || hs >= B.len || hl == 0)
-                    continue;
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(slots + B.tslot + (size_t) hq * cap);
-                const uint32_t  m   = min(hl, cap);
-                uint8_t*        dst = ob + hs;
-                for (uint32_t o = 4 * l; o < m; o += 64)
-                {
-                    const uint32_t v = src[o >> 2];
-                    if (o + 4 <= m)
-                        *reinterpret_cast<u32_u*>(dst + o) = v;
-                    else
-                        for (uint32_t t = 0; o + t < m; ++t)
-                            dst[o + t] = (uint8_t) (v >> (8 * t));
-                }
-#else
             for (uint32_t h0 = 0; h0 < 16; h0 += CP_BATCH)
             {
                 // the first 256 bytes of CP_BATCH hops (a whole slot when S = 64): all loads in
@@ -1024,7 +1005,6 @@ __global__ void __launch_bounds__(256) k_ib_copy16(const IbBlk* __restrict__ blk
                 uint8_t*       dst = ob + hs;
                 for (uint32_t o = 256 + 16 * l; o < m; o += 256)
                     store_head(dst + o, *reinterpret_cast<const uint4*>(src + o), min(m - o, 16u));
-#endif
                 uint32_t c = hl > cap ? hop_ovf[base + hq] : 0xFFFFFFFFu;
                 for (uint32_t o0 = cap; o0 < hl && c < pool_cap; o0 += IB_CHUNK)
                 {

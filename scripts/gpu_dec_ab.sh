@@ -19,3 +19,7 @@ done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 scripts/decode_bench.py text $((1 << 20)) 5 > $O/prof_dec.json 2> $O/prof.err
 echo "prof rc $?"
+if [ "${PMC:-0}" = 1 ]; then
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT -d $O/pmc_sq -o run --output-format csv -- python3 scripts/decode_bench.py text $((1 << 20)) 1 > $O/pmc_sq.log 2>&1
+  echo "pmc sq rc $?"
+fi
