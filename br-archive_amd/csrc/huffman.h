@@ -37,6 +37,8 @@ struct HuffWorkspace
     uint32_t*             tab   = nullptr;
     uint32_t*             trans = nullptr;
     uint32_t*             seg_info = nullptr;
+    uint32_t*             bmbuf    = nullptr;  // per segment: the entry-0 path's boundary bitmap
+    uint32_t*             tflag    = nullptr;  // per task: compute every entry; [ntasks]: the chain's redo flag
     void*                 tasks = nullptr;
     uint32_t              cap_fb = 0, cap_fs = 0, cap_ft = 0;
     std::vector<uint32_t> h_segb;

@@ -1047,7 +1047,7 @@ static_assert(HD2_LMAX + 2 <= HD2_STRD, "the sub records follow the entries' tra
 static_assert(HD2_SEG <= 2048 && HD2_LMAX < 32, "ranks and offsets of the sub records fit 11 + 5 bits");
 
 // table layout (u32 words)
-constexpr uint32_t T_LUT = 0, T_LIM = 2048, T_FIRST = 2112, T_IDX = 2144, T_PERM = 2176, T_INFO = 2240;  // info: lmax, clean
+constexpr uint32_t T_LUT = 0, T_LIM = 2048, T_FIRST = 2112, T_IDX = 2144, T_PERM = 2176, T_INFO = 2240;  // info: lmax, clean, even
 
 struct Hd2Lds
 {
@@ -1064,7 +1064,7 @@ __global__ void __launch_bounds__(256) k_hd_canon(const HuffMetaRec* __restrict_
 {
     __shared__ uint32_t ln[256], cnt[257];
     __shared__ uint64_t lim[32];
-    __shared__ uint32_t first[32], idx[32], sh_lmax, sh_clean;
+    __shared__ uint32_t first[32], idx[32], sh_lmax, sh_clean, sh_even;
     __shared__ __attribute__((aligned(4))) uint8_t perm[256];
     for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x)
     {
@@ -1081,13 +1081,17 @@ __global__ void __launch_bounds__(256) k_hd_canon(const HuffMetaRec* __restrict_
         __syncthreads();
         if (t == 0)
         {
-            uint32_t lmax = 0, nsym = 0;
+            uint32_t lmax = 0, lmin = 0, nsym = 0;
             for (uint32_t l = 1; l <= 255; ++l)
                 if (cnt[l])
                 {
+                    lmin = lmin ? lmin : l;
                     lmax = l;
                     nsym += cnt[l];
                 }
+            // code lengths within 2 of each other (near-uniform data): paths from different entries
+            // keep their phases, so k_hd_trans does not try the guessed entries
+            sh_even = lmax - lmin <= 2 ? 1u : 0u;
             bool     clean = nsym > 0 && lmax <= HD2_LMAX;
             uint64_t code = 0;
             uint32_t id   = 0;
@@ -1150,6 +1154,7 @@ __global__ void __launch_bounds__(256) k_hd_canon(const HuffMetaRec* __restrict_
             {
                 T[T_INFO]     = lmax;
                 T[T_INFO + 1] = 1;
+                T[T_INFO + 2] = sh_even;
             }
         }
         else if (t == 0)
@@ -1264,14 +1269,116 @@ struct Hd2Task
     uint32_t block, seg0;
 };
 
+constexpr uint32_t HD2_UNSET = 0xFFFFFFFFu;  // a transfer word not computed (real words have bits 21-29 clear)
+
+// Walks of entries ea (and eb when `two`) of segment [s, stop) until they end, die or land on a
+// codeword start of the entry-0 path (boundary bitmap bm over its first HD2_REFB bits; r0 / c0:
+// its transfer word without the count, and its count).  Two walks in lockstep: both paths' window
+// loads and LUT reads are issued before either result is used (one path's step is a dependent
+// load chain).
+__device__ __forceinline__ void hd2_walk_entries(const Hd2Lds& L, const uint8_t* payload, uint64_t off, uint32_t nbytes, uint32_t s, uint32_t stop,
+                                                 const uint32_t (&bm)[HD2_REFB / 32], uint32_t r0, uint32_t c0, uint32_t ea, uint32_t eb,
+                                                 bool two, uint32_t& ra, uint32_t& rb, bool give_up = false)
+{
+    const uint32_t nbits = nbytes * 8;
+    BitWin         WA = hd2_win(payload, off, nbytes), WB = hd2_win(payload, off, nbytes);
+    uint32_t       pa = s + ea, pb = s + (two ? eb : ea), ca = 0, cb = 0;
+    bool           la = true, lb = two;
+    ra = rb = 0;
+    WA.init(pa);
+    WB.init(pb);
+    // end / merge checks of one path (registers only)
+    const auto check = [&](uint32_t pq, uint32_t cq, uint32_t& rq, bool& lq) __attribute__((always_inline)) {
+        if (!lq)
+            return;
+        if (pq >= stop)
+        {
+            rq = (((pq - stop) & 31u) << 16) | cq;
+            lq = false;
+            return;
+        }
+        const uint32_t d = pq - s;
+        if (give_up && d >= HD2_REFB)
+        {
+            // past the bitmap the path can no longer join: leave it to HD_REST
+            rq = HD2_UNSET;
+            lq = false;
+            return;
+        }
+        if (d < HD2_REFB)
+        {
+            uint32_t wsel = 0;
+#pragma unroll
+            for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                wsel = (d >> 5) == (uint32_t) i ? bm[i] : wsel;
+            if ((wsel >> (d & 31)) & 1u)
+            {
+                uint32_t rank = 0;
+#pragma unroll
+                for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                {
+                    const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
+                    rank += (uint32_t) __popc(bm[i] & m);
+                }
+                rq = r0 | (cq + c0 - rank);
+                lq = false;
+            }
+        }
+    };
+    const auto advance = [&](uint32_t v, uint32_t le, uint32_t& pq, uint32_t& cq, uint32_t& rq, bool& lq) __attribute__((always_inline)) {
+        if (!lq)
+            return;
+        uint32_t len, sym;
+        if (!hd2_dec_e(L, v, le, len, sym) || len > nbits - pq)
+        {
+            rq = (1u << 31) | (((pq - stop) & 31u) << 16) | cq;
+            lq = false;
+            return;
+        }
+        pq += len;
+        ++cq;
+    };
+    while (la || lb)
+    {
+        check(pa, ca, ra, la);
+        check(pb, cb, rb, lb);
+        const uint32_t va = WA.peek(pa), vb = WB.peek(pb);
+        const uint32_t xa = L.lut[va >> 21], xb = L.lut[vb >> 21];
+        advance(va, xa, pa, ca, ra, la);
+        advance(vb, xb, pb, cb, rb, lb);
+    }
+}
+
+// Transfer words of the segments, in three passes (HD_E0, HD_GUESS, HD_REST):
+//   HD_E0     the entry-0 path of every segment: its word (bit 30: "joined the entry-0 path", trivially),
+//             the sub records, its boundary bitmap over the first HD2_REFB bits (bmbuf), and
+//             HD2_UNSET in the words of the other entries;
+//   HD_GUESS  the entry where the entry-0 path of the segment before leaves it (the true entry
+//             whenever the true path joined its entry-0 path there; k_hd_chain's guess): that one
+//             walk per segment, given up past the bitmap's HD2_REFB bits (it can no longer join).
+//             A guess that does not join marks its task and the next one;
+//   HD_REST   every other entry, for the marked tasks only.
+// Huffman codes of unequal lengths resynchronise within a few codewords, so text-like data needs
+// the first two passes only (text: 1.03 -> 0.62 ms); blocks whose code lengths lie within 2 of
+// each other (uniform bytes: paths keep their phases) walk every entry in HD_E0, as one pass.
+enum : int
+{
+    HD_E0    = 0,
+    HD_GUESS = 1,
+    HD_REST  = 2
+};
+
+template <int MODE>
 __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restrict__ meta, const uint8_t* __restrict__ payload,
                                                       const uint64_t* __restrict__ payload_off, const uint32_t* __restrict__ tab,
                                                       const Hd2Task* __restrict__ tasks, uint32_t ntasks, const uint32_t* __restrict__ seg_base,
-                                                      uint32_t* __restrict__ trans)
+                                                      uint32_t* __restrict__ trans, uint32_t* __restrict__ bmbuf, uint32_t* __restrict__ tflag)
 {
     __shared__ Hd2Lds L;
     for (uint32_t tk = blockIdx.x; tk < ntasks; tk += gridDim.x)
     {
+        if (MODE == HD_REST && tflag[tk] == 0)
+            continue;  // uniform over the workgroup
         const Hd2Task  K = tasks[tk];
         const uint32_t b = K.block;
         __syncthreads();
@@ -1280,114 +1387,114 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
         const uint32_t j = K.seg0 + threadIdx.x, g0 = seg_base[b], ns = seg_base[b + 1] - g0;
         if (j >= ns)
             continue;
-        BitWin         W = hd2_win(payload, payload_off[b], nbytes);
         const uint32_t s = j * HD2_SEG, stop = min(s + HD2_SEG, nbits), nent = j == 0 ? 1u : L.lmax;
         uint32_t*      out = trans + (size_t) (g0 + j) * HD2_STRD;
-        // the reference path from entry 0, recording its boundaries over the first HD2_REFB bits
-        uint32_t bm[HD2_REFB / 32];
-#pragma unroll
-        for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
-            bm[i] = 0;
-        W.init(s);
-        uint32_t p = s, c = 0, bad = 0, len, sym;
-        // the path's first codeword at or after bits HD2_SUB, 2 HD2_SUB, 3 HD2_SUB: (offset past the
-        // mark << 11) | rank, 0xFFFF when the path ends before (k_hd_write2 starts its sub-segment
-        // lanes there)
-        uint32_t mark = HD2_SUB, sub1 = 0xFFFFu, sub2 = 0xFFFFu, sub3 = 0xFFFFu;
-        while (p < stop)
+        uint4*         bmo = reinterpret_cast<uint4*>(bmbuf + (size_t) (g0 + j) * (HD2_REFB / 32));
+        uint32_t       bm[HD2_REFB / 32];
+        if (MODE == HD_E0)
         {
-            const uint32_t d = p - s;
-            if (d < HD2_REFB)
-            {
+            // the reference path from entry 0, recording its boundaries over the first HD2_REFB bits
 #pragma unroll
-                for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
-                    if ((d >> 5) == (uint32_t) i)
-                        bm[i] |= 1u << (d & 31);
-            }
-            if (d >= mark)
+            for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                bm[i] = 0;
+            BitWin W = hd2_win(payload, payload_off[b], nbytes);
+            W.init(s);
+            uint32_t p = s, c = 0, bad = 0, len, sym;
+            // the path's first codeword at or after bits HD2_SUB, 2 HD2_SUB, 3 HD2_SUB: (offset past
+            // the mark << 11) | rank, 0xFFFF when the path ends before (k_hd_write2 starts its
+            // sub-segment lanes there)
+            uint32_t mark = HD2_SUB, sub1 = 0xFFFFu, sub2 = 0xFFFFu, sub3 = 0xFFFFu;
+            while (p < stop)
             {
-                const uint32_t rec = ((d - mark) << 11) | c;
-                sub1 = mark == HD2_SUB ? rec : sub1;
-                sub2 = mark == 2 * HD2_SUB ? rec : sub2;
-                sub3 = mark == 3 * HD2_SUB ? rec : sub3;
-                mark += HD2_SUB;
+                const uint32_t d = p - s;
+                if (d < HD2_REFB)
+                {
+#pragma unroll
+                    for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
+                        if ((d >> 5) == (uint32_t) i)
+                            bm[i] |= 1u << (d & 31);
+                }
+                if (d >= mark)
+                {
+                    const uint32_t rec = ((d - mark) << 11) | c;
+                    sub1               = mark == HD2_SUB ? rec : sub1;
+                    sub2               = mark == 2 * HD2_SUB ? rec : sub2;
+                    sub3               = mark == 3 * HD2_SUB ? rec : sub3;
+                    mark += HD2_SUB;
+                }
+                if (!hd2_dec(L, W.peek(p), len, sym) || len > nbits - p)
+                {
+                    bad = 1;
+                    break;
+                }
+                p += len;
+                ++c;
             }
-            if (!hd2_dec(L, W.peek(p), len, sym) || len > nbits - p)
+            // bit 30: the path joins the entry-0 path (so k_hd_write2 may split it at the sub records)
+            const uint32_t w0 = (bad << 31) | (1u << 30) | (((p - stop) & 31u) << 16) | c;
+            uint4*         o4 = reinterpret_cast<uint4*>(out);
+            o4[0]             = make_uint4(w0, HD2_UNSET, HD2_UNSET, HD2_UNSET);
+#pragma unroll
+            for (int i = 1; i < (int) (HD2_STRD / 4) - 1; ++i)
+                o4[i] = make_uint4(HD2_UNSET, HD2_UNSET, HD2_UNSET, HD2_UNSET);
+            o4[HD2_STRD / 4 - 1] = make_uint4(HD2_UNSET, HD2_UNSET, sub1 | sub2 << 16, sub3);
+#pragma unroll
+            for (int i = 0; i < (int) (HD2_REFB / 128); ++i)
+                bmo[i] = make_uint4(bm[4 * i], bm[4 * i + 1], bm[4 * i + 2], bm[4 * i + 3]);
+            if (tab[(size_t) b * HD2_TAB + T_INFO + 2])
             {
-                bad = 1;
-                break;
+                // near-uniform code lengths: no guessing, every entry here (the bitmap in registers)
+                for (uint32_t e = 1; e < nent; e += 2)
+                {
+                    const bool two = e + 1 < nent;
+                    uint32_t   ra, rb;
+                    hd2_walk_entries(L, payload, payload_off[b], nbytes, s, stop, bm, w0 & ~0xFFFFu, w0 & 0xFFFFu, e, e + 1, two, ra, rb);
+                    out[e] = ra;
+                    if (two)
+                        out[e + 1] = rb;
+                }
             }
-            p += len;
-            ++c;
+            continue;
         }
-        // bit 30: the path joins the entry-0 path (so k_hd_write2 may split it at the sub records)
-        const uint32_t c0 = c, r0 = (bad << 31) | (1u << 30) | (((p - stop) & 31u) << 16);
-        out[0]               = r0 | c0;
-        out[HD2_STRD - 2]    = sub1 | sub2 << 16;
-        out[HD2_STRD - 1]    = sub3;
-        // the other entries two at a time in lockstep: both paths' window loads and LUT reads are
-        // issued before either result is used (one path's step is a dependent load chain)
+        // HD_GUESS / HD_REST: the entry-0 path's records
+        const uint32_t w0 = out[0], c0 = w0 & 0xFFFFu, r0 = w0 & ~0xFFFFu;
+        uint32_t       eg = 0;
+        if (MODE == HD_GUESS)
+        {
+            if (tab[(size_t) b * HD2_TAB + T_INFO + 2])
+                continue;  // near-uniform code lengths: HD_E0 walked every entry
+            if (j == 0)
+                continue;
+            eg = (trans[(size_t) (g0 + j - 1) * HD2_STRD] >> 16) & 31u;
+            if (eg == 0 || eg >= nent)
+                continue;  // entry 0: its word is there; >= lmax cannot happen (left unset)
+        }
+#pragma unroll
+        for (int i = 0; i < (int) (HD2_REFB / 128); ++i)
+        {
+            const uint4 v = bmo[i];
+            bm[4 * i] = v.x, bm[4 * i + 1] = v.y, bm[4 * i + 2] = v.z, bm[4 * i + 3] = v.w;
+        }
+        if (MODE == HD_GUESS)
+        {
+            uint32_t r, unused;
+            hd2_walk_entries(L, payload, payload_off[b], nbytes, s, stop, bm, r0, c0, eg, eg, false, r, unused, true);
+            out[eg] = r;
+            // (an unjoined word in the block's last segment is the true one all the same: no next
+            // segment can be entered off the guess)
+            if (r == HD2_UNSET || (!((r >> 30) & 1u) && j + 1 < ns))
+            {
+                tflag[tk] = 1;  // benign race: every writer stores 1
+                if (tk + 1 < ntasks)
+                    tflag[tk + 1] = 1;  // its first segment may be entered off the guess
+            }
+            continue;
+        }
         for (uint32_t e = 1; e < nent; e += 2)
         {
             const bool two = e + 1 < nent;
-            BitWin     WA = hd2_win(payload, payload_off[b], nbytes), WB = hd2_win(payload, payload_off[b], nbytes);
-            uint32_t   pa = s + e, pb = s + (two ? e + 1 : e), ca = 0, cb = 0, ra = 0, rb = 0;
-            bool       la = true, lb = two;
-            WA.init(pa);
-            WB.init(pb);
-            // end / merge checks of one path (registers only)
-            const auto check = [&](uint32_t pq, uint32_t cq, uint32_t& rq, bool& lq) __attribute__((always_inline)) {
-                if (!lq)
-                    return;
-                if (pq >= stop)
-                {
-                    rq = (((pq - stop) & 31u) << 16) | cq;
-                    lq = false;
-                    return;
-                }
-                const uint32_t d = pq - s;
-                if (d < HD2_REFB)
-                {
-                    uint32_t wsel = 0;
-#pragma unroll
-                    for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
-                        wsel = (d >> 5) == (uint32_t) i ? bm[i] : wsel;
-                    if ((wsel >> (d & 31)) & 1u)
-                    {
-                        uint32_t rank = 0;
-#pragma unroll
-                        for (int i = 0; i < (int) (HD2_REFB / 32); ++i)
-                        {
-                            const uint32_t m = (d >> 5) == (uint32_t) i ? ((1u << (d & 31)) - 1u) : ((d >> 5) > (uint32_t) i ? 0xFFFFFFFFu : 0u);
-                            rank += (uint32_t) __popc(bm[i] & m);
-                        }
-                        rq = r0 | (cq + c0 - rank);
-                        lq = false;
-                    }
-                }
-            };
-            const auto advance = [&](uint32_t v, uint32_t le, uint32_t& pq, uint32_t& cq, uint32_t& rq, bool& lq) __attribute__((always_inline)) {
-                if (!lq)
-                    return;
-                uint32_t len, sym;
-                if (!hd2_dec_e(L, v, le, len, sym) || len > nbits - pq)
-                {
-                    rq = (1u << 31) | (((pq - stop) & 31u) << 16) | cq;
-                    lq = false;
-                    return;
-                }
-                pq += len;
-                ++cq;
-            };
-            while (la || lb)
-            {
-                check(pa, ca, ra, la);
-                check(pb, cb, rb, lb);
-                const uint32_t va = WA.peek(pa), vb = WB.peek(pb);
-                const uint32_t ea = L.lut[va >> 21], eb = L.lut[vb >> 21];
-                advance(va, ea, pa, ca, ra, la);
-                advance(vb, eb, pb, cb, rb, lb);
-            }
+            uint32_t   ra, rb;
+            hd2_walk_entries(L, payload, payload_off[b], nbytes, s, stop, bm, r0, c0, e, e + 1, two, ra, rb);
             out[e] = ra;
             if (two)
                 out[e + 1] = rb;
@@ -1397,16 +1504,18 @@ __global__ void __launch_bounds__(HD2_TPB) k_hd_trans(const HuffMetaRec* __restr
 
 // Per block: the true path from segment to segment, 256 segments at a time.  Guess: segment k is
 // entered where the entry-0 path of segment k - 1 leaves it.  That holds whenever the true path of
-// k - 1 joined its entry-0 path (bit 30), so if every guessed word of the chunk has bit 30 (the
-// chunk's first segment is entered where the chunk before left), the guesses are the true path by
-// induction and the chunk's offsets are one prefix sum -- Huffman codes of unequal lengths
-// resynchronise within a few codewords, so text and skewed data take this path.  Otherwise (codes
-// of near-equal lengths keep separate phases) one lane walks the chunk serially.  Either way the
-// result is the reference's sequential walk: offsets up to orig_size, nothing after the first
-// death, fail when the path dies before symbol orig_size.
+// k - 1 joined its entry-0 path (bit 30), so if every guessed word of the chunk but the last has
+// bit 30 (the chunk's first segment is entered where the chunk before left), the guesses are the
+// true path by induction and the chunk's offsets are one prefix sum -- Huffman codes of unequal
+// lengths resynchronise within a few codewords, so text and skewed data take this path.
+// Otherwise (codes of near-equal lengths keep separate phases) one lane walks the chunk serially;
+// a word it needs that k_hd_trans left unset sets *redo (the host reruns the batch with every
+// entry).  Either way the result is the reference's sequential walk: offsets up to orig_size,
+// nothing after the first death, fail when the path dies before symbol orig_size.
 constexpr uint32_t HD2_CTPB = 256;
 __global__ void __launch_bounds__(HD2_CTPB) k_hd_chain(const HuffMetaRec* __restrict__ meta, uint32_t nblocks, const uint32_t* __restrict__ seg_base,
-                                                       const uint32_t* __restrict__ trans, uint32_t* __restrict__ seg_info, uint32_t* __restrict__ status)
+                                                       const uint32_t* __restrict__ trans, uint32_t* __restrict__ seg_info, uint32_t* __restrict__ status,
+                                                       uint32_t* __restrict__ redo)
 {
     __shared__ uint32_t rows[HD2_CTPB * HD2_STRD];
     __shared__ uint32_t wsum[HD2_CTPB / 64], wdead[HD2_CTPB / 64], sh_e, sh_acc, sh_done, sh_fail, sh_all;
@@ -1436,7 +1545,9 @@ __global__ void __launch_bounds__(HD2_CTPB) k_hd_chain(const HuffMetaRec* __rest
                 g    = t == 0 ? e0 : (rows[(t - 1) * HD2_STRD] >> 16) & 31u;
                 word = rows[t * HD2_STRD + g];
                 cnt  = word & 0xFFFFu;
-                if (!((word >> 30) & 1u))
+                // the last word of the chunk need not have joined: the next chunk starts from its
+                // exit, carried in sh_e
+                if (word == HD2_UNSET || (!((word >> 30) & 1u) && t + 1 < nr))
                     sh_all = 0;  // benign race: every writer stores 0
             }
             // inclusive prefix of the counts and of the death flags over the chunk
@@ -1488,13 +1599,16 @@ __global__ void __launch_bounds__(HD2_CTPB) k_hd_chain(const HuffMetaRec* __rest
             }
             else if (t == 0)
             {
-                uint32_t e = e0, acc = acc0, done = 0, fail = 0;
+                uint32_t e = e0, acc = acc0, done = 0, fail = 0, unset = 0;
                 for (uint32_t k = 0; k < nr; ++k)
                 {
                     uint32_t info = 0xFFFFFFFFu;
                     if (!done && acc < osz)
                     {
                         const uint32_t r = rows[k * HD2_STRD + e], cnt = r & 0xFFFFu;
+                        // a word k_hd_trans left unset (HD_REST skipped the task): the walk goes on
+                        // with garbage inside the row and the host reruns the batch with every entry
+                        unset |= r == HD2_UNSET ? 1u : 0u;
                         info             = (e << 27) | acc;
                         if (r >> 31)
                         {
@@ -1510,6 +1624,8 @@ __global__ void __launch_bounds__(HD2_CTPB) k_hd_chain(const HuffMetaRec* __rest
                 sh_e = e, sh_acc = acc, sh_done = done;
                 if (fail)
                     sh_fail = 1;
+                if (unset)
+                    *redo = 1;
             }
         }
         __syncthreads();
@@ -1748,6 +1864,8 @@ void HuffWorkspace::release()
     (void) hipFree(tab);
     (void) hipFree(trans);
     (void) hipFree(seg_info);
+    (void) hipFree(bmbuf);
+    (void) hipFree(tflag);
     (void) hipFree(tasks);
     *this = HuffWorkspace{};
 }
@@ -1873,6 +1991,15 @@ static bool huff_decode_tree(HuffWorkspace& w, const HuffMetaRec* d_meta, const 
     return true;
 }
 
+// Test hook (tests/test_gpu_parity.py): BRA_HD_TEST_UNMARK=1 clears the task marks of the
+// guessing pass, so every true path that leaves the guesses meets unset words in the chain and the
+// batch takes the rerun with every entry.  Read per call.
+static bool hd_test_unmark()
+{
+    const char* e = getenv("BRA_HD_TEST_UNMARK");
+    return e && e[0] == '1';
+}
+
 bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint32_t* h_encoded_size, uint32_t nblocks, const uint8_t* d_payload,
                         const uint64_t* d_payload_off, uint8_t* d_out, const uint64_t* d_out_base, uint32_t* d_status, hipStream_t s)
 {
@@ -1918,11 +2045,35 @@ bool huff_decode_device(HuffWorkspace& w, const HuffMetaRec* d_meta, const uint3
                 hb += h_encoded_size[b];
             prof_bytes(P_DEC_HD_TRANS, hb);
         }
-        hipLaunchKernelGGL(k_hd_trans, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
-                           w.seg_base, w.trans);
+        const dim3 g(std::min<uint32_t>(nt, 65535));
+        BRA_HIP_CHECK(hipMemsetAsync(w.tflag, 0, (size_t) (nt + 1) * 4, s));
+        hipLaunchKernelGGL(k_hd_trans<HD_E0>, g, dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt, w.seg_base, w.trans, w.bmbuf,
+                           w.tflag);
+        hipLaunchKernelGGL(k_hd_trans<HD_GUESS>, g, dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt, w.seg_base, w.trans,
+                           w.bmbuf, w.tflag);
+        if (hd_test_unmark())
+            BRA_HIP_CHECK(hipMemsetAsync(w.tflag, 0, (size_t) nt * 4, s));
+        hipLaunchKernelGGL(k_hd_trans<HD_REST>, g, dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt, w.seg_base, w.trans,
+                           w.bmbuf, w.tflag);
     }
     hipLaunchKernelGGL(k_hd_chain, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(HD2_CTPB), 0, s, d_meta, nblocks, w.seg_base, w.trans, w.seg_info,
-                       d_status);
+                       d_status, nt ? w.tflag + nt : w.flag);  // no task: no segment, the flag is never written
+    *w.h_flag = 0;
+    if (nt)
+    {
+        BRA_HIP_CHECK(hipMemcpyAsync(w.h_flag, w.tflag + nt, 4, hipMemcpyDeviceToHost, s));
+        BRA_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    if (*w.h_flag)
+    {
+        // a true path left the guessed entries where HD_REST had not run: every entry, then the chain again
+        BRA_HIP_CHECK(hipMemsetAsync(w.tflag, 1, (size_t) nt * 4, s));
+        BRA_HIP_CHECK(hipMemsetAsync(w.tflag + nt, 0, 4, s));
+        hipLaunchKernelGGL(k_hd_trans<HD_REST>, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_TPB), 0, s, d_meta, d_payload, d_payload_off, w.tab,
+                           dt, nt, w.seg_base, w.trans, w.bmbuf, w.tflag);
+        hipLaunchKernelGGL(k_hd_chain, dim3(std::min<uint32_t>(nblocks, 65535)), dim3(HD2_CTPB), 0, s, d_meta, nblocks, w.seg_base, w.trans,
+                           w.seg_info, d_status, w.tflag + nt);
+    }
     if (nt)
         hipLaunchKernelGGL(k_hd_write2, dim3(std::min<uint32_t>(nt, 65535)), dim3(HD2_WTPB), 0, s, d_meta, d_payload, d_payload_off, w.tab, dt, nt,
                            w.seg_base, w.trans, w.seg_info, d_status, d_out, d_out_base, w.end_pos);
@@ -1946,7 +2097,7 @@ bool HuffWorkspace::reserve_fast(uint32_t nblocks, uint32_t nseg, uint32_t ntask
     {
         cap_fs           = 0;
         const uint32_t c = nseg + nseg / 4 + 256;
-        if (!dev_alloc(trans, (uint64_t) c * HD2_STRD) || !dev_alloc(seg_info, c))
+        if (!dev_alloc(trans, (uint64_t) c * HD2_STRD) || !dev_alloc(seg_info, c) || !dev_alloc(bmbuf, (uint64_t) c * (HD2_REFB / 32)))
             return false;
         cap_fs = c;
     }
@@ -1954,7 +2105,7 @@ bool HuffWorkspace::reserve_fast(uint32_t nblocks, uint32_t nseg, uint32_t ntask
     {
         cap_ft           = 0;
         const uint32_t c = ntasks + ntasks / 4 + 64;
-        if (!dev_alloc_bytes(tasks, (uint64_t) c * sizeof(Hd2Task)))
+        if (!dev_alloc_bytes(tasks, (uint64_t) c * sizeof(Hd2Task)) || !dev_alloc(tflag, (uint64_t) c + 1))
             return false;
         cap_ft = c;
     }

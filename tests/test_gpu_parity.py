@@ -410,6 +410,15 @@ def test_huffman_decode_large_streams(bra, orc):
         assert bra.huffman_decode(lens, osz, esz, pay) == orc.huffman_decode(lens, osz, esz, pay), (osz, esz)
 
 
+def test_huffman_decode_rerun_with_every_entry(bra, orc, monkeypatch):
+    """With the guessing pass's task marks cleared (test hook), every true path that leaves the
+    guessed entries meets an unset transfer word in the chain, which makes the decode rerun the
+    batch with every entry: same output and verdicts as the oracle."""
+    monkeypatch.setenv("BRA_HD_TEST_UNMARK", "1")
+    for lens, osz, esz, pay in _large_huffman_streams(orc, seed=12):
+        assert bra.huffman_decode(lens, osz, esz, pay) == orc.huffman_decode(lens, osz, esz, pay), (osz, esz)
+
+
 @pytest.mark.gpu
 def test_batch_decode_rejects_corruption(bra, codec):
     """A corrupted payload in one block makes the batch decode fail (no silent garbage)."""
