@@ -419,6 +419,21 @@ def test_huffman_decode_rerun_with_every_entry(bra, orc, monkeypatch):
         assert bra.huffman_decode(lens, osz, esz, pay) == orc.huffman_decode(lens, osz, esz, pay), (osz, esz)
 
 
+def test_batch_decode_mixed_phases(bra, codec, orc, monkeypatch):
+    """Blocks half text, half uniform bytes (wide code lengths, so the guessing pass runs, and its
+    guesses do not rejoin in the uniform half) beside plain text and uniform blocks in one batch:
+    every block against the oracle and the round trip, once as is and once with the guessing
+    pass's task marks cleared (the chain meets unset words and the batch reruns with every entry)."""
+    rng = np.random.default_rng(77)
+    bs = 1 << 20
+    half = [np.concatenate([bra.synth_fill(0, bs // 2, bs // 2, first_block=3 + i), rng.integers(0, 256, bs // 2, dtype=np.uint8)])
+            for i in range(2)]
+    data = np.concatenate([half[0], bra.synth_fill(0, bs, bs, first_block=5), rng.integers(0, 256, bs, dtype=np.uint8), half[1]])
+    _encode_check(bra, codec, orc, data, bs)
+    monkeypatch.setenv("BRA_HD_TEST_UNMARK", "1")
+    _encode_check(bra, codec, orc, data, bs)
+
+
 @pytest.mark.gpu
 def test_batch_decode_rejects_corruption(bra, codec):
     """A corrupted payload in one block makes the batch decode fail (no silent garbage)."""
